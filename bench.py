@@ -1,0 +1,200 @@
+"""Benchmark: Mrays/s + ms/frame of the trace worker on suzanne.obj 1920x1080.
+
+A "step" is one full frame of tracer.Trace semantics over example/scene.json
+(BASELINE.json configs[1]): primary ray per pixel, one shadow ray per light per hit
+(3 lights), Phong, uint8 packing — everything worker/sequential's draw loop does per
+frame.  Inputs (mesh, frame params) are resident on the GPU before timing; outputs stay
+in HBM.  With N GPUs (torchrun, one process per GPU) the same frame is split into
+interleaved 64x64 tiles and the packed tiles are gathered to rank 0 over RCCL and
+unpacked into the framebuffer inside the timed region (strong scaling: total work is
+one frame whatever N is).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).  Fields beyond the
+contract: primary_mrays_s, rays_per_frame, hits, ms_kernels, parity.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+SCENE = os.path.join(ROOT, "tests", "golden", "example", "scene.json")
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"] if os.path.exists(
+    os.path.join(ROOT, "BASELINE.json")) else "Mrays/sec + ms/frame, suzanne.obj 1920x1080"
+BYTES_PER_TRI_TEST = 72  # fp64 P1, E1, E2 read per ray-triangle test
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec, vector FP64 (FMA = 2 flops)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--scene", default=SCENE)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                    help="per-launch HBM bytes of k_primary from a rocprofv3 --pmc pass (see profiles/)")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
+    """The oracle's faithful variant (R-tree culling like rtreego, 1 thread, fp64,
+    worker/sequential's serial i/j loop) timed on this host over the full frame."""
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    orc = Oracle(load_scene(scene_path), use_rtree=True)
+    t0 = time.perf_counter()
+    r = orc.frame(W, H, nthreads=1)
+    dt = time.perf_counter() - t0
+    rays = r["stats"]["primary_rays"] + r["stats"]["shadow_rays"]
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"one full {W}x{H} frame ({rays} primary+shadow rays), oracle/rt_oracle.c with "
+                      f"rtreego-style R-tree culling, single thread, {dt:.2f} s",
+            "ms_per_frame": round(dt * 1e3, 1)}
+
+
+def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int) -> dict:
+    """Bounded check of the timed frame: every 64th column vs the oracle (bit-exact)."""
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    cols = list(range(5, W, 64))
+    ref = Oracle(load_scene(scene_path)).trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=8)
+    sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
+    ok = bool(np.array_equal(fb_valid[sub], ref["valid"]) and np.array_equal(fb_rgb8[sub], ref["rgb8"]))
+    return {"columns_checked": len(cols), "bit_exact": ok, "hits": int(fb_valid.sum())}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import FrameSharder
+
+    W, H = a.width, a.height
+    ctx = rt.Context(local)
+    if a.no_prefilter:
+        ctx.set_options(rt._lib.MIRT_OPT_NO_PREFILTER)
+    env = rt.Environment.from_file(a.scene, ctx)
+    frame = env.mutable().to_frame()
+    tris = sum(len(m.face_v) for m in env.meshes)
+    nl = len(env.mutable().lights)
+    sh = FrameSharder(ctx, W, H, rank, world, a.tile)
+    dev = torch.device("cuda", local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    for _ in range(a.warmup):
+        sh.render(frame)
+    torch.cuda.synchronize(dev)
+
+    ctx.profile_enable(True)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sh.render(frame)
+    torch.cuda.synchronize(dev)
+    barrier()
+    t1 = time.perf_counter()
+    ctx.profile_enable(False)
+    prof = ctx.profile_read()
+
+    elapsed = t1 - t0
+    counts = torch.tensor([elapsed, float(prof["primary_rays"]), float(prof["shadow_rays"]), float(prof["hits"])],
+                          dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = counts[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        sums = counts[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax.item())
+        primary, shadow, hits = (float(x) for x in sums.tolist())
+    else:
+        primary, shadow, hits = float(prof["primary_rays"]), float(prof["shadow_rays"]), float(prof["hits"])
+
+    if rank == 0:
+        steps = a.steps
+        ms = elapsed / steps * 1e3
+        rays_per_frame = (primary + shadow) / steps
+        launches = max(prof["launches"], 1)
+        prim_ms = prof["primary_ms_sum"] / launches
+        prim_tests = prof["primary_tri_tests"] / launches
+        achieved = prim_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                tj = json.load(open(a.traffic_json))
+                if tj.get("width") == W and tj.get("height") == H and tj.get("gpus", 1) == world:
+                    traffic = tj.get("k_primary_hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), static frame-0 camera",
+            "config": {"workload": f"suzanne.obj {W}x{H}, primary + one shadow ray per light (3) + Phong "
+                                   f"(BASELINE configs[1])", "width": W, "height": H, "triangles": tris,
+                       "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
+                                                                                if world > 1 else "")},
+            "primary_mrays_s": round(primary / steps / (ms / 1e3) / 1e6, 3),
+            "rays_per_frame": int(rays_per_frame),
+            "hits_per_frame": int(hits / steps),
+            "ms_kernels": {"primary": round(prim_ms, 4),
+                           "shadow": round(prof["shadow_ms_sum"] / launches, 4),
+                           "shade": round(prof["shade_ms_sum"] / launches, 4),
+                           "frame_device": round(prof["frame_ms_sum"] / launches, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_primary", "bytes_per_unit": BYTES_PER_TRI_TEST,
+                         "units_per_launch": int(prim_tests),
+                         "note": "algorithmic bytes (72 B fp64 triangle record per ray-triangle test); the mesh is "
+                                 "LDS-resident so the real bound is fp64 VALU, see DESIGN.md"},
+        }
+        if not a.no_parity:
+            fr = sh.frame
+            line["parity"] = parity_check(fr.valid.cpu().numpy(), fr.rgb8.cpu().numpy(), a.scene, W, H)
+        if not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(a.scene, W, H)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

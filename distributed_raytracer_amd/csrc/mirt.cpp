@@ -1,0 +1,719 @@
+// mirt.cpp — host side of libmirt.so: context, mesh upload, per-call slots, launches.
+//
+// Re-entrancy: gRPC serves each BulkTrace in its own goroutine, so any
+// number of threads may call mirt_trace_* concurrently on one context with different
+// frames.  Each call takes a "slot" (HIP stream + workspace + events) from a pool under
+// a mutex and returns it afterwards; meshes are immutable after upload.  hipSetDevice is
+// called on every entry because cgo calls can land on any OS thread.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mirt.h"
+#include "gomath.hpp"
+#include "mirt_internal.hpp"
+
+using namespace mirt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(MIRT_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+struct MeshDev {
+    double* tri = nullptr;
+    double* vnrm = nullptr;
+    uint32_t* fmat = nullptr;
+    double* mats = nullptr;
+    uint32_t ntri = 0, nmat = 0;
+    bool has_normals = false;
+    bool live = false;
+};
+
+// Device workspace of one in-flight call.
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    HitRec* hits = nullptr;
+    size_t hits_cap = 0;
+    uint8_t* lit = nullptr;
+    size_t lit_cap = 0;
+    uint32_t* counters = nullptr;
+    TileDesc* d_tiles = nullptr;
+    TileDesc* h_tiles = nullptr;  // pinned staging
+    size_t tiles_cap = 0, h_tiles_cap = 0;
+    uint32_t* h_counters = nullptr;  // pinned
+    // device-side outputs for the host-buffer API
+    void* out_buf = nullptr;
+    size_t out_cap = 0;
+};
+
+struct ProfRec {
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t* h_hits = nullptr;  // pinned, written by an async D2H copy
+    uint64_t pixels = 0, tris = 0, nl = 0;
+};
+
+}  // namespace
+
+struct mirt_ctx {
+    int device = 0;
+    int cus = 256;
+    std::mutex mu;
+    std::vector<MeshDev> meshes;
+    std::vector<std::unique_ptr<Slot>> slots;
+    std::vector<Slot*> free_slots;
+    uint32_t flags = 0;
+    bool profiling = false;
+    std::vector<ProfRec> prof_pending;
+    std::vector<ProfRec> prof_free;
+};
+
+namespace {
+
+template <class T>
+int dev_grow(T*& p, size_t& cap, size_t need) {
+    if (need <= cap) return MIRT_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t n = std::max(need, (size_t)1);
+    hipError_t e = hipMalloc((void**)&p, n * sizeof(T));
+    if (e != hipSuccess) return fail(MIRT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    cap = n;
+    return MIRT_OK;
+}
+
+int slot_acquire(mirt_ctx* c, Slot*& out) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->free_slots.empty()) {
+            out = c->free_slots.back();
+            c->free_slots.pop_back();
+        } else {
+            c->slots.emplace_back(new Slot());
+            out = c->slots.back().get();
+        }
+    }
+    Slot* s = out;
+    if (!s->stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+        HIP_TRY(hipMalloc((void**)&s->counters, kCntN * sizeof(uint32_t)));
+        HIP_TRY(hipHostMalloc((void**)&s->h_counters, kCntN * sizeof(uint32_t)));
+    }
+    // previous asynchronous use of this slot's staging/workspace must be finished
+    if (s->pending) {
+        HIP_TRY(hipEventSynchronize(s->done));
+        s->pending = false;
+    }
+    return MIRT_OK;
+}
+
+// Device + pinned host tile descriptors, grow-only (the slot is idle when this runs).
+int tiles_grow(Slot* sl, uint32_t n) {
+    int r = dev_grow(sl->d_tiles, sl->tiles_cap, n);
+    if (r != MIRT_OK) return r;
+    if (sl->h_tiles_cap < n) {
+        if (sl->h_tiles) (void)hipHostFree(sl->h_tiles);
+        sl->h_tiles = nullptr;
+        sl->h_tiles_cap = 0;
+        size_t cap = std::max<size_t>(n, 64);
+        HIP_TRY(hipHostMalloc((void**)&sl->h_tiles, sizeof(TileDesc) * cap));
+        sl->h_tiles_cap = cap;
+    }
+    return MIRT_OK;
+}
+
+void slot_release(mirt_ctx* c, Slot* s) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->free_slots.push_back(s);
+}
+
+struct SlotGuard {
+    mirt_ctx* c;
+    Slot* s;
+    ~SlotGuard() {
+        if (s) slot_release(c, s);
+    }
+};
+
+int check_frame(const mirt_ctx* c, const mirt_frame* f) {
+    if (!f) return fail(MIRT_E_INVALID, "frame is NULL");
+    if (f->n_objects > MIRT_MAX_OBJECTS)
+        return fail(MIRT_E_LIMIT, "n_objects > MIRT_MAX_OBJECTS (" + std::to_string(MIRT_MAX_OBJECTS) + ")");
+    if (f->n_lights > MIRT_MAX_LIGHTS)
+        return fail(MIRT_E_LIMIT, "n_lights > MIRT_MAX_LIGHTS (" + std::to_string(MIRT_MAX_LIGHTS) + ")");
+    if (f->n_objects && !f->objects) return fail(MIRT_E_INVALID, "objects is NULL");
+    if (f->n_lights && !f->lights) return fail(MIRT_E_INVALID, "lights is NULL");
+    for (uint32_t i = 0; i < f->n_objects; ++i) {
+        uint32_t id = f->objects[i].mesh_id;
+        if (id >= c->meshes.size() || !c->meshes[id].live)
+            return fail(MIRT_E_INVALID, "object " + std::to_string(i) + " names unknown mesh id " + std::to_string(id));
+    }
+    return MIRT_OK;
+}
+
+void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, FrameArgs& fa, uint64_t& tris) {
+    memset(&fa, 0, sizeof(fa));
+    const mirt_camera& cam = f->camera;
+    for (int k = 0; k < 3; ++k) {
+        fa.cam[k] = cam.pos[k];
+        fa.fwd[k] = cam.forward[k];
+        fa.left[k] = cam.left[k];
+        fa.up[k] = cam.up[k];
+    }
+    // tracer.go:16-18: halfWidth, halfHeight := width/2, height/2 (integer division);
+    // projHalfHeight := projHalfWidth * float64(height) / float64(width)
+    fa.phw = cam.proj_half_width;
+    fa.phh = fa.phw * (double)H / (double)W;
+    fa.W = (int32_t)W;
+    fa.H = (int32_t)H;
+    fa.halfW = (int32_t)(W / 2);
+    fa.halfH = (int32_t)(H / 2);
+    fa.n_objects = f->n_objects;
+    fa.n_lights = f->n_lights;
+    tris = 0;
+    for (uint32_t i = 0; i < f->n_objects; ++i) {
+        const MeshDev& m = c->meshes[f->objects[i].mesh_id];
+        DevObject& o = fa.obj[i];
+        o.m.tri = m.tri;
+        o.m.vnrm = m.vnrm;
+        o.m.fmat = m.fmat;
+        o.m.mats = m.mats;
+        o.m.ntri = m.ntri;
+        o.m.has_normals = m.has_normals ? 1u : 0u;
+        for (int k = 0; k < 3; ++k) o.pos[k] = f->objects[i].pos[k];
+        tris += m.ntri;
+    }
+    for (uint32_t l = 0; l < f->n_lights; ++l)
+        for (int k = 0; k < 3; ++k) {
+            fa.lpos[l][k] = f->lights[l].pos[k];
+            fa.lcol[l][k] = f->lights[l].col[k];
+        }
+}
+
+int prof_get(mirt_ctx* c, ProfRec& r) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->prof_free.empty()) {
+        r = c->prof_free.back();
+        c->prof_free.pop_back();
+        return MIRT_OK;
+    }
+    for (int k = 0; k < 4; ++k) HIP_TRY(hipEventCreate(&r.ev[k]));
+    HIP_TRY(hipHostMalloc((void**)&r.h_hits, sizeof(uint32_t)));
+    return MIRT_OK;
+}
+
+// Enqueue primary -> shadow -> shade for a tile list on stream s.
+int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
+                  uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel, uint64_t* pixels_out,
+                  uint64_t* tris_out) {
+    if (W == 0 || H == 0) return fail(MIRT_E_INVALID, "screen width/height must be > 0");
+    if (n == 0 || !tiles) return fail(MIRT_E_INVALID, "empty tile list");
+    uint64_t pixels = 0;
+    uint32_t units = 0;
+    int r = MIRT_OK;
+    if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
+    for (uint32_t t = 0; t < n; ++t) {
+        const mirt_tile& tl = tiles[t];
+        if (tl.w == 0 || tl.h == 0) return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty");
+        if ((uint64_t)tl.x + tl.w > W || (uint64_t)tl.y + tl.h > H)
+            return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " exceeds the screen");
+        TileDesc& d = sl->h_tiles[t];
+        d.x = tl.x;
+        d.y = tl.y;
+        d.w = tl.w;
+        d.h = tl.h;
+        d.out_off = pixels;
+        d.unit_begin = units;
+        d.units_w = (tl.w + kUnitW - 1) / kUnitW;
+        uint64_t u = (uint64_t)d.units_w * ((tl.h + kUnitH - 1) / kUnitH);
+        if ((uint64_t)units + u > 0xffffffffull) return fail(MIRT_E_LIMIT, "too many work units");
+        units += (uint32_t)u;
+        pixels += (uint64_t)tl.w * tl.h;
+    }
+    if (pixels > 0xffffffffull) return fail(MIRT_E_LIMIT, "more than 2^32 pixels in one call");
+    FrameArgs fa;
+    uint64_t tris = 0;
+    fill_args(c, f, W, H, fa, tris);
+    if ((r = dev_grow(sl->hits, sl->hits_cap, pixels)) != MIRT_OK) return r;
+    if ((r = dev_grow(sl->lit, sl->lit_cap, pixels * std::max<uint32_t>(f->n_lights, 1))) != MIRT_OK) return r;
+
+    ProfRec pr;
+    const bool prof = c->profiling;
+    if (prof && (r = prof_get(c, pr)) != MIRT_OK) return r;
+
+    HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(uint32_t), s));
+    const bool pre = !(c->flags & MIRT_OPT_NO_PREFILTER);
+    const int pgrid = (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
+    const int sgrid = (int)std::max<uint64_t>(
+        1, std::min<uint64_t>((pixels * std::max<uint32_t>(f->n_lights, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
+    const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((pixels + 255) / 256, (uint64_t)8 * c->cus));
+    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+    if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
+    HIP_TRY(launch_primary(fa, sl->d_tiles, n, units, out, sl->hits, sl->counters, pgrid, pre, s));
+    if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
+    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+    if (f->n_lights) {
+        HIP_TRY(launch_shadow(fa, sl->hits, sl->counters, sl->lit, sgrid, pre, s));
+    }
+    if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
+    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+    HIP_TRY(launch_shade(fa, sl->hits, sl->counters, sl->lit, out, pixels, hgrid, s));
+    if (prof) {
+        HIP_TRY(hipEventRecord(pr.ev[3], s));
+        HIP_TRY(hipMemcpyAsync(pr.h_hits, sl->counters + kCntHits, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        pr.pixels = pixels;
+        pr.tris = tris;
+        pr.nl = f->n_lights;
+        std::lock_guard<std::mutex> g(c->mu);
+        c->prof_pending.push_back(pr);
+    }
+    HIP_TRY(hipEventRecord(sl->done, s));
+    sl->pending = true;
+    *pixels_out = pixels;
+    *tris_out = tris;
+    return MIRT_OK;
+}
+
+int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t nl, mirt_stats* st) {
+    HIP_TRY(hipMemcpyAsync(sl->h_counters, sl->counters, kCntN * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    memset(st, 0, sizeof(*st));
+    st->primary_rays = pixels;
+    st->hits = sl->h_counters[kCntHits];
+    st->shadow_rays = st->hits * nl;
+    st->tri_tests = (st->primary_rays + st->shadow_rays) * tris;
+    return MIRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mirt_abi_version(void) { return MIRT_ABI_VERSION; }
+const char* mirt_last_error(void) { return g_err.c_str(); }
+
+int mirt_create(int device, mirt_ctx** out) {
+    if (!out) return fail(MIRT_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(MIRT_E_INVALID, "no HIP device " + std::to_string(device));
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(MIRT_E_DEVICE, std::string("libmirt is built for gfx950 only; device is ") + prop.gcnArchName);
+    mirt_ctx* c = new (std::nothrow) mirt_ctx();
+    if (!c) return fail(MIRT_E_NOMEM, "context allocation failed");
+    c->device = device;
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    *out = c;
+    return MIRT_OK;
+}
+
+void mirt_destroy(mirt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (auto& sp : c->slots) {
+        Slot* s = sp.get();
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        if (s->hits) (void)hipFree(s->hits);
+        if (s->lit) (void)hipFree(s->lit);
+        if (s->counters) (void)hipFree(s->counters);
+        if (s->d_tiles) (void)hipFree(s->d_tiles);
+        if (s->h_tiles) (void)hipHostFree(s->h_tiles);
+        if (s->h_counters) (void)hipHostFree(s->h_counters);
+        if (s->out_buf) (void)hipFree(s->out_buf);
+        if (s->done) (void)hipEventDestroy(s->done);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    for (auto* v : {&c->prof_pending, &c->prof_free})
+        for (auto& r : *v) {
+            for (auto e : r.ev)
+                if (e) (void)hipEventDestroy(e);
+            if (r.h_hits) (void)hipHostFree(r.h_hits);
+        }
+    for (auto& m : c->meshes) {
+        if (m.tri) (void)hipFree(m.tri);
+        if (m.vnrm) (void)hipFree(m.vnrm);
+        if (m.fmat) (void)hipFree(m.fmat);
+        if (m.mats) (void)hipFree(m.mats);
+    }
+    delete c;
+}
+
+int mirt_device(const mirt_ctx* c) { return c ? c->device : -1; }
+
+double mirt_go_tan(double x);
+
+int mirt_camera_init(const double pos[3], const double dir[3], double fov, mirt_camera* out) {
+    if (!pos || !dir || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    // camera.go:35-44 with GlobalUp = (0,1,0) (environment.go:22)
+    V3 d{dir[0], dir[1], dir[2]};
+    V3 gup{0, 1, 0};
+    if (is_zero(cross(d, gup))) return fail(MIRT_E_CAMERA, "Camera dir is parallel to global up {0 1 0}.");
+    V3 f = norm(d);
+    V3 l = norm(cross(d, gup));
+    V3 u = cross(l, f);
+    for (int k = 0; k < 3; ++k) out->pos[k] = pos[k];
+    out->forward[0] = f.x; out->forward[1] = f.y; out->forward[2] = f.z;
+    out->left[0] = l.x; out->left[1] = l.y; out->left[2] = l.z;
+    out->up[0] = u.x; out->up[1] = u.y; out->up[2] = u.z;
+    out->fov = fov;
+    out->proj_half_width = mirt_go_tan(fov / 2.0);  // tracer.go:17
+    return MIRT_OK;
+}
+
+// Go math.Tan (src/math/tan.go, Cephes): Cody–Waite reduction by pi/4 and a rational
+// approximation.  Coefficients verified bit-for-bit against Go's published hex values
+// (tests/test_host.py).  Beyond 2^29 Go switches to Payne–Hanek; camera fovs never do.
+double mirt_go_tan(double x) {
+    static const double P[3] = {-1.30936939181383777646e4, 1.15351664838587416140e6, -1.79565251976484877988e7};
+    static const double Q[5] = {1.0, 1.36812963470692954678e4, -1.32089234440210967447e6,
+                                2.50083801823357915839e7, -5.38695755929454629881e7};
+    const double PI4A = 7.85398125648498535156e-1, PI4B = 3.77489470793079817668e-8,
+                 PI4C = 2.69515142907905952645e-15;
+    const double M4PI = 1.27323954473516268615107010698011489627567716592365;
+    if (x == 0 || x != x) return x;
+    if (d_isinf(x)) return __builtin_nan("");
+    bool sign = false;
+    if (x < 0) {
+        x = -x;
+        sign = true;
+    }
+    if (x >= 536870912.0) return sign ? -std::tan(x) : std::tan(x);
+    uint64_t j = (uint64_t)(x * M4PI);
+    double y = (double)j;
+    if (j & 1) {
+        j++;
+        y++;
+    }
+    double z = ((x - y * PI4A) - y * PI4B) - y * PI4C;
+    double zz = z * z;
+    if (zz > 1e-14)
+        y = z + z * (zz * (((P[0] * zz) + P[1]) * zz + P[2]) / ((((zz + Q[1]) * zz + Q[2]) * zz + Q[3]) * zz + Q[4]));
+    else
+        y = z;
+    if (j & 2) y = -1 / y;
+    if (sign) y = -y;
+    return y;
+}
+
+double mirt_go_pow(double x, double y) { return go_pow(x, y); }
+
+int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn, uint32_t nn, const uint32_t* fv,
+                     const uint32_t* fn, const uint32_t* fmat, uint32_t nf, const mirt_material* mats, uint32_t nm,
+                     uint32_t* mesh_id) {
+    if (!c || !mesh_id) return fail(MIRT_E_INVALID, "NULL context or mesh_id");
+    if (nf && (!v || !fv || !fmat)) return fail(MIRT_E_INVALID, "NULL vertex/face array");
+    if (nf && (!mats || nm == 0)) return fail(MIRT_E_INVALID, "faces need at least one material");
+    const bool has_n = vn && nn > 0;
+    if (has_n && nf && !fn) return fail(MIRT_E_INVALID, "normals given without face normal indices");
+    for (uint32_t f = 0; f < nf; ++f) {
+        for (int k = 0; k < 3; ++k) {
+            if (fv[3 * f + k] >= nv) return fail(MIRT_E_INVALID, "face " + std::to_string(f) + " vertex out of range");
+            if (has_n && fn[3 * f + k] >= nn)
+                return fail(MIRT_E_INVALID, "face " + std::to_string(f) + " normal out of range");
+        }
+        if (fmat[f] >= nm) return fail(MIRT_E_INVALID, "face " + std::to_string(f) + " material out of range");
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    // P1, E1 = P2 - P1, E2 = P3 - P1 (triangle.go:38: single fp64 subtractions, so the
+    // precomputed edges are bit-identical to the per-test ones of the reference).
+    std::vector<double> tri((size_t)nf * kTriD), vnrm(has_n ? (size_t)nf * kTriD : 0), mt((size_t)nm * 10);
+    for (uint32_t f = 0; f < nf; ++f) {
+        const double* p1 = v + 3 * (size_t)fv[3 * f];
+        const double* p2 = v + 3 * (size_t)fv[3 * f + 1];
+        const double* p3 = v + 3 * (size_t)fv[3 * f + 2];
+        double* t = &tri[(size_t)f * kTriD];
+        for (int k = 0; k < 3; ++k) {
+            t[k] = p1[k];
+            t[3 + k] = p2[k] - p1[k];
+            t[6 + k] = p3[k] - p1[k];
+        }
+        if (has_n)
+            for (int q = 0; q < 3; ++q)
+                for (int k = 0; k < 3; ++k) vnrm[(size_t)f * kTriD + 3 * q + k] = vn[3 * (size_t)fn[3 * f + q] + k];
+    }
+    for (uint32_t m = 0; m < nm; ++m) {
+        for (int k = 0; k < 3; ++k) {
+            mt[10 * m + k] = mats[m].ka[k];
+            mt[10 * m + 3 + k] = mats[m].kd[k];
+            mt[10 * m + 6 + k] = mats[m].ks[k];
+        }
+        mt[10 * m + 9] = mats[m].ns;
+    }
+    MeshDev md;
+    md.ntri = nf;
+    md.nmat = nm;
+    md.has_normals = has_n;
+    auto upload = [&](void** dst, const void* src, size_t bytes) -> int {
+        if (bytes == 0) return MIRT_OK;
+        hipError_t e = hipMalloc(dst, bytes);
+        if (e != hipSuccess) return fail(MIRT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy mesh");
+        return MIRT_OK;
+    };
+    int r;
+    if ((r = upload((void**)&md.tri, tri.data(), tri.size() * 8)) != MIRT_OK) return r;
+    if ((r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK) return r;
+    if ((r = upload((void**)&md.fmat, fmat, (size_t)nf * 4)) != MIRT_OK) return r;
+    if ((r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) return r;
+    md.live = true;
+    std::lock_guard<std::mutex> g(c->mu);
+    *mesh_id = (uint32_t)c->meshes.size();
+    c->meshes.push_back(md);
+    return MIRT_OK;
+}
+
+int mirt_mesh_release(mirt_ctx* c, uint32_t id) {
+    if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (id >= c->meshes.size() || !c->meshes[id].live) return fail(MIRT_E_INVALID, "unknown mesh id");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    MeshDev& m = c->meshes[id];
+    if (m.tri) (void)hipFree(m.tri);
+    if (m.vnrm) (void)hipFree(m.vnrm);
+    if (m.fmat) (void)hipFree(m.fmat);
+    if (m.mats) (void)hipFree(m.mats);
+    m = MeshDev();
+    return MIRT_OK;
+}
+
+int mirt_trace_tiles_async(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
+                           uint32_t n, const mirt_outputs* dout, void* stream, mirt_stats* st) {
+    if (!c || !dout) return fail(MIRT_E_INVALID, "NULL context or outputs");
+    HIP_TRY(hipSetDevice(c->device));
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    Slot* sl = nullptr;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    hipStream_t s = stream ? (hipStream_t)stream : sl->stream;
+    OutPlanes out{dout->rgb, dout->rgb8, dout->valid, dout->face, dout->object};
+    uint64_t pixels = 0, tris = 0;
+    if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, nullptr, &pixels, &tris)) != MIRT_OK) {
+        (void)hipStreamSynchronize(s);
+        sl->pending = false;
+        return r;
+    }
+    if (st) return fill_stats(sl, s, pixels, tris, f->n_lights, st);
+    return MIRT_OK;
+}
+
+int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t w, uint32_t h, uint32_t W,
+                    uint32_t H, const mirt_outputs* hout, const volatile int* cancel, mirt_stats* st) {
+    if (!c || !hout) return fail(MIRT_E_INVALID, "NULL context or outputs");
+    HIP_TRY(hipSetDevice(c->device));
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    Slot* sl = nullptr;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    const uint64_t npx = (uint64_t)w * h;
+    // device staging for the requested planes: rgb(24) rgb8(3) valid(1) face(4) object(4)
+    const size_t need = npx * (24 + 4 + 4 + 3 + 1) + 64;
+    uint8_t* base = (uint8_t*)sl->out_buf;
+    size_t cap = sl->out_cap;
+    if ((r = dev_grow(base, cap, need)) != MIRT_OK) return r;
+    sl->out_buf = base;
+    sl->out_cap = cap;
+    OutPlanes out{};
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        uint8_t* p = base + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    out.rgb = hout->rgb ? (double*)carve(npx * 24) : nullptr;
+    out.face = hout->face ? (int32_t*)carve(npx * 4) : nullptr;
+    out.object = hout->object ? (int32_t*)carve(npx * 4) : nullptr;
+    out.rgb8 = hout->rgb8 ? carve(npx * 3) : nullptr;
+    out.valid = hout->valid ? carve(npx) : nullptr;
+    mirt_tile t{x, y, w, h};
+    uint64_t pixels = 0, tris = 0;
+    hipStream_t s = sl->stream;
+    if ((r = enqueue_trace(c, sl, f, W, H, &t, 1, out, s, cancel, &pixels, &tris)) != MIRT_OK) {
+        (void)hipStreamSynchronize(s);
+        sl->pending = false;
+        return r;
+    }
+    if (out.rgb) HIP_TRY(hipMemcpyAsync(hout->rgb, out.rgb, npx * 24, hipMemcpyDeviceToHost, s));
+    if (out.rgb8) HIP_TRY(hipMemcpyAsync(hout->rgb8, out.rgb8, npx * 3, hipMemcpyDeviceToHost, s));
+    if (out.valid) HIP_TRY(hipMemcpyAsync(hout->valid, out.valid, npx, hipMemcpyDeviceToHost, s));
+    if (out.face) HIP_TRY(hipMemcpyAsync(hout->face, out.face, npx * 4, hipMemcpyDeviceToHost, s));
+    if (out.object) HIP_TRY(hipMemcpyAsync(hout->object, out.object, npx * 4, hipMemcpyDeviceToHost, s));
+    if (st) {
+        if ((r = fill_stats(sl, s, pixels, tris, f->n_lights, st)) != MIRT_OK) return r;
+    } else {
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    sl->pending = false;
+    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+    return MIRT_OK;
+}
+
+int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
+                            const mirt_outputs* packed, const mirt_outputs* fb, void* stream) {
+    if (!c || !tiles || !packed || !fb || n == 0) return fail(MIRT_E_INVALID, "NULL argument or empty tile list");
+    HIP_TRY(hipSetDevice(c->device));
+    Slot* sl = nullptr;
+    int r;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    hipStream_t s = stream ? (hipStream_t)stream : sl->stream;
+    if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
+    uint64_t pixels = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        if ((uint64_t)tiles[t].x + tiles[t].w > W || (uint64_t)tiles[t].y + tiles[t].h > H || !tiles[t].w ||
+            !tiles[t].h)
+            return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty or exceeds the screen");
+        TileDesc& d = sl->h_tiles[t];
+        d = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, pixels, 0, 0};
+        pixels += (uint64_t)tiles[t].w * tiles[t].h;
+    }
+    HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
+    OutPlanes src{packed->rgb, packed->rgb8, packed->valid, packed->face, packed->object};
+    OutPlanes dst{fb->rgb, fb->rgb8, fb->valid, fb->face, fb->object};
+    HIP_TRY(launch_unpack(sl->d_tiles, n, pixels, H, src, dst, s));
+    HIP_TRY(hipEventRecord(sl->done, s));
+    sl->pending = true;
+    return MIRT_OK;
+}
+
+int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* orig, const double* dir, uint8_t* ok,
+                    double* hit, double* normal, int32_t* face, int32_t* object) {
+    if (!c || !orig || !dir || !ok || !hit || !normal || !face || !object)
+        return fail(MIRT_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    if (n == 0) return MIRT_OK;
+    Slot* sl = nullptr;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    const size_t need = (size_t)n * (24 * 4 + 1 + 8) + 128;
+    uint8_t* base = (uint8_t*)sl->out_buf;
+    size_t cap = sl->out_cap;
+    if ((r = dev_grow(base, cap, need)) != MIRT_OK) return r;
+    sl->out_buf = base;
+    sl->out_cap = cap;
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        uint8_t* p = base + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    RayIO io;
+    io.orig = (const double*)carve((size_t)n * 24);
+    io.dir = (const double*)carve((size_t)n * 24);
+    io.hit = (double*)carve((size_t)n * 24);
+    io.normal = (double*)carve((size_t)n * 24);
+    io.face = (int32_t*)carve((size_t)n * 4);
+    io.object = (int32_t*)carve((size_t)n * 4);
+    io.ok = carve(n);
+    io.n = n;
+    hipStream_t s = sl->stream;
+    FrameArgs fa;
+    uint64_t tris;
+    fill_args(c, f, 1, 1, fa, tris);
+    HIP_TRY(hipMemcpyAsync((void*)io.orig, orig, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync((void*)io.dir, dir, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n + kWG - 1) / kWG, 2 * (uint64_t)c->cus));
+    HIP_TRY(launch_rays(fa, io, grid, s));
+    HIP_TRY(hipMemcpyAsync(ok, io.ok, n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hit, io.hit, (size_t)n * 24, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(normal, io.normal, (size_t)n * 24, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(face, io.face, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(object, io.object, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MIRT_OK;
+}
+
+int mirt_profile_enable(mirt_ctx* c, int enable) {
+    if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    c->profiling = enable != 0;
+    return MIRT_OK;
+}
+
+int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<ProfRec> recs;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        recs.swap(c->prof_pending);
+    }
+    memset(out, 0, sizeof(*out));
+    for (auto& r : recs) {
+        HIP_TRY(hipEventSynchronize(r.ev[3]));
+        float a = 0, b = 0, d = 0, t = 0;
+        HIP_TRY(hipEventElapsedTime(&a, r.ev[0], r.ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, r.ev[1], r.ev[2]));
+        HIP_TRY(hipEventElapsedTime(&d, r.ev[2], r.ev[3]));
+        HIP_TRY(hipEventElapsedTime(&t, r.ev[0], r.ev[3]));
+        out->launches++;
+        out->primary_ms_sum += a;
+        out->shadow_ms_sum += b;
+        out->shade_ms_sum += d;
+        out->frame_ms_sum += t;
+        const uint64_t hits = *r.h_hits;
+        out->primary_rays += r.pixels;
+        out->hits += hits;
+        out->shadow_rays += hits * r.nl;
+        out->primary_tri_tests += r.pixels * r.tris;
+        out->shadow_tri_tests += hits * r.nl * r.tris;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto& r : recs) c->prof_free.push_back(r);
+    return MIRT_OK;
+}
+
+int mirt_debug_fp64(mirt_ctx* c, int op, uint32_t n, const double* a, const double* b, double* out) {
+    if (!c || !a || !b || !out || op < 0 || op > 3) return fail(MIRT_E_INVALID, "bad argument");
+    if (n == 0) return MIRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    double* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, (size_t)n * 24));
+    hipError_t e = hipMemcpy(d, a, (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, b, (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_debug_fp64(op, n, d, d + n, d + 2 * (size_t)n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * (size_t)n, (size_t)n * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "mirt_debug_fp64");
+    return MIRT_OK;
+}
+
+int mirt_set_options(mirt_ctx* c, uint32_t flags) {
+    if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    c->flags = flags;
+    return MIRT_OK;
+}
+
+}  // extern "C"

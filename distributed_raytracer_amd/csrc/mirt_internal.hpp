@@ -1,0 +1,102 @@
+// mirt_internal.hpp — layouts shared by the host side (mirt.cpp) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mirt.h"
+
+namespace mirt {
+
+// Launch geometry.  One workgroup = 8 waves; each wave traces an 8x8 pixel block, so a
+// workgroup's unit of primary work is a 32x16 pixel block of one tile.
+constexpr int kWG = 512;
+constexpr int kUnitW = 32, kUnitH = 16;
+// Doubles per triangle record in HBM and LDS: P1, E1 = P2-P1, E2 = P3-P1 (72 B).
+constexpr int kTriD = 9;
+// Triangles one workgroup holds in LDS (73,728 B; two workgroups per CU fit in 160 KiB).
+// Meshes up to this size stay resident in LDS for the life of a persistent workgroup;
+// larger meshes stream through it in batches of this size.
+constexpr int kLdsTris = 1024;
+
+// One uploaded mesh, device pointers (shared/state/mesh.go:100-106).
+struct DevMesh {
+    const double* tri;       // ntri * 9 : P1, E1, E2
+    const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
+    const uint32_t* fmat;    // ntri     : material index
+    const double* mats;      // nmat * 10: ka[3] kd[3] ks[3] ns
+    uint32_t ntri;
+    uint32_t has_normals;
+};
+
+struct DevObject {
+    DevMesh m;
+    double pos[3];
+};
+
+// Everything per frame travels by value in the kernel-argument block (s_load'ed).
+struct FrameArgs {
+    double cam[3], fwd[3], left[3], up[3];
+    double phw, phh;              // tan(fov/2) and phw*H/W (tracer.go:17-18)
+    int32_t W, H, halfW, halfH;   // halfW = W/2 with Go integer division
+    uint32_t n_objects, n_lights;
+    uint32_t flags, pad;
+    DevObject obj[MIRT_MAX_OBJECTS];
+    double lpos[MIRT_MAX_LIGHTS][3];
+    double lcol[MIRT_MAX_LIGHTS][3];
+};
+
+struct TileDesc {
+    uint32_t x, y, w, h;
+    uint64_t out_off;      // first packed pixel of this tile
+    uint32_t unit_begin;   // first 32x16 work unit of this tile
+    uint32_t units_w;      // ceil(w / 32)
+};
+
+// A primary hit handed from the primary kernel to the shadow and shade kernels.
+struct HitRec {
+    double h[3];     // world-space intersection
+    double n[3];     // interpolated (or flat) normal
+    uint64_t out;    // packed output pixel index
+    uint32_t obj;    // object index
+    uint32_t mat;    // material index inside that object's mesh
+};
+
+struct OutPlanes {
+    double* rgb;
+    uint8_t* rgb8;
+    uint8_t* valid;
+    int32_t* face;
+    int32_t* object;
+};
+
+// Counters kept in device memory per call slot.
+enum { kCntHits = 0, kCntN = 4 };
+
+enum SecondaryMode { kModeShadow = 0, kModeRays = 1 };
+
+// Arbitrary-ray inputs/outputs for mirt_trace_rays.
+struct RayIO {
+    const double* orig;
+    const double* dir;
+    uint8_t* ok;
+    double* hit;
+    double* normal;
+    int32_t* face;
+    int32_t* object;
+    uint32_t n;
+};
+
+hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
+                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, bool prefilter,
+                          hipStream_t s);
+hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, uint8_t* lit,
+                         int grid, bool prefilter, hipStream_t s);
+hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, const uint8_t* lit,
+                        const OutPlanes& out, uint64_t lit_stride, int grid, hipStream_t s);
+hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, hipStream_t s);
+hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
+hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
+                         const OutPlanes& dst, hipStream_t s);
+
+}  // namespace mirt

@@ -1,0 +1,216 @@
+/*
+ * mirt.h — C ABI of libmirt.so, the MI355X-native trace worker.
+ *
+ * Plain C, cgo-safe: no C++ types, no torch types, plain pointers and sizes.  Every
+ * buffer is owned by the caller; the library copies what it needs during the call and
+ * keeps no caller pointer after return (cgo pointer rules).  Every entry returns 0
+ * (MIRT_OK) or a negative MIRT_E_* code, with detail in the thread-local
+ * mirt_last_error().  No exception crosses the ABI.  All entries are re-entrant:
+ * frame state is an argument, never global (gRPC serves each BulkTrace in its own
+ * goroutine, and the master pipelines frames with different cameras).
+ *
+ * What each entry replaces in the reference (paths relative to its root):
+ *   mirt_trace_tile      — the BulkTrace tile loop worker/distributed/main.go:67-89
+ *                          calling tracer.Trace (worker/shared/tracer/tracer.go:81-91)
+ *                          per pixel; also the sequential draw loop
+ *                          worker/sequential/main.go:21-28 (tile = whole screen).
+ *   mirt_trace_rays      — tracer.trace (tracer.go:27-50) on arbitrary rays.
+ *   mirt_mesh_upload     — the immutable mesh a worker receives at Register
+ *                          (shared/state/environment.go:25-62, mesh.go:100-106).
+ *   mirt_frame / mirt_camera — the per-frame EnvMutables carried by WorkOrder.diff
+ *                          (environment.go:65-69, camera.go:20-24, light.go:10-13).
+ *   mirt_camera_init     — state.NewCamera (camera.go:35-44) + the math.Tan of
+ *                          tracer.go:17.
+ */
+#ifndef MIRT_H
+#define MIRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIRT_ABI_VERSION 1
+
+/* error codes */
+#define MIRT_OK 0
+#define MIRT_E_INVALID (-1)   /* bad argument (null pointer, zero size, bad id) */
+#define MIRT_E_DEVICE (-2)    /* HIP runtime / kernel launch error */
+#define MIRT_E_LIMIT (-3)     /* more objects/lights than the kernel-argument block holds */
+#define MIRT_E_NOMEM (-4)     /* device or host allocation failed */
+#define MIRT_E_CAMERA (-5)    /* camera dir parallel to the global up vector (camera.go:37) */
+#define MIRT_E_CANCELLED (-6) /* *cancel became non-zero (worker/distributed/main.go:73) */
+#define MIRT_E_IO (-7)        /* scene / OBJ / MTL file could not be read or parsed */
+
+#define MIRT_MAX_OBJECTS 16
+#define MIRT_MAX_LIGHTS 16
+
+typedef struct mirt_ctx mirt_ctx;
+
+/* shared/state/mesh.go:94-97 Material (colour.RGB channels as fp64 in [0,1]) */
+typedef struct {
+    double ka[3], kd[3], ks[3];
+    double ns;
+} mirt_material;
+
+/* shared/state/object.go:17-22 Object (Pos + the mesh its id links to) */
+typedef struct {
+    uint32_t mesh_id;
+    uint32_t reserved;
+    double pos[3];
+} mirt_object;
+
+/* shared/state/light.go:10-13 Light (Col = NewRGB(u8)/255) */
+typedef struct {
+    double pos[3];
+    double col[3];
+} mirt_light;
+
+/*
+ * shared/state/camera.go:20-24 Camera.  forward/left/up exactly as NewCamera made them.
+ * proj_half_width = math.Tan(fov / 2.0) as the caller computed it (tracer.go:17); a
+ * Go caller passes its own math.Tan so the value is bit-identical to the reference.
+ * mirt_camera_init fills it with a restatement of Go's math.Tan.
+ */
+typedef struct {
+    double pos[3];
+    double forward[3];
+    double left[3];
+    double up[3];
+    double fov;
+    double proj_half_width;
+} mirt_camera;
+
+/* shared/state/environment.go:65-69 EnvMutables */
+typedef struct {
+    const mirt_object *objects;
+    uint32_t n_objects;
+    const mirt_light *lights;
+    uint32_t n_lights;
+    mirt_camera camera;
+} mirt_frame;
+
+/* shared/comms/comms.proto:25-31 WorkOrder geometry */
+typedef struct {
+    uint32_t x, y, w, h;
+} mirt_tile;
+
+/*
+ * Output planes.  Any pointer may be NULL (not produced).  Pixel (x+i, y+j) of a tile
+ * lands at index i*h + j (column-major, worker/distributed/main.go:82); for a tile list
+ * the tiles are packed back to back in list order.
+ *   rgb    3 fp64 per pixel, the colour.RGB returned by tracer.Trace (misses: 0)
+ *   rgb8   3 u8 per pixel, uint8(255*c) truncating (colour.go:59-61; misses: 0)
+ *   valid  1 u8 per pixel, Trace's bool
+ *   face   winning face index inside its mesh (-1 on a miss)      [diagnostic]
+ *   object winning object index inside mirt_frame.objects (-1)    [diagnostic]
+ */
+typedef struct {
+    double *rgb;
+    uint8_t *rgb8;
+    uint8_t *valid;
+    int32_t *face;
+    int32_t *object;
+} mirt_outputs;
+
+/* Counters of one call; timings are device time from HIP events (0 if not recorded). */
+typedef struct {
+    uint64_t primary_rays;
+    uint64_t shadow_rays;
+    uint64_t hits;
+    uint64_t tri_tests;     /* ray-triangle tests performed (brute force: rays * tris) */
+    double ms_primary;      /* raygen + nearest-hit kernel */
+    double ms_shadow;       /* shadow-ray kernel */
+    double ms_shade;        /* Phong + output kernel */
+    double ms_total;        /* first kernel start -> last kernel end */
+} mirt_stats;
+
+/* Accumulated per-kernel device times while profiling is enabled (HIP events). */
+typedef struct {
+    uint64_t launches;
+    double primary_ms_sum, shadow_ms_sum, shade_ms_sum, frame_ms_sum;
+    uint64_t primary_tri_tests, shadow_tri_tests;
+    uint64_t primary_rays, shadow_rays, hits;
+} mirt_profile;
+
+int mirt_abi_version(void);
+const char *mirt_last_error(void);
+
+/* Context bound to one HIP device (one process per GPU). */
+int mirt_create(int device, mirt_ctx **out);
+void mirt_destroy(mirt_ctx *ctx);
+int mirt_device(const mirt_ctx *ctx);
+
+/* camera.go:35-44 NewCamera + tracer.go:17 math.Tan(fov/2).  MIRT_E_CAMERA if dir x up = 0. */
+int mirt_camera_init(const double pos[3], const double dir[3], double fov, mirt_camera *out);
+/* Restatement of Go's math.Tan (pure Go, Cephes). */
+double mirt_go_tan(double x);
+/* Restatement of Go's math.Pow (the specular term of tracer.go:72). */
+double mirt_go_pow(double x, double y);
+
+/*
+ * Upload one immutable mesh (shared/state/mesh.go:100-106 after MeshFromFile):
+ *   v    nv*3 vertex positions (float32-parsed, widened to fp64)
+ *   vn   nn*3 vertex normals, already normalised; NULL/0 => flat Normal() shading
+ *   fv   nf*3 vertex indices; fn nf*3 normal indices (ignored if vn is NULL); fmat nf
+ *   mats nm materials
+ * Indices are range-checked here.  The mesh id is returned in *mesh_id.
+ */
+int mirt_mesh_upload(mirt_ctx *ctx, const double *v, uint32_t nv, const double *vn, uint32_t nn,
+                     const uint32_t *fv, const uint32_t *fn, const uint32_t *fmat, uint32_t nf,
+                     const mirt_material *mats, uint32_t nm, uint32_t *mesh_id);
+int mirt_mesh_release(mirt_ctx *ctx, uint32_t mesh_id);
+
+/*
+ * BulkTrace: trace tile (x, y, w, h) of a W x H screen into HOST buffers.  Synchronous.
+ * cancel (may be NULL) is polled between kernel launches.  stats may be NULL.
+ */
+int mirt_trace_tile(mirt_ctx *ctx, const mirt_frame *frame, uint32_t x, uint32_t y, uint32_t w, uint32_t h,
+                    uint32_t W, uint32_t H, const mirt_outputs *host_out, const volatile int *cancel,
+                    mirt_stats *stats);
+
+/*
+ * Trace a list of tiles into DEVICE buffers on `stream` (a hipStream_t; NULL = the
+ * context's own stream).  Asynchronous: returns after enqueueing.  If stats is non-NULL
+ * the call synchronises the stream and fills it.  Device buffers must hold
+ * sum(w*h) pixels of each requested plane.
+ */
+int mirt_trace_tiles_async(mirt_ctx *ctx, const mirt_frame *frame, uint32_t W, uint32_t H,
+                           const mirt_tile *tiles, uint32_t n_tiles, const mirt_outputs *device_out,
+                           void *stream, mirt_stats *stats);
+
+/*
+ * Framebuffer assembly after a gather: scatter packed tile planes (device) into a
+ * W x H column-major framebuffer (pixel (x, y) at x*H + y, the worker/sequential
+ * layout).  Planes that are NULL in either struct are skipped.  Asynchronous on stream.
+ */
+int mirt_unpack_tiles_async(mirt_ctx *ctx, uint32_t W, uint32_t H, const mirt_tile *tiles, uint32_t n_tiles,
+                            const mirt_outputs *packed, const mirt_outputs *frame_out, void *stream);
+
+/* tracer.go:27-50 trace() on n arbitrary rays (host buffers), brute force. */
+int mirt_trace_rays(mirt_ctx *ctx, const mirt_frame *frame, uint32_t n, const double *origins,
+                    const double *dirs, uint8_t *ok, double *hit, double *normal, int32_t *face,
+                    int32_t *object);
+
+/* HIP-event profiling of every subsequent trace call (per-kernel device time). */
+int mirt_profile_enable(mirt_ctx *ctx, int enable);
+/* Synchronises outstanding profiled work, returns the sums and resets them. */
+int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
+
+/* Ask for kernel variants (benchmark ablations).  0 = defaults. */
+#define MIRT_OPT_NO_PREFILTER 1u  /* always take the true fp64 divide for r2 */
+int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
+
+/*
+ * Diagnostic: evaluate one fp64 primitive of the kernels on the device for n inputs
+ * (host buffers) so tests can pin device arithmetic against the host bit-for-bit.
+ *   op 0: sqrt(a)   op 1: a / b   op 2: Go math.Pow(a, b)   op 3: Go math.Max(a, b)
+ */
+int mirt_debug_fp64(mirt_ctx *ctx, int op, uint32_t n, const double *a, const double *b, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIRT_H */

@@ -1,0 +1,285 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the golden vectors.
+
+Bar: hit mask, winning face and object bit-exact; RGB bit-exact (tolerance stated where
+a test allows one: 1e-5 per channel is the north-star bound, but every path here is
+expected to be bit-identical because both sides use unfused fp64 in the reference's
+operation order).
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+RGB_TOL = 1e-5  # north-star bound per channel; asserted in addition to bit-exactness counts
+
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def test_device_fp64_primitives_bit_exact(ctx):
+    import distributed_raytracer_amd as rt
+    rng = np.random.default_rng(7)
+    a = np.concatenate([rng.random(20000) * 10, rng.random(2000) * 1e-300, np.array([0.0, 1.0, 4.0, 2.0, 1e-310,
+                                                                                      5e-324, 1e300])])
+    b = np.concatenate([rng.random(20000) + 0.1, rng.random(2000) * 1e10 + 1, np.ones(7)])
+    assert np.array_equal(ctx.debug_fp64(0, a, b), np.sqrt(a)), "device sqrt is not correctly rounded"
+    assert np.array_equal(ctx.debug_fp64(1, a, b), a / b), "device division is not IEEE"
+    x = rng.random(5000)
+    y = rng.integers(0, 40, 5000).astype(np.float64)
+    host = np.array([rt._lib.lib().mirt_go_pow(float(p), float(q)) for p, q in zip(x, y)])
+    assert np.array_equal(ctx.debug_fp64(2, x, y), host), "device go_pow differs from host"
+    from oracle.oracle import go_pow
+    assert np.array_equal(host, np.array([go_pow(float(p), float(q)) for p, q in zip(x, y)]))
+    mx = ctx.debug_fp64(3, np.array([-0.0, 0.0, -1.0, np.nan]), np.array([0.0, -0.0, 0.0, 1.0]))
+    assert np.signbit(mx[0]) == False and np.signbit(mx[1]) == False and mx[2] == 0.0 and np.isnan(mx[3])  # noqa: E712
+
+
+def test_frame_64x48_matches_golden(env):
+    import distributed_raytracer_amd as rt
+    g = _golden("suzanne_64x48.npz")
+    fb = rt.draw(env, 64, 48)
+    assert np.array_equal(fb.valid, g["valid"])
+    assert np.array_equal(fb.face, g["face"])
+    assert np.array_equal(fb.obj, g["obj"])
+    assert np.array_equal(fb.rgb, g["rgb"])
+    assert np.array_equal(fb.rgb8, g["rgb8"])
+    assert fb.stats["hits"] == int(g["valid"].sum())
+
+
+def test_frame_320x240_matches_golden(env):
+    import distributed_raytracer_amd as rt
+    g = _golden("suzanne_320x240.npz")
+    fb = rt.draw(env, 320, 240)
+    hit = np.nonzero(fb.valid)[0]
+    assert np.array_equal(hit, g["hit_index"].astype(np.int64))
+    assert np.array_equal(fb.face[hit], g["face"])
+    assert np.abs(fb.rgb[hit] - g["rgb"]).max() <= RGB_TOL
+    assert np.array_equal(fb.rgb[hit], g["rgb"]), f"{(fb.rgb[hit] != g['rgb']).sum()} channels not bit-exact"
+    assert np.array_equal(fb.rgb8[hit], g["rgb8"])
+    miss = fb.valid == 0
+    assert not fb.rgb[miss].any() and not fb.rgb8[miss].any() and (fb.face[miss] == -1).all()
+    assert fb.stats["primary_rays"] == 76800 and fb.stats["shadow_rays"] == int(g["shadow_rays"])
+
+
+def test_prefilter_is_exact(ctx, env):
+    import distributed_raytracer_amd as rt
+    a = rt.draw(env, 160, 120)
+    ctx.set_options(rt._lib.MIRT_OPT_NO_PREFILTER)
+    try:
+        b = rt.draw(env, 160, 120)
+    finally:
+        ctx.set_options(0)
+    for k in ("valid", "face", "rgb", "rgb8"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+
+
+@pytest.mark.parametrize("tile", [(0, 0, 1, 1), (37, 11, 50, 33), (319, 239, 1, 1), (100, 80, 120, 90),
+                                  (0, 0, 320, 240), (13, 200, 307, 40), (150, 0, 1, 240)])
+def test_tile_contract_column_major(env, tile):
+    """BulkTrace: pixel (x+i, y+j) at i*h + j, global pixel coords, full-screen W,H."""
+    import distributed_raytracer_amd as rt
+    g = _golden("suzanne_320x240.npz")
+    W, H = 320, 240
+    full_valid = np.zeros(W * H, np.uint8)
+    full_valid[g["hit_index"]] = 1
+    full_rgb8 = np.zeros((W * H, 3), np.uint8)
+    full_rgb8[g["hit_index"]] = g["rgb8"]
+    x, y, w, h = tile
+    r = rt.trace_tile(env, x, y, w, h, W, H)
+    exp_valid = full_valid.reshape(W, H)[x:x + w, y:y + h].reshape(-1)
+    exp_rgb8 = full_rgb8.reshape(W, H, 3)[x:x + w, y:y + h].reshape(-1, 3)
+    assert np.array_equal(r.valid, exp_valid)
+    assert np.array_equal(r.rgb8, exp_rgb8)
+
+
+def test_bulk_trace_master_partition(env):
+    """Every rectangle of the master's bisection (master/main.go:54-91) for 24 workers,
+    traced as BulkTrace orders and reassembled, equals the full frame."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import master_partition, unpack_host
+    g = _golden("suzanne_320x240.npz")
+    W, H = 320, 240
+    parts, _ = master_partition((0, 0, W, H), 24)
+    tr = rt.Tracer(env, W, H)
+    packed = np.concatenate([tr.bulk_trace(rt.WorkOrder(*p)).results for p in parts])
+    fb = np.zeros((W * H, 3), np.uint8)
+    unpack_host(W, H, parts, packed, fb)
+    exp = np.zeros((W * H, 3), np.uint8)
+    exp[g["hit_index"]] = g["rgb8"]
+    assert np.array_equal(fb, exp)
+
+
+def test_trace_single_pixel_api(env):
+    import distributed_raytracer_amd as rt
+    g = _golden("suzanne_64x48.npz")
+    for (i, j) in [(32, 24), (0, 0), (40, 20), (20, 30)]:
+        col, ok = rt.trace(i, j, 64, 48, env)
+        idx = i * 48 + j
+        assert ok == bool(g["valid"][idx])
+        assert (col.r, col.g, col.b) == tuple(g["rgb"][idx])
+        assert col.rgb() == tuple(int(v) for v in g["rgb8"][idx])
+
+
+def test_device_tiles_packed_and_unpacked(ctx, env):
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import framebuffer as fbm
+    g = _golden("suzanne_320x240.npz")
+    W, H = 320, 240
+    tiles = fbm.plan_tiles(W, H, 48)
+    dev = torch.device("cuda", 0)
+    mut = env.mutable()
+    frame = mut.to_frame()
+    for world in (1, 3):
+        full = fbm.alloc_planes(W * H, dev, with_rgb=True)
+        full.valid.zero_()
+        for r in range(world):
+            mine = fbm.assign(tiles, world, r)
+            packed = fbm.alloc_planes(fbm.pixels_of(mine), dev, with_rgb=True)
+            fbm.trace_tiles_device(ctx, frame, W, H, mine, packed, torch.cuda.current_stream().cuda_stream)
+            fbm.unpack_device(ctx, W, H, mine, packed, full, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        valid = full.valid.cpu().numpy()
+        hit = np.nonzero(valid)[0]
+        assert np.array_equal(hit, g["hit_index"].astype(np.int64))
+        assert np.array_equal(full.rgb.cpu().numpy()[hit], g["rgb"])
+        assert np.array_equal(full.rgb8.cpu().numpy()[hit], g["rgb8"])
+
+
+def test_trace_rays_matches_oracle(env, oracle, py_scene):
+    import distributed_raytracer_amd as rt
+    rng = np.random.default_rng(3)
+    n = 4000
+    m = py_scene.meshes[0]
+    pos = np.array(py_scene.objects[0][1])
+    # rays aimed exactly at vertices, edge midpoints and random surface points
+    V = m.vertices[m.face_v]
+    targets = np.concatenate([V[:, 0], (V[:, 0] + V[:, 1]) / 2, V.mean(axis=1)])[:n] + pos
+    origins = targets + rng.normal(size=targets.shape) * 3.0
+    dirs = targets - origins
+    dirs /= np.linalg.norm(dirs, axis=1)[:, None]
+    g = rt.trace_rays(origins, dirs, env)
+    o = oracle.trace_rays(origins, dirs)
+    assert np.array_equal(g["ok"], o["ok"])
+    assert np.array_equal(g["face"], o["face"])
+    assert np.array_equal(g["hit"], o["hit"])
+    assert np.array_equal(g["normal"], o["normal"])
+
+
+def test_multi_object_flat_and_default_material(ctx, py_scene):
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from scenes import gpu_env, multi_object_scene
+    sc = multi_object_scene(py_scene.meshes[0])
+    env = gpu_env(ctx, sc)
+    W, H = 96, 72
+    fb = rt.draw(env, W, H)
+    ref = Oracle(sc).frame(W, H, nthreads=8)
+    assert ref["valid"].sum() > 1000 and len(np.unique(ref["obj"][ref["valid"] == 1])) == 4
+    assert np.array_equal(fb.valid, ref["valid"])
+    assert np.array_equal(fb.obj, ref["obj"])
+    assert np.array_equal(fb.face, ref["face"])
+    assert np.array_equal(fb.rgb, ref["rgb"])
+
+
+def test_streamed_mesh_larger_than_lds(ctx):
+    """> kLdsTris triangles: the batch-streaming path (not LDS-resident)."""
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from oracle.scene_py import PyScene
+    from scenes import gpu_env, uv_sphere
+    sc = PyScene()
+    sc.meshes = [uv_sphere(40, 60, 1.2)]  # 4800 triangles
+    sc.objects = [(0, (1.0, 1.0, -1.0))]
+    sc.lights = [((0.0, 0.0, 10.0), (0.0, 1.0, 0.0)), ((0.0, 10.0, 10.0), (1.0, 0.0, 0.0))]
+    sc.cam_pos, sc.cam_dir, sc.fov = (1.0, 1.0, 5.0), (0.0, 0.0, -1.0), 1.04719755
+    env = gpu_env(ctx, sc)
+    fb = rt.draw(env, 64, 48)
+    ref = Oracle(sc).frame(64, 48, nthreads=8)
+    assert ref["valid"].sum() > 200
+    for k in ("valid", "face", "rgb"):
+        assert np.array_equal(getattr(fb, k), ref[k]), k
+
+
+def test_1080p_subsample_matches_oracle(ctx, env, oracle):
+    """configs[1] size: the full GPU frame, checked on every 16th column against the
+    oracle (each column a 1-pixel-wide tile of the same 1920x1080 screen)."""
+    import distributed_raytracer_amd as rt
+    W, H = 1920, 1080
+    fb = rt.draw(env, W, H)
+    cols = list(range(3, W, 16))
+    ref = oracle.trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=16)
+    sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
+    assert np.array_equal(fb.valid[sub], ref["valid"])
+    assert np.array_equal(fb.face[sub], ref["face"])
+    assert np.array_equal(fb.rgb[sub], ref["rgb"])
+    # SURVEY.md §8c sanity figure for the whole frame
+    assert int(fb.valid.sum()) == 209584
+    assert fb.stats["shadow_rays"] == 3 * 209584
+
+
+def test_concurrent_calls_with_different_cameras(ctx, env):
+    """Re-entrancy: BulkTrace calls from many threads, each with its own camera."""
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    cams = [rt.Camera.new((1.0 + 0.1 * k, 1.0, 5.0 - 0.2 * k), (0.05 * k, 0.0, -1.0), 1.04719755)
+            for k in range(6)]
+    muts = [rt.EnvMutables(base.objects, base.lights, c) for c in cams]
+    expect = [rt.trace_tile(env, 0, 0, 80, 60, 80, 60, m) for m in muts]
+    got = [None] * (len(muts) * 3)
+    errs = []
+
+    def work(k):
+        try:
+            got[k] = rt.trace_tile(env, 0, 0, 80, 60, 80, 60, muts[k % len(muts)])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(len(got))]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    assert not errs
+    for k, r in enumerate(got):
+        e = expect[k % len(muts)]
+        assert np.array_equal(r.rgb, e.rgb) and np.array_equal(r.valid, e.valid)
+
+
+def test_cancel_and_errors(ctx, env):
+    import distributed_raytracer_amd as rt
+    cancel = C.c_int(1)
+    with pytest.raises(rt.MirtError) as ei:
+        rt.trace_tile(env, 0, 0, 32, 32, 64, 48, cancel=cancel)
+    assert ei.value.code == rt._lib.MIRT_E_CANCELLED
+    with pytest.raises(rt.MirtError) as ei:
+        rt.trace_tile(env, 60, 0, 10, 10, 64, 48)  # exceeds the screen
+    assert ei.value.code == rt._lib.MIRT_E_INVALID
+    base = env.mutable()
+    bad = rt.EnvMutables([rt.SceneObject(999, (0, 0, 0))], base.lights, base.cam)
+    with pytest.raises(rt.MirtError):
+        rt.trace_tile(env, 0, 0, 8, 8, 64, 48, bad)
+    many = rt.EnvMutables(base.objects, base.lights * 6, base.cam)
+    with pytest.raises(rt.MirtError) as ei:
+        rt.trace_tile(env, 0, 0, 8, 8, 64, 48, many)
+    assert ei.value.code == rt._lib.MIRT_E_LIMIT
+    # the context still works after errors
+    assert rt.trace_tile(env, 0, 0, 8, 8, 64, 48).valid.shape == (64,)
+
+
+def test_profile_counters(ctx, env):
+    import distributed_raytracer_amd as rt
+    ctx.profile_enable(True)
+    rt.draw(env, 320, 240)
+    rt.draw(env, 320, 240)
+    p = ctx.profile_read()
+    ctx.profile_enable(False)
+    assert p["launches"] == 2
+    assert p["primary_rays"] == 2 * 76800 and p["hits"] == 2 * 5820
+    assert p["primary_tri_tests"] == 2 * 76800 * 968
+    assert p["primary_ms_sum"] > 0 and p["frame_ms_sum"] >= p["primary_ms_sum"]
