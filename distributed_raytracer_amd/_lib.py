@@ -128,6 +128,15 @@ def lib() -> C.CDLL:
     """Load libmirt.so (built in-tree by __graft_entry__.build()).  Raises if absent."""
     global _lib
     if _lib is None:
+        # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever
+        # is loaded first serves the whole process, so load torch's first when torch is
+        # installed: one HIP runtime per process, and torch stream handles passed to
+        # mirt_trace_tiles_async are valid in libmirt.  A Go/C caller without torch gets
+        # /opt/rocm's runtime through libmirt's RUNPATH.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is missing: the HIP trace worker is not built. Run "

@@ -87,6 +87,17 @@ def unpack_host(W: int, H: int, tiles: Sequence[TileT], packed: np.ndarray, out:
         off += w * h
 
 
+def gather_packed(buf, world: int, rank: int, root: int = 0, group=None):
+    """Gather every rank's packed buffer (same shape on all ranks) to `root`.  The one
+    collective of the multi-GPU path: RCCL over xGMI for cuda tensors ("nccl"
+    backend), gloo for CPU tensors (tests).  Returns the list on root, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    out = [torch.empty_like(buf) for _ in range(world)] if rank == root else None
+    dist.gather(buf, out, dst=root, group=group)
+    return out
+
+
 @dataclass
 class DevicePlanes:
     """Device tensors of one packed or full-frame output (torch, on the context's GPU)."""
@@ -94,6 +105,7 @@ class DevicePlanes:
     valid: object           # (n,)   uint8
     rgb: Optional[object] = None   # (n, 3) float64
     face: Optional[object] = None  # (n,) int32
+    raw: Optional[object] = None   # (4n,) uint8: the allocation rgb8 ++ valid live in
 
     def outputs(self, offset: int = 0) -> L.Outputs:
         def p(t, elem_bytes):
@@ -107,7 +119,7 @@ def alloc_planes(n: int, device, with_rgb: bool = False, with_face: bool = False
     buf = torch.empty(n * 4, dtype=torch.uint8, device=device)
     return DevicePlanes(rgb8=buf[: n * 3].view(n, 3), valid=buf[n * 3:],
                         rgb=torch.empty((n, 3), dtype=torch.float64, device=device) if with_rgb else None,
-                        face=torch.empty(n, dtype=torch.int32, device=device) if with_face else None)
+                        face=torch.empty(n, dtype=torch.int32, device=device) if with_face else None, raw=buf)
 
 
 def _tiles_c(tiles: Sequence[TileT]):
@@ -165,31 +177,23 @@ class FrameSharder:
         else:
             self.packed = alloc_planes(self.cap, self.device, with_rgb)
             self.frame = alloc_planes(W * H, self.device, with_rgb) if rank == root else None
-            if rank == root:
-                self.gbuf = [torch.empty(self.cap * 4, dtype=torch.uint8, device=self.device) for _ in range(world)]
-                self.gbuf_rgb = ([torch.empty((self.cap, 3), dtype=torch.float64, device=self.device)
-                                  for _ in range(world)] if with_rgb else None)
 
     def render(self, frame_and_keep) -> None:
         """Enqueue one frame on torch's current stream (no host sync)."""
         import torch
-        import torch.distributed as dist
         s = torch.cuda.current_stream(self.device).cuda_stream
         if self.world == 1:
             trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.tiles_all, self.frame, s)
             return
         trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.mine, self.packed, s)
-        base = self.packed.rgb8.view(-1)
-        flat = torch.as_strided(base, (self.cap * 4,), (1,))  # rgb8 ++ valid share storage
-        dist.gather(flat, self.gbuf if self.rank == self.root else None, dst=self.root, group=self.group)
-        if self.with_rgb:
-            dist.gather(self.packed.rgb, self.gbuf_rgb if self.rank == self.root else None, dst=self.root,
-                        group=self.group)
+        got = gather_packed(self.packed.raw, self.world, self.rank, self.root, self.group)
+        got_rgb = (gather_packed(self.packed.rgb, self.world, self.rank, self.root, self.group)
+                   if self.with_rgb else None)
         if self.rank == self.root:
+            n = self.cap
             for r in range(self.world):
                 tiles_r = assign(self.tiles_all, self.world, r)
-                n = self.cap
-                buf = self.gbuf[r]
+                buf = got[r]
                 src = DevicePlanes(rgb8=buf[: n * 3].view(n, 3), valid=buf[n * 3:],
-                                   rgb=self.gbuf_rgb[r] if self.with_rgb else None)
+                                   rgb=got_rgb[r] if got_rgb is not None else None)
                 unpack_device(self.ctx, self.W, self.H, tiles_r, src, self.frame, s)
