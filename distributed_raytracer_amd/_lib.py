@@ -22,6 +22,7 @@ MIRT_E_IO = -7
 MIRT_MAX_OBJECTS = 16
 MIRT_MAX_LIGHTS = 16
 MIRT_OPT_NO_PREFILTER = 1
+MIRT_OPT_BRUTE_FORCE = 2
 
 D3 = C.c_double * 3
 

@@ -1,28 +1,37 @@
 // kernels.hip — CDNA4 (gfx950) kernels of the trace worker.
 //
 // Replaces, per pixel of a tile, worker/shared/tracer/tracer.go:81-91 Trace:
-//   k_primary   pixelToPoint + primary dir (tracer.go:15-22, 83-86), brute-force
-//               nearest hit over every triangle of every object (tracer.go:27-50,
-//               object.go:63-110, triangle.go:37-77), miss outputs, hit compaction.
-//   k_secondary shadow rays of phong (tracer.go:60-64): one lane per (hit, light), or
+//   k_primary   pixelToPoint + primary dir (tracer.go:15-22, 83-86), nearest hit over
+//               every object (tracer.go:27-50, object.go:63-110, triangle.go:37-77),
+//               miss outputs, wave-aggregated compaction of the hits.
+//   k_secondary shadow rays of phong (tracer.go:60-64): one lane per (hit, light); or
 //               arbitrary rays for mirt_trace_rays (tracer.go:27-50).
-//   k_shade     Phong (tracer.go:53-77) with the colour clamping of colour.go:38-50 and
-//               uint8(255*c) packing (colour.go:59-61, worker/distributed/main.go:79-86).
+//   k_shade     Phong (tracer.go:53-77) with colour.go:38-50 clamping and the
+//               uint8(255*c) packing of worker/distributed/main.go:79-86.
 //   k_unpack    framebuffer assembly after the multi-GPU gather.
 //
-// Mapping: one lane = one ray, wave64 over an 8x8 pixel block (coherent branches).
-// Triangles are staged cooperatively into LDS (72 B each) and read wave-uniformly, i.e.
-// as LDS broadcasts; meshes of <= kLdsTris triangles stay LDS-resident for the life of
-// a persistent workgroup.  The running nearest hit is a per-lane (distance, face) pair;
-// the winner's normal/material are recomputed once after the sweep (bit-identical).
+// Mapping: one lane = one ray; a wave traces an 8x8 pixel block (coherent rays).
+// Triangles are read wave-uniformly (LDS broadcast when the mesh is LDS-resident).
+// Two sweep modes per object:
+//   kModeBrute  every triangle, in LDS batches (the north star's brute force);
+//   kModeBvh    (default) the whole wave walks the mesh's BVH together (packet
+//               traversal, stackless skip pointers, wave-uniform node loads); a node is
+//               entered when ANY lane's ray hits its inflated box.  Culling never
+//               changes a result: boxes are inflated far beyond the fp64 rounding of
+//               both tests, and the nearest rule is order-free (below).
 //
-// Numerics: fp64, built with -ffp-contract=off, the reference's operation order, true
-// IEEE division, correctly rounded sqrt.  Hit/miss and the nearest-hit choice are
-// therefore bit-identical to the CPU restatement.
+// Numerics: fp64, -ffp-contract=off, the reference's operation order, true IEEE
+// division, correctly rounded sqrt.  Hit/miss, the winning face and the colour are
+// bit-identical to the CPU restatement (oracle/rt_oracle.c).
 #include "gomath.hpp"
 #include "mirt_internal.hpp"
 
 namespace mirt {
+
+// Wave-uniform reads of immutable device data (BVH nodes, triangles streamed from HBM)
+// go through the constant address space so hipcc emits scalar s_load into SGPRs.
+typedef const __attribute__((address_space(4))) double* cdptr;
+typedef const __attribute__((address_space(4))) BvhNode* cnptr;
 
 __device__ __forceinline__ V3 vload(const double* p) { return V3{p[0], p[1], p[2]}; }
 __device__ __forceinline__ void vstore(double* p, V3 v) {
@@ -32,19 +41,17 @@ __device__ __forceinline__ void vstore(double* p, V3 v) {
 }
 
 // Sound pre-reject for the first barycentric test of triangle.go:50-53:
-//   r2 = fl(n / d);  test 0 <= r2 <= 1.
-// Returns true only when that test certainly FAILS, without dividing.  Valid for
-// 2^-900 <= |d| <= 2^900 (outside: never rejects, the exact path decides):
-//  * opposite signs and |n| * 2^1000 > |d|: q < -2^-1000, so fl(q) < 0 (not -0);
-//  * same signs and |n| > fl(|d| (1 + 2^-50)) >= |d| (1 + 2^-51): fl(q) > 1.
-// Scaling by 2^1000 is exact (or overflows to +inf, which is also a correct reject).
+//   r2 = fl(n / d);  test 0 <= r2 <= 1   (d finite, non-zero).
+// Returns true only when that test certainly FAILS, without dividing:
+//  * n * copysign(2^1000, d) < -|d|  <=>  n, d of opposite signs and |n| 2^1000 > |d|,
+//    i.e. q < -2^-1000: fl(q) is negative and not -0.  The product is exact, or
+//    overflows to -inf, which only happens when |q| > 2^-1000 as well.
+//  * |n| > fl(|d| (1 + 2^-50)): |q| > 1 + 2^-51, so fl(q) is outside [-1, 1] — out
+//    whatever the sign.  For a subnormal |d| the product may round to |d|, and then
+//    |n| > |d| already means |q| >= 1 + 2^-52; overflow to +inf never rejects.
 __device__ __forceinline__ bool r2_certainly_out(double n, double d) {
-    double an = __builtin_fabs(n), ad = __builtin_fabs(d);
-    bool in_range = ad >= 0x1p-900 && ad <= 0x1p900;
-    bool opp = (n < 0.0) != (d < 0.0);
-    bool neg_out = n != 0.0 && opp && an * 0x1p1000 > ad;
-    bool big_out = !opp && an > ad * (1.0 + 0x1p-50);
-    return in_range && (neg_out || big_out);
+    const double k = __builtin_copysign(0x1p1000, d);
+    return (n * k < -__builtin_fabs(d)) | (__builtin_fabs(n) > __builtin_fabs(d) * (1.0 + 0x1p-50));
 }
 
 // Möller–Trumbore exactly as triangle.go:37-77, on (p1or = O - P1, E1, E2), returning
@@ -95,8 +102,8 @@ __device__ __forceinline__ bool mt_full(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
     return false;
 }
 
-// Stage triangles [base, base+n) of a mesh into LDS.  REL: store p1or = ro - P1 instead
-// of P1 (primary rays share one origin per object, so object.go:71 + triangle.go:48's
+// Stage triangles [base, base+n) into LDS.  REL: store p1or = ro - P1 instead of P1
+// (primary rays share one origin per object, so object.go:71 + triangle.go:48's
 // subtraction is done once per triangle instead of once per ray; same fp64 value).
 template <bool REL>
 __device__ __forceinline__ void stage_tris(double* __restrict__ s, const double* __restrict__ g, uint32_t base,
@@ -118,27 +125,132 @@ __device__ __forceinline__ void stage_tris(double* __restrict__ s, const double*
     }
 }
 
-// Sweep n staged triangles for one ray; object.go:97-103 nearest rule (strict <, the
-// first face reaching the minimum distance wins in ascending face order).
-template <bool REL, bool PREFILTER>
-__device__ __forceinline__ void sweep(const double* __restrict__ s, uint32_t n, uint32_t base, V3 ro, V3 d, V3 neg,
-                                      bool& has, double& bestd, uint32_t& bface) {
+// Nearest-hit state of one object sweep.  object.go:97-103 keeps the first candidate
+// (in its iteration order) reaching the minimum distance, with strict `<`.  With faces
+// visited in ascending index order that is: the lowest face index among the hits at
+// the minimum distance — except that a NaN distance on the lowest-indexed hit wins (no
+// later `<` beats NaN) and a NaN anywhere else never wins.  `consider` computes exactly
+// that in ANY visiting order, so culling/reordering cannot change the result.
+struct Best {
+    bool has;          // any non-NaN hit
+    double d;          // its minimum distance
+    uint32_t face;     // lowest original face index at that distance
+    uint32_t pos;      // its position in the BVH-ordered arrays
+    uint32_t first;    // lowest original face index of any hit (0xffffffff: none)
+    uint32_t first_pos;
+    bool first_nan;    // that hit's distance is NaN
+};
+__device__ __forceinline__ void best_init(Best& b) {
+    b.has = false;
+    b.d = 0;
+    b.face = b.pos = 0;
+    b.first = 0xffffffffu;
+    b.first_pos = 0;
+    b.first_nan = false;
+}
+__device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
+    const bool isnan_d = dist != dist;
+    if (face < b.first) {
+        b.first = face;
+        b.first_pos = pos;
+        b.first_nan = isnan_d;
+    }
+    if (!isnan_d && (!b.has || dist < b.d || (dist == b.d && face < b.face))) {
+        b.has = true;
+        b.d = dist;
+        b.face = face;
+        b.pos = pos;
+    }
+}
+__device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint32_t& pos) {
+    if (b.first == 0xffffffffu) return false;
+    if (b.first_nan || !b.has) {
+        face = b.first;
+        pos = b.first_pos;
+    } else {
+        face = b.face;
+        pos = b.pos;
+    }
+    return true;
+}
+
+// Test n triangles at positions pos0.. of the BVH-ordered arrays; `src` points at the
+// record of position pos0 (in LDS or in HBM).
+template <bool REL, bool PREFILTER, typename SrcPtr>
+__device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
+                                           uint32_t n, V3 ro, V3 d, V3 neg, Best& b) {
 #pragma unroll 2
-    for (uint32_t k = 0; k < n; ++k) {
-        const double* t = s + (size_t)k * kTriD;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t k = pos0 + i;
+        const auto t = src + (size_t)i * kTriD;
         V3 p1or = REL ? V3{t[0], t[1], t[2]} : sub(ro, V3{t[0], t[1], t[2]});
         V3 e1{t[3], t[4], t[5]};
         V3 e2{t[6], t[7], t[8]};
         double tt;
         if (mt_test<PREFILTER>(p1or, e1, e2, neg, tt)) {
-            V3 ip = add(ro, scale(d, tt));         // triangle.go:69
-            double dist = len(sub(ro, ip));        // object.go:97
-            if (!has || dist < bestd) {
-                has = true;
-                bestd = dist;
-                bface = base + k;
-            }
+            V3 ip = add(ro, scale(d, tt));  // triangle.go:69
+            consider(b, len(sub(ro, ip)), fidx[k], k);  // object.go:97
         }
+    }
+}
+
+// Per-ray slab-test constants: 1/D with zero/subnormal components replaced by a huge
+// finite value of the same sign, so (bound - origin) * inv is never 0 * inf = NaN.
+__device__ __forceinline__ V3 ray_inv(V3 d) {
+    V3 r{1.0 / d.x, 1.0 / d.y, 1.0 / d.z};
+    r.x = __builtin_fabs(r.x) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.x) : r.x;
+    r.y = __builtin_fabs(r.y) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.y) : r.y;
+    r.z = __builtin_fabs(r.z) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.z) : r.z;
+    return r;
+}
+__device__ __forceinline__ BvhNode load_node(cnptr p) {
+    BvhNode n;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        n.lo[k] = p->lo[k];
+        n.hi[k] = p->hi[k];
+    }
+    n.skip = p->skip;
+    n.first = p->first;
+    n.count = p->count;
+    n.pad = 0;
+    return n;
+}
+
+// Ray vs inflated node box, t >= 0 half-line.
+__device__ __forceinline__ bool slab_hit(const BvhNode& nd, V3 ro, V3 inv) {
+    const double ax = (nd.lo[0] - ro.x) * inv.x, bx = (nd.hi[0] - ro.x) * inv.x;
+    const double ay = (nd.lo[1] - ro.y) * inv.y, by = (nd.hi[1] - ro.y) * inv.y;
+    const double az = (nd.lo[2] - ro.z) * inv.z, bz = (nd.hi[2] - ro.z) * inv.z;
+    const double tn = fmax(fmax(fmin(ax, bx), fmin(ay, by)), fmax(fmin(az, bz), 0.0));
+    const double tf = fmin(fmin(fmax(ax, bx), fmax(ay, by)), fmax(az, bz));
+    return tn <= tf;
+}
+
+// Wave-uniform stackless BVH walk over one object's mesh.  `lane_on`: this lane has a
+// ray to trace.  Lanes whose origin is far from the mesh (beyond cull_limit) never cull.
+template <bool REL, bool PREFILTER, typename SrcPtr>
+__device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on,
+                                          Best& b) {
+    const V3 inv = ray_inv(d);
+    const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+    const bool force = lane_on && !(far <= m.cull_limit);
+    uint32_t ni = 0;
+    const uint32_t nn = m.nnodes;
+    while (ni < nn) {
+        ni = __builtin_amdgcn_readfirstlane(ni);
+        const BvhNode nd = load_node((cnptr)m.nodes + ni);
+        const bool want = force || (lane_on && slab_hit(nd, ro, inv));
+        if (__ballot(want) == 0) {
+            ni = nd.skip;
+            continue;
+        }
+        if (nd.count == 0) {
+            ++ni;  // depth-first layout: the left child follows its parent
+            continue;
+        }
+        test_range<REL, PREFILTER>(src + (size_t)nd.first * kTriD, m.fidx, nd.first, nd.count, ro, d, neg, b);
+        ni = nd.skip;
     }
 }
 
@@ -150,9 +262,9 @@ struct Nearest {
 
 // Winner recompute for one object: world hit, normal (InterpNormal or Normal),
 // material.  Same arithmetic as the sweep, so the same hit point.
-__device__ __forceinline__ void winner(const DevObject& ob, uint32_t f, V3 ro, V3 d, V3 neg, V3& world,
+__device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro, V3 d, V3 neg, V3& world,
                                        V3& normal, uint32_t& mat, bool want_normal) {
-    const double* t = ob.m.tri + (size_t)f * kTriD;
+    const double* t = ob.m.tri + (size_t)pos * kTriD;
     V3 p1 = vload(t), e1 = vload(t + 3), e2 = vload(t + 6);
     double tt = 0, r1 = 0, r2 = 0, r3 = 0;
     mt_full(sub(ro, p1), e1, e2, neg, tt, r1, r2, r3);
@@ -160,22 +272,24 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t f, V3 ro, V
     world = add(ip, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:109
     if (want_normal) {
         if (ob.m.has_normals) {
-            const double* nn = ob.m.vnrm + (size_t)f * kTriD;
+            const double* nn = ob.m.vnrm + (size_t)pos * kTriD;
             // triangle.go:29-31: ((N1*r1 + N2*r2) + N3*r3).Norm()
             normal = norm(add(add(scale(vload(nn), r1), scale(vload(nn + 3), r2)), scale(vload(nn + 6), r3)));
         } else {
             // triangle.go:24-26: (P2-P1) x (P3-P1) normalised
             normal = norm(cross(e1, e2));
         }
-        mat = ob.m.fmat[f];
+        mat = ob.m.fmat[pos];
     }
 }
 
-// tracer.go:27-50: nearest over objects by |hit - Cam.Pos| (also for shadow rays).
-// REL (primary rays only) requires every lane of the workgroup to share `o`.
-template <bool REL, bool PREFILTER>
+// tracer.go:27-50: nearest over objects by |hit - Cam.Pos| (also for shadow rays),
+// first object in order wins ties (strict <).
+//   RESIDENT: object 0's mesh sits in LDS (`lds`), relative (p1or) when REL.
+//   BRUTE:    sweep every triangle instead of walking the BVH.
+template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool want_normal) {
+                                 bool lane_on, bool want_normal) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -186,31 +300,37 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
     for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
         const DevObject& ob = fa.obj[oi];
         V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
-        bool has = false;
-        double bestd = 0;
-        uint32_t bface = 0;
+        Best b;
+        best_init(b);
         const uint32_t ntri = ob.m.ntri;
         if (resident) {
-            sweep<REL, PREFILTER>(lds, ntri, 0, ro, d, neg, has, bestd, bface);
-        } else {
+            if (BRUTE)
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b);
+            else
+                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b);
+        } else if (BRUTE) {
+            // stream the mesh through LDS in batches (every lane of the workgroup joins)
             for (uint32_t base = 0; base < ntri; base += kLdsTris) {
                 uint32_t n = min((uint32_t)kLdsTris, ntri - base);
                 __syncthreads();
                 stage_tris<REL>(lds, ob.m.tri, base, n, ro);
                 __syncthreads();
-                sweep<REL, PREFILTER>(lds, n, base, ro, d, neg, has, bestd, bface);
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b);
             }
+        } else {
+            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b);
         }
-        if (has) {
+        uint32_t face, pos;
+        if (best_result(b, face, pos)) {
             V3 world, normal{0, 0, 0};
             uint32_t mat = 0;
-            winner(ob, bface, ro, d, neg, world, normal, mat, want_normal);
+            winner(ob, pos, ro, d, neg, world, normal, mat, want_normal);
             double cd = len(sub(world, cam));  // tracer.go:38
             if (!best.ok || cd < bestcd) {
                 best.ok = true;
                 bestcd = cd;
                 best.obj = oi;
-                best.face = bface;
+                best.face = face;
                 best.mat = mat;
                 best.hit = world;
                 best.normal = normal;
@@ -233,14 +353,15 @@ __device__ __forceinline__ uint32_t find_tile(const TileDesc* __restrict__ tiles
 }
 
 // ---------------------------------------------------------------- primary
-template <bool PREFILTER>
+// RESIDENT (host-decided): one object whose mesh fits in LDS; it is staged once per
+// persistent workgroup, relative to the camera (p1or), and every sweep reads LDS.
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const TileDesc* __restrict__ tiles,
                                                      uint32_t ntiles, uint32_t total_units, OutPlanes out,
                                                      HitRec* __restrict__ hits, uint32_t* __restrict__ counters) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    const bool resident = fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    if (resident) {
+    if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
         __syncthreads();
@@ -264,7 +385,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
                    scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
         V3 d = norm(sub(p, cam));
 
-        Nearest nh = trace_nearest<true, PREFILTER>(fa, lds, resident, cam, d, true);
+        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true);
 
         const uint64_t oidx = td.out_off + (uint64_t)lx * td.h + ly;
         const bool is_hit = active && nh.ok;
@@ -307,13 +428,12 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
 }
 
 // ---------------------------------------------------------------- secondary rays
-template <int MODE, bool PREFILTER>
+template <int MODE, bool PREFILTER, bool BRUTE, bool RESIDENT>
 __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const HitRec* __restrict__ hits,
                                                        const uint32_t* __restrict__ counters,
                                                        uint8_t* __restrict__ lit, RayIO io) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    const bool resident = fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
-    if (resident) {
+    if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
@@ -341,7 +461,7 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
                 d = vload(io.dir + 3 * item);
             }
         }
-        Nearest r = trace_nearest<false, PREFILTER>(fa, lds, resident, o, d, MODE == kModeRays);
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays);
         if (active) {
             if (MODE == kModeShadow) {
                 // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
@@ -445,38 +565,57 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_debug_fp64, dim3((n + 255) / 256), dim3(256), 0, s, op, n, a, b, out);
-    return hipGetLastError();
+// opts: MIRT_OPT_* bits (mirt.h)
+// opts: MIRT_OPT_* bits (mirt.h); resident: one object whose mesh fits in LDS.
+#define MIRT_DISPATCH(KERNEL)                                                                      \
+    do {                                                                                           \
+        const bool pre = !(opts & MIRT_OPT_NO_PREFILTER), brute = (opts & MIRT_OPT_BRUTE_FORCE) != 0; \
+        if (resident) {                                                                            \
+            if (pre && !brute) KERNEL(true, false, true);                                          \
+            else if (pre) KERNEL(true, true, true);                                                \
+            else if (!brute) KERNEL(false, false, true);                                           \
+            else KERNEL(false, true, true);                                                        \
+        } else {                                                                                   \
+            if (pre && !brute) KERNEL(true, false, false);                                         \
+            else if (pre) KERNEL(true, true, false);                                               \
+            else if (!brute) KERNEL(false, false, false);                                          \
+            else KERNEL(false, true, false);                                                       \
+        }                                                                                          \
+    } while (0)
+
+static bool is_resident(const FrameArgs& fa) {
+    return fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
 }
 
 hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, bool prefilter,
+                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, uint32_t opts,
                           hipStream_t s) {
-    if (prefilter)
-        hipLaunchKernelGGL(k_primary<true>, dim3(grid), dim3(kWG), 0, s, fa, tiles, ntiles, total_units, out, hits,
-                           counters);
-    else
-        hipLaunchKernelGGL(k_primary<false>, dim3(grid), dim3(kWG), 0, s, fa, tiles, ntiles, total_units, out, hits,
-                           counters);
+    const bool resident = is_resident(fa);
+#define K_PRIM(P, B, R) \
+    hipLaunchKernelGGL((k_primary<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, tiles, ntiles, total_units, out, hits, counters)
+    MIRT_DISPATCH(K_PRIM);
+#undef K_PRIM
     return hipGetLastError();
 }
 
 hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, uint8_t* lit, int grid,
-                         bool prefilter, hipStream_t s) {
+                         uint32_t opts, hipStream_t s) {
     RayIO none{};
-    if (prefilter)
-        hipLaunchKernelGGL((k_secondary<kModeShadow, true>), dim3(grid), dim3(kWG), 0, s, fa, hits, counters, lit,
-                           none);
-    else
-        hipLaunchKernelGGL((k_secondary<kModeShadow, false>), dim3(grid), dim3(kWG), 0, s, fa, hits, counters, lit,
-                           none);
+    const bool resident = is_resident(fa);
+#define K_SHADOW(P, B, R) \
+    hipLaunchKernelGGL((k_secondary<kModeShadow, P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, hits, counters, lit, none)
+    MIRT_DISPATCH(K_SHADOW);
+#undef K_SHADOW
     return hipGetLastError();
 }
 
-hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_secondary<kModeRays, true>), dim3(grid), dim3(kWG), 0, s, fa, (const HitRec*)nullptr,
-                       (const uint32_t*)nullptr, (uint8_t*)nullptr, io);
+hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s) {
+    const bool resident = is_resident(fa);
+#define K_RAYS(P, B, R)                                                                                        \
+    hipLaunchKernelGGL((k_secondary<kModeRays, P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, (const HitRec*)nullptr, \
+                       (const uint32_t*)nullptr, (uint8_t*)nullptr, io)
+    MIRT_DISPATCH(K_RAYS);
+#undef K_RAYS
     return hipGetLastError();
 }
 
@@ -491,6 +630,11 @@ hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, 
     uint64_t blocks = (npix + 255) / 256;
     int grid = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
     hipLaunchKernelGGL(k_unpack, dim3(grid), dim3(256), 0, s, tiles, ntiles, npix, H, src, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_fp64, dim3((n + 255) / 256), dim3(256), 0, s, op, n, a, b, out);
     return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 #include "../../include/mirt.h"
 #include "gomath.hpp"
 #include "mirt_internal.hpp"
+#include "bvh.hpp"
 
 using namespace mirt;
 
@@ -43,8 +44,11 @@ struct MeshDev {
     double* tri = nullptr;
     double* vnrm = nullptr;
     uint32_t* fmat = nullptr;
+    uint32_t* fidx = nullptr;
+    BvhNode* nodes = nullptr;
     double* mats = nullptr;
-    uint32_t ntri = 0, nmat = 0;
+    uint32_t ntri = 0, nmat = 0, nnodes = 0;
+    double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
     bool has_normals = false;
     bool live = false;
 };
@@ -90,6 +94,12 @@ struct mirt_ctx {
 };
 
 namespace {
+
+void mesh_free(MeshDev& m) {
+    for (void* p : {(void*)m.tri, (void*)m.vnrm, (void*)m.fmat, (void*)m.fidx, (void*)m.nodes, (void*)m.mats})
+        if (p) (void)hipFree(p);
+    m = MeshDev();
+}
 
 template <class T>
 int dev_grow(T*& p, size_t& cap, size_t need) {
@@ -200,6 +210,10 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         o.m.tri = m.tri;
         o.m.vnrm = m.vnrm;
         o.m.fmat = m.fmat;
+        o.m.fidx = m.fidx;
+        o.m.nodes = m.nodes;
+        o.m.nnodes = m.nnodes;
+        o.m.cull_limit = 256.0 * m.scale;
         o.m.mats = m.mats;
         o.m.ntri = m.ntri;
         o.m.has_normals = m.has_normals ? 1u : 0u;
@@ -266,18 +280,17 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 
     HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(uint32_t), s));
-    const bool pre = !(c->flags & MIRT_OPT_NO_PREFILTER);
     const int pgrid = (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(f->n_lights, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((pixels + 255) / 256, (uint64_t)8 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    HIP_TRY(launch_primary(fa, sl->d_tiles, n, units, out, sl->hits, sl->counters, pgrid, pre, s));
+    HIP_TRY(launch_primary(fa, sl->d_tiles, n, units, out, sl->hits, sl->counters, pgrid, c->flags, s));
     if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (f->n_lights) {
-        HIP_TRY(launch_shadow(fa, sl->hits, sl->counters, sl->lit, sgrid, pre, s));
+        HIP_TRY(launch_shadow(fa, sl->hits, sl->counters, sl->lit, sgrid, c->flags, s));
     }
     if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
@@ -357,12 +370,7 @@ void mirt_destroy(mirt_ctx* c) {
                 if (e) (void)hipEventDestroy(e);
             if (r.h_hits) (void)hipHostFree(r.h_hits);
         }
-    for (auto& m : c->meshes) {
-        if (m.tri) (void)hipFree(m.tri);
-        if (m.vnrm) (void)hipFree(m.vnrm);
-        if (m.fmat) (void)hipFree(m.fmat);
-        if (m.mats) (void)hipFree(m.mats);
-    }
+    for (auto& m : c->meshes) mesh_free(m);
     delete c;
 }
 
@@ -442,14 +450,22 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         if (fmat[f] >= nm) return fail(MIRT_E_INVALID, "face " + std::to_string(f) + " material out of range");
     }
     HIP_TRY(hipSetDevice(c->device));
+    // Culling structure: BVH over the faces, boxes inflated by 2^-24 of the mesh's
+    // largest |coordinate|.  All per-face arrays are stored in BVH order.
+    double scale = 0;
+    for (size_t i = 0; i < (size_t)nv * 3; ++i) scale = std::max(scale, std::fabs(v[i]));
+    scale = std::max(scale, 1e-300);
+    BvhBuild bvh = build_bvh(v, fv, nf, std::ldexp(scale, -24));
     // P1, E1 = P2 - P1, E2 = P3 - P1 (triangle.go:38: single fp64 subtractions, so the
     // precomputed edges are bit-identical to the per-test ones of the reference).
     std::vector<double> tri((size_t)nf * kTriD), vnrm(has_n ? (size_t)nf * kTriD : 0), mt((size_t)nm * 10);
-    for (uint32_t f = 0; f < nf; ++f) {
+    std::vector<uint32_t> fm(nf);
+    for (uint32_t pos = 0; pos < nf; ++pos) {
+        const uint32_t f = bvh.order[pos];
         const double* p1 = v + 3 * (size_t)fv[3 * f];
         const double* p2 = v + 3 * (size_t)fv[3 * f + 1];
         const double* p3 = v + 3 * (size_t)fv[3 * f + 2];
-        double* t = &tri[(size_t)f * kTriD];
+        double* t = &tri[(size_t)pos * kTriD];
         for (int k = 0; k < 3; ++k) {
             t[k] = p1[k];
             t[3 + k] = p2[k] - p1[k];
@@ -457,7 +473,8 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         }
         if (has_n)
             for (int q = 0; q < 3; ++q)
-                for (int k = 0; k < 3; ++k) vnrm[(size_t)f * kTriD + 3 * q + k] = vn[3 * (size_t)fn[3 * f + q] + k];
+                for (int k = 0; k < 3; ++k) vnrm[(size_t)pos * kTriD + 3 * q + k] = vn[3 * (size_t)fn[3 * f + q] + k];
+        fm[pos] = fmat[f];
     }
     for (uint32_t m = 0; m < nm; ++m) {
         for (int k = 0; k < 3; ++k) {
@@ -471,6 +488,8 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     md.ntri = nf;
     md.nmat = nm;
     md.has_normals = has_n;
+    md.nnodes = (uint32_t)bvh.nodes.size();
+    md.scale = scale;
     auto upload = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return MIRT_OK;
         hipError_t e = hipMalloc(dst, bytes);
@@ -480,10 +499,15 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         return MIRT_OK;
     };
     int r;
-    if ((r = upload((void**)&md.tri, tri.data(), tri.size() * 8)) != MIRT_OK) return r;
-    if ((r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK) return r;
-    if ((r = upload((void**)&md.fmat, fmat, (size_t)nf * 4)) != MIRT_OK) return r;
-    if ((r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) return r;
+    if ((r = upload((void**)&md.tri, tri.data(), tri.size() * 8)) != MIRT_OK ||
+        (r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK ||
+        (r = upload((void**)&md.fmat, fm.data(), (size_t)nf * 4)) != MIRT_OK ||
+        (r = upload((void**)&md.fidx, bvh.order.data(), (size_t)nf * 4)) != MIRT_OK ||
+        (r = upload((void**)&md.nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(BvhNode))) != MIRT_OK ||
+        (r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) {
+        mesh_free(md);
+        return r;
+    }
     md.live = true;
     std::lock_guard<std::mutex> g(c->mu);
     *mesh_id = (uint32_t)c->meshes.size();
@@ -497,12 +521,7 @@ int mirt_mesh_release(mirt_ctx* c, uint32_t id) {
     if (id >= c->meshes.size() || !c->meshes[id].live) return fail(MIRT_E_INVALID, "unknown mesh id");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    MeshDev& m = c->meshes[id];
-    if (m.tri) (void)hipFree(m.tri);
-    if (m.vnrm) (void)hipFree(m.vnrm);
-    if (m.fmat) (void)hipFree(m.fmat);
-    if (m.mats) (void)hipFree(m.mats);
-    m = MeshDev();
+    mesh_free(c->meshes[id]);
     return MIRT_OK;
 }
 
@@ -646,7 +665,7 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* 
     HIP_TRY(hipMemcpyAsync((void*)io.orig, orig, (size_t)n * 24, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync((void*)io.dir, dir, (size_t)n * 24, hipMemcpyHostToDevice, s));
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n + kWG - 1) / kWG, 2 * (uint64_t)c->cus));
-    HIP_TRY(launch_rays(fa, io, grid, s));
+    HIP_TRY(launch_rays(fa, io, grid, c->flags, s));
     HIP_TRY(hipMemcpyAsync(ok, io.ok, n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(hit, io.hit, (size_t)n * 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(normal, io.normal, (size_t)n * 24, hipMemcpyDeviceToHost, s));

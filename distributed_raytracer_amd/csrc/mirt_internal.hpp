@@ -19,15 +19,39 @@ constexpr int kTriD = 9;
 // larger meshes stream through it in batches of this size.
 constexpr int kLdsTris = 1024;
 
-// One uploaded mesh, device pointers (shared/state/mesh.go:100-106).
+// BVH node (64 B), nodes in depth-first order: an inner node's left child is the next
+// node; `skip` is the first node after this node's subtree (stackless traversal).
+// Boxes are inflated so that a ray the fp64 Möller–Trumbore test could report as a hit
+// always passes the box test (see DESIGN.md §4 "Exact culling").
+struct BvhNode {
+    double lo[3], hi[3];
+    uint32_t skip;
+    uint32_t first;   // first triangle (position in the BVH-ordered arrays)
+    uint32_t count;   // 0 for an inner node
+    uint32_t pad;
+};
+constexpr int kBvhLeaf = 8;  // max triangles per leaf
+
+// One uploaded mesh, device pointers (shared/state/mesh.go:100-106).  Every per-face
+// array is stored in BVH leaf order; fidx maps a position back to the face index of
+// the uploaded mesh (reported outputs and tie-breaking use that original index).
 struct DevMesh {
     const double* tri;       // ntri * 9 : P1, E1, E2
     const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
     const uint32_t* fmat;    // ntri     : material index
+    const uint32_t* fidx;    // ntri     : original face index
+    const BvhNode* nodes;    // nnodes
     const double* mats;      // nmat * 10: ka[3] kd[3] ks[3] ns
     uint32_t ntri;
     uint32_t has_normals;
+    uint32_t nnodes;
+    uint32_t pad;
+    double cull_limit;       // rays whose object-space origin has a coordinate beyond this
+                             // are never culled (tolerance scales with |origin|)
 };
+
+// Kernel modes (mirt_set_options): exact BVH culling (default) or brute force.
+enum TraceMode { kModeBvh = 0, kModeBrute = 1 };
 
 struct DevObject {
     DevMesh m;
@@ -88,13 +112,13 @@ struct RayIO {
 };
 
 hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, bool prefilter,
+                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, uint8_t* lit,
-                         int grid, bool prefilter, hipStream_t s);
+                         int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, const uint8_t* lit,
                         const OutPlanes& out, uint64_t lit_stride, int grid, hipStream_t s);
-hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, hipStream_t s);
+hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);

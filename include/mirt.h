@@ -201,6 +201,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 
 /* Ask for kernel variants (benchmark ablations).  0 = defaults. */
 #define MIRT_OPT_NO_PREFILTER 1u  /* always take the true fp64 divide for r2 */
+#define MIRT_OPT_BRUTE_FORCE 2u   /* test every triangle (no BVH culling), mesh streamed via LDS */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*
