@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
+    ap.add_argument("--brute-force", action="store_true",
+                    help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes of k_primary from a rocprofv3 --pmc pass (see profiles/)")
     return ap.parse_args()
@@ -96,8 +98,9 @@ def main():
 
     W, H = a.width, a.height
     ctx = rt.Context(local)
-    if a.no_prefilter:
-        ctx.set_options(rt._lib.MIRT_OPT_NO_PREFILTER)
+    opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
+        rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0)
+    ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     frame = env.mutable().to_frame()
     tris = sum(len(m.face_v) for m in env.meshes)
@@ -170,10 +173,12 @@ def main():
             "config": {"workload": f"suzanne.obj {W}x{H}, primary + one shadow ray per light (3) + Phong "
                                    f"(BASELINE configs[1])", "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
-                                                                                if world > 1 else "")},
+                                                                                if world > 1 else ""),
+                       "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
             "primary_mrays_s": round(primary / steps / (ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
             "hits_per_frame": int(hits / steps),
+            "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / launches),
             "ms_kernels": {"primary": round(prim_ms, 4),
                            "shadow": round(prof["shadow_ms_sum"] / launches, 4),
                            "shade": round(prof["shade_ms_sum"] / launches, 4),
@@ -182,8 +187,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_primary", "bytes_per_unit": BYTES_PER_TRI_TEST,
                          "units_per_launch": int(prim_tests),
-                         "note": "algorithmic bytes (72 B fp64 triangle record per ray-triangle test); the mesh is "
-                                 "LDS-resident so the real bound is fp64 VALU, see DESIGN.md"},
+                         "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
+                                 "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
+                                 "VALU, see DESIGN.md"},
         }
         if not a.no_parity:
             fr = sh.frame

@@ -178,7 +178,8 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
 // record of position pos0 (in LDS or in HBM).
 template <bool REL, bool PREFILTER, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
-                                           uint32_t n, V3 ro, V3 d, V3 neg, Best& b) {
+                                           uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests) {
+    wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
 #pragma unroll 2
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t k = pos0 + i;
@@ -231,7 +232,7 @@ __device__ __forceinline__ bool slab_hit(const BvhNode& nd, V3 ro, V3 inv) {
 // ray to trace.  Lanes whose origin is far from the mesh (beyond cull_limit) never cull.
 template <bool REL, bool PREFILTER, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on,
-                                          Best& b) {
+                                          Best& b, uint32_t& wtests) {
     const V3 inv = ray_inv(d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
     const bool force = lane_on && !(far <= m.cull_limit);
@@ -249,7 +250,8 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             ++ni;  // depth-first layout: the left child follows its parent
             continue;
         }
-        test_range<REL, PREFILTER>(src + (size_t)nd.first * kTriD, m.fidx, nd.first, nd.count, ro, d, neg, b);
+        test_range<REL, PREFILTER>(src + (size_t)nd.first * kTriD, m.fidx, nd.first, nd.count, ro, d, neg, b,
+                                   wtests);
         ni = nd.skip;
     }
 }
@@ -289,7 +291,7 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   BRUTE:    sweep every triangle instead of walking the BVH.
 template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal) {
+                                 bool lane_on, bool want_normal, uint32_t& wtests) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -305,9 +307,9 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
         const uint32_t ntri = ob.m.ntri;
         if (resident) {
             if (BRUTE)
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b);
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b, wtests);
             else
-                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b);
+                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b, wtests);
         } else if (BRUTE) {
             // stream the mesh through LDS in batches (every lane of the workgroup joins)
             for (uint32_t base = 0; base < ntri; base += kLdsTris) {
@@ -315,10 +317,10 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
                 __syncthreads();
                 stage_tris<REL>(lds, ob.m.tri, base, n, ro);
                 __syncthreads();
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b);
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b, wtests);
             }
         } else {
-            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b);
+            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, wtests);
         }
         uint32_t face, pos;
         if (best_result(b, face, pos)) {
@@ -358,7 +360,7 @@ __device__ __forceinline__ uint32_t find_tile(const TileDesc* __restrict__ tiles
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const TileDesc* __restrict__ tiles,
                                                      uint32_t ntiles, uint32_t total_units, OutPlanes out,
-                                                     HitRec* __restrict__ hits, uint32_t* __restrict__ counters) {
+                                                     HitRec* __restrict__ hits, cnt_t* __restrict__ counters) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     if (RESIDENT) {
@@ -385,7 +387,10 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
                    scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
         V3 d = norm(sub(p, cam));
 
-        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true);
+        uint32_t wtests = 0;
+        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, wtests);
+        const uint32_t nact = __popcll(__ballot(active));
+        if (lane == 0 && nact) atomicAdd(&counters[kCntPrimTests], (cnt_t)wtests * nact);
 
         const uint64_t oidx = td.out_off + (uint64_t)lx * td.h + ly;
         const bool is_hit = active && nh.ok;
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
             const uint32_t cnt = __popcll(mask);
             const uint32_t leader = __ffsll((unsigned long long)mask) - 1;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&counters[kCntHits], cnt);
+            if (lane == leader) base = (uint32_t)atomicAdd(&counters[kCntHits], (cnt_t)cnt);
             base = __shfl(base, leader);
             if (is_hit) {
                 const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
@@ -430,14 +435,14 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
 // ---------------------------------------------------------------- secondary rays
 template <int MODE, bool PREFILTER, bool BRUTE, bool RESIDENT>
 __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const HitRec* __restrict__ hits,
-                                                       const uint32_t* __restrict__ counters,
+                                                       cnt_t* __restrict__ counters,
                                                        uint8_t* __restrict__ lit, RayIO io) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
-    const uint32_t nh = MODE == kModeShadow ? counters[kCntHits] : io.n;
+    const uint32_t nh = MODE == kModeShadow ? (uint32_t)counters[kCntHits] : io.n;
     const uint64_t items = MODE == kModeShadow ? (uint64_t)nh * fa.n_lights : (uint64_t)io.n;
     const uint64_t nchunks = (items + kWG - 1) / kWG;
     for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -461,7 +466,11 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
                 d = vload(io.dir + 3 * item);
             }
         }
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays);
+        uint32_t wtests = 0;
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays, wtests);
+        const uint32_t nact = __popcll(__ballot(active));
+        if (MODE == kModeShadow && (threadIdx.x & 63) == 0 && nact)
+            atomicAdd(&counters[kCntShadowTests], (cnt_t)wtests * nact);
         if (active) {
             if (MODE == kModeShadow) {
                 // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
@@ -480,9 +489,9 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
 
 // ---------------------------------------------------------------- shade
 __global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const HitRec* __restrict__ hits,
-                                               const uint32_t* __restrict__ counters,
+                                               const cnt_t* __restrict__ counters,
                                                const uint8_t* __restrict__ lit, OutPlanes out) {
-    const uint32_t nh = counters[kCntHits];
+    const uint32_t nh = (uint32_t)counters[kCntHits];
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
         const HitRec hr = hits[h];
@@ -588,7 +597,7 @@ static bool is_resident(const FrameArgs& fa) {
 }
 
 hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, uint32_t opts,
+                          const OutPlanes& out, HitRec* hits, cnt_t* counters, int grid, uint32_t opts,
                           hipStream_t s) {
     const bool resident = is_resident(fa);
 #define K_PRIM(P, B, R) \
@@ -598,7 +607,7 @@ hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t n
     return hipGetLastError();
 }
 
-hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, uint8_t* lit, int grid,
+hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, cnt_t* counters, uint8_t* lit, int grid,
                          uint32_t opts, hipStream_t s) {
     RayIO none{};
     const bool resident = is_resident(fa);
@@ -613,13 +622,13 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
     const bool resident = is_resident(fa);
 #define K_RAYS(P, B, R)                                                                                        \
     hipLaunchKernelGGL((k_secondary<kModeRays, P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, (const HitRec*)nullptr, \
-                       (const uint32_t*)nullptr, (uint8_t*)nullptr, io)
+                       (cnt_t*)nullptr, (uint8_t*)nullptr, io)
     MIRT_DISPATCH(K_RAYS);
 #undef K_RAYS
     return hipGetLastError();
 }
 
-hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, const uint8_t* lit,
+hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const cnt_t* counters, const uint8_t* lit,
                         const OutPlanes& out, uint64_t /*lit_stride*/, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(256), 0, s, fa, hits, counters, lit, out);
     return hipGetLastError();

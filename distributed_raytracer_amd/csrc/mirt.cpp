@@ -62,11 +62,11 @@ struct Slot {
     size_t hits_cap = 0;
     uint8_t* lit = nullptr;
     size_t lit_cap = 0;
-    uint32_t* counters = nullptr;
+    cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
     size_t tiles_cap = 0, h_tiles_cap = 0;
-    uint32_t* h_counters = nullptr;  // pinned
+    cnt_t* h_counters = nullptr;  // pinned
     // device-side outputs for the host-buffer API
     void* out_buf = nullptr;
     size_t out_cap = 0;
@@ -74,7 +74,7 @@ struct Slot {
 
 struct ProfRec {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    uint32_t* h_hits = nullptr;  // pinned, written by an async D2H copy
+    cnt_t* h_cnt = nullptr;  // pinned kCntN counters, written by an async D2H copy
     uint64_t pixels = 0, tris = 0, nl = 0;
 };
 
@@ -129,8 +129,8 @@ int slot_acquire(mirt_ctx* c, Slot*& out) {
     if (!s->stream) {
         HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
-        HIP_TRY(hipMalloc((void**)&s->counters, kCntN * sizeof(uint32_t)));
-        HIP_TRY(hipHostMalloc((void**)&s->h_counters, kCntN * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&s->counters, kCntN * sizeof(cnt_t)));
+        HIP_TRY(hipHostMalloc((void**)&s->h_counters, kCntN * sizeof(cnt_t)));
     }
     // previous asynchronous use of this slot's staging/workspace must be finished
     if (s->pending) {
@@ -235,7 +235,7 @@ int prof_get(mirt_ctx* c, ProfRec& r) {
         return MIRT_OK;
     }
     for (int k = 0; k < 4; ++k) HIP_TRY(hipEventCreate(&r.ev[k]));
-    HIP_TRY(hipHostMalloc((void**)&r.h_hits, sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc((void**)&r.h_cnt, kCntN * sizeof(cnt_t)));
     return MIRT_OK;
 }
 
@@ -279,7 +279,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if (prof && (r = prof_get(c, pr)) != MIRT_OK) return r;
 
     HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(cnt_t), s));
     const int pgrid = (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(f->n_lights, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
@@ -297,7 +297,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     HIP_TRY(launch_shade(fa, sl->hits, sl->counters, sl->lit, out, pixels, hgrid, s));
     if (prof) {
         HIP_TRY(hipEventRecord(pr.ev[3], s));
-        HIP_TRY(hipMemcpyAsync(pr.h_hits, sl->counters + kCntHits, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pr.h_cnt, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
         pr.pixels = pixels;
         pr.tris = tris;
         pr.nl = f->n_lights;
@@ -312,13 +312,13 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 }
 
 int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t nl, mirt_stats* st) {
-    HIP_TRY(hipMemcpyAsync(sl->h_counters, sl->counters, kCntN * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(sl->h_counters, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memset(st, 0, sizeof(*st));
     st->primary_rays = pixels;
     st->hits = sl->h_counters[kCntHits];
     st->shadow_rays = st->hits * nl;
-    st->tri_tests = (st->primary_rays + st->shadow_rays) * tris;
+    st->tri_tests = sl->h_counters[kCntPrimTests] + sl->h_counters[kCntShadowTests];
     return MIRT_OK;
 }
 
@@ -368,7 +368,7 @@ void mirt_destroy(mirt_ctx* c) {
         for (auto& r : *v) {
             for (auto e : r.ev)
                 if (e) (void)hipEventDestroy(e);
-            if (r.h_hits) (void)hipHostFree(r.h_hits);
+            if (r.h_cnt) (void)hipHostFree(r.h_cnt);
         }
     for (auto& m : c->meshes) mesh_free(m);
     delete c;
@@ -702,12 +702,12 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->shadow_ms_sum += b;
         out->shade_ms_sum += d;
         out->frame_ms_sum += t;
-        const uint64_t hits = *r.h_hits;
+        const uint64_t hits = r.h_cnt[kCntHits];
         out->primary_rays += r.pixels;
         out->hits += hits;
         out->shadow_rays += hits * r.nl;
-        out->primary_tri_tests += r.pixels * r.tris;
-        out->shadow_tri_tests += hits * r.nl * r.tris;
+        out->primary_tri_tests += r.h_cnt[kCntPrimTests];
+        out->shadow_tri_tests += r.h_cnt[kCntShadowTests];
     }
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);

@@ -95,7 +95,9 @@ struct OutPlanes {
 };
 
 // Counters kept in device memory per call slot.
-enum { kCntHits = 0, kCntN = 4 };
+// 64-bit: hits, ray-triangle tests performed by the primary / shadow kernels.
+enum { kCntHits = 0, kCntPrimTests = 1, kCntShadowTests = 2, kCntN = 4 };
+typedef unsigned long long cnt_t;
 
 enum SecondaryMode { kModeShadow = 0, kModeRays = 1 };
 
@@ -112,11 +114,11 @@ struct RayIO {
 };
 
 hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, uint32_t* counters, int grid, uint32_t opts,
+                          const OutPlanes& out, HitRec* hits, cnt_t* counters, int grid, uint32_t opts,
                           hipStream_t s);
-hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, uint8_t* lit,
+hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, cnt_t* counters, uint8_t* lit,
                          int grid, uint32_t opts, hipStream_t s);
-hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const uint32_t* counters, const uint8_t* lit,
+hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const cnt_t* counters, const uint8_t* lit,
                         const OutPlanes& out, uint64_t lit_stride, int grid, hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);

@@ -337,8 +337,14 @@ def test_profile_counters(ctx, env):
     rt.draw(env, 320, 240)
     rt.draw(env, 320, 240)
     p = ctx.profile_read()
+    ctx.set_options(rt._lib.MIRT_OPT_BRUTE_FORCE)
+    rt.draw(env, 320, 240)
+    b = ctx.profile_read()
+    ctx.set_options(0)
     ctx.profile_enable(False)
-    assert p["launches"] == 2
+    assert p["launches"] == 2 and b["launches"] == 1
     assert p["primary_rays"] == 2 * 76800 and p["hits"] == 2 * 5820
-    assert p["primary_tri_tests"] == 2 * 76800 * 968
+    # brute force tests every triangle for every ray; the BVH far fewer
+    assert b["primary_tri_tests"] == 76800 * 968 and b["shadow_tri_tests"] == 3 * 5820 * 968
+    assert 0 < p["primary_tri_tests"] < 2 * 76800 * 968 / 5
     assert p["primary_ms_sum"] > 0 and p["frame_ms_sum"] >= p["primary_ms_sum"]
