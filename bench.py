@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
+    ap.add_argument("--nonpersistent", action="store_true", help="ablation: one workgroup per primary unit")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
@@ -99,7 +100,7 @@ def main():
     W, H = a.width, a.height
     ctx = rt.Context(local)
     opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
-        rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0)
+        rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (rt._lib.MIRT_OPT_NONPERSISTENT if a.nonpersistent else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     frame = env.mutable().to_frame()
@@ -179,6 +180,8 @@ def main():
             "rays_per_frame": int(rays_per_frame),
             "hits_per_frame": int(hits / steps),
             "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / launches),
+            "bvh_visits_per_frame": {k: int(prof[k] / launches) for k in (
+                "primary_node_visits", "primary_leaf_visits", "shadow_node_visits", "shadow_leaf_visits")},
             "ms_kernels": {"primary": round(prim_ms, 4),
                            "shadow": round(prof["shadow_ms_sum"] / launches, 4),
                            "shade": round(prof["shade_ms_sum"] / launches, 4),

@@ -23,6 +23,7 @@ MIRT_MAX_OBJECTS = 16
 MIRT_MAX_LIGHTS = 16
 MIRT_OPT_NO_PREFILTER = 1
 MIRT_OPT_BRUTE_FORCE = 2
+MIRT_OPT_NONPERSISTENT = 4
 
 D3 = C.c_double * 3
 
@@ -68,7 +69,9 @@ class Profile(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("primary_ms_sum", C.c_double), ("shadow_ms_sum", C.c_double),
                 ("shade_ms_sum", C.c_double), ("frame_ms_sum", C.c_double),
                 ("primary_tri_tests", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
-                ("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64)]
+                ("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
+                ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
+                ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64)]
 
 
 class MeshView(C.Structure):

@@ -230,9 +230,28 @@ __device__ __forceinline__ bool slab_hit(const BvhNode& nd, V3 ro, V3 inv) {
 
 // Wave-uniform stackless BVH walk over one object's mesh.  `lane_on`: this lane has a
 // ray to trace.  Lanes whose origin is far from the mesh (beyond cull_limit) never cull.
+struct Visits {
+    uint32_t tests;   // triangles tested by the wave (x active lanes = ray-triangle tests)
+    uint32_t nodes;   // BVH nodes whose box the wave tested
+    uint32_t leaves;  // leaves the wave entered
+};
+// Per-wave totals over a whole persistent kernel, flushed once (see kStatBase).
+struct WaveStats {
+    cnt_t tests, nodes, leaves;
+};
+__device__ __forceinline__ void stats_flush(cnt_t* counters, int stat_tests, int stat_nodes, int stat_leaves,
+                                            const WaveStats& w) {
+    if ((threadIdx.x & 63) == 0) {
+        const int shard = (blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) & (kShards - 1);
+        if (w.tests) atomicAdd(&counters[kStatBase + stat_tests * kShards + shard], w.tests);
+        if (w.nodes) atomicAdd(&counters[kStatBase + stat_nodes * kShards + shard], w.nodes);
+        if (w.leaves) atomicAdd(&counters[kStatBase + stat_leaves * kShards + shard], w.leaves);
+    }
+}
+
 template <bool REL, bool PREFILTER, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on,
-                                          Best& b, uint32_t& wtests) {
+                                          Best& b, Visits& vis) {
     const V3 inv = ray_inv(d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
     const bool force = lane_on && !(far <= m.cull_limit);
@@ -241,6 +260,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
     while (ni < nn) {
         ni = __builtin_amdgcn_readfirstlane(ni);
         const BvhNode nd = load_node((cnptr)m.nodes + ni);
+        ++vis.nodes;
         const bool want = force || (lane_on && slab_hit(nd, ro, inv));
         if (__ballot(want) == 0) {
             ni = nd.skip;
@@ -250,8 +270,9 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             ++ni;  // depth-first layout: the left child follows its parent
             continue;
         }
+        ++vis.leaves;
         test_range<REL, PREFILTER>(src + (size_t)nd.first * kTriD, m.fidx, nd.first, nd.count, ro, d, neg, b,
-                                   wtests);
+                                   vis.tests);
         ni = nd.skip;
     }
 }
@@ -291,7 +312,7 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   BRUTE:    sweep every triangle instead of walking the BVH.
 template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal, uint32_t& wtests) {
+                                 bool lane_on, bool want_normal, Visits& vis) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -307,9 +328,9 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
         const uint32_t ntri = ob.m.ntri;
         if (resident) {
             if (BRUTE)
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b, wtests);
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
             else
-                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b, wtests);
+                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b, vis);
         } else if (BRUTE) {
             // stream the mesh through LDS in batches (every lane of the workgroup joins)
             for (uint32_t base = 0; base < ntri; base += kLdsTris) {
@@ -317,10 +338,10 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
                 __syncthreads();
                 stage_tris<REL>(lds, ob.m.tri, base, n, ro);
                 __syncthreads();
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b, wtests);
+                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b, vis.tests);
             }
         } else {
-            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, wtests);
+            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis);
         }
         uint32_t face, pos;
         if (best_result(b, face, pos)) {
@@ -369,6 +390,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
         __syncthreads();
     }
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    WaveStats ws{0, 0, 0};
     for (uint32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
         const uint32_t ti = find_tile(tiles, ntiles, unit);
         const TileDesc td = tiles[ti];
@@ -387,10 +409,11 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
                    scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
         V3 d = norm(sub(p, cam));
 
-        uint32_t wtests = 0;
-        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, wtests);
-        const uint32_t nact = __popcll(__ballot(active));
-        if (lane == 0 && nact) atomicAdd(&counters[kCntPrimTests], (cnt_t)wtests * nact);
+        Visits vis{0, 0, 0};
+        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
+        ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+        ws.nodes += vis.nodes;
+        ws.leaves += vis.leaves;
 
         const uint64_t oidx = td.out_off + (uint64_t)lx * td.h + ly;
         const bool is_hit = active && nh.ok;
@@ -430,6 +453,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
             }
         }
     }
+    stats_flush(counters, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, ws);
 }
 
 // ---------------------------------------------------------------- secondary rays
@@ -445,6 +469,7 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
     const uint32_t nh = MODE == kModeShadow ? (uint32_t)counters[kCntHits] : io.n;
     const uint64_t items = MODE == kModeShadow ? (uint64_t)nh * fa.n_lights : (uint64_t)io.n;
     const uint64_t nchunks = (items + kWG - 1) / kWG;
+    WaveStats ws{0, 0, 0};
     for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
         const uint64_t item = chunk * kWG + threadIdx.x;
         const bool active = item < items;
@@ -466,11 +491,11 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
                 d = vload(io.dir + 3 * item);
             }
         }
-        uint32_t wtests = 0;
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays, wtests);
-        const uint32_t nact = __popcll(__ballot(active));
-        if (MODE == kModeShadow && (threadIdx.x & 63) == 0 && nact)
-            atomicAdd(&counters[kCntShadowTests], (cnt_t)wtests * nact);
+        Visits vis{0, 0, 0};
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays, vis);
+        ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+        ws.nodes += vis.nodes;
+        ws.leaves += vis.leaves;
         if (active) {
             if (MODE == kModeShadow) {
                 // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
@@ -485,6 +510,7 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
             }
         }
     }
+    if (MODE == kModeShadow) stats_flush(counters, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, ws);
 }
 
 // ---------------------------------------------------------------- shade

@@ -114,15 +114,31 @@ int dev_grow(T*& p, size_t& cap, size_t need) {
     return MIRT_OK;
 }
 
+// Up to this many slots are created before a caller blocks on a busy one, so a caller
+// enqueueing frames back to back runs ahead of the GPU instead of waiting per frame.
+constexpr size_t kMaxIdleBlockSlots = 4;
+
 int slot_acquire(mirt_ctx* c, Slot*& out) {
     {
         std::lock_guard<std::mutex> g(c->mu);
-        if (!c->free_slots.empty()) {
-            out = c->free_slots.back();
-            c->free_slots.pop_back();
-        } else {
+        out = nullptr;
+        // prefer a free slot whose previous asynchronous work has already completed
+        for (size_t i = 0; i < c->free_slots.size(); ++i) {
+            Slot* s = c->free_slots[i];
+            if (!s->pending || hipEventQuery(s->done) == hipSuccess) {
+                s->pending = false;
+                out = s;
+                c->free_slots.erase(c->free_slots.begin() + (long)i);
+                break;
+            }
+        }
+        if (!out && (c->free_slots.empty() || c->slots.size() < kMaxIdleBlockSlots)) {
             c->slots.emplace_back(new Slot());
             out = c->slots.back().get();
+        }
+        if (!out) {  // every slot busy: take the oldest free one and wait for it below
+            out = c->free_slots.front();
+            c->free_slots.erase(c->free_slots.begin());
         }
     }
     Slot* s = out;
@@ -280,7 +296,10 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 
     HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(cnt_t), s));
-    const int pgrid = (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
+    // persistent: two 512-thread workgroups per CU walk the units; MIRT_OPT_NONPERSISTENT
+    // launches one workgroup per unit and lets the dispatcher balance the load.
+    const int pgrid = (c->flags & MIRT_OPT_NONPERSISTENT) ? (int)units
+                                                           : (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(f->n_lights, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((pixels + 255) / 256, (uint64_t)8 * c->cus));
@@ -311,6 +330,12 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     return MIRT_OK;
 }
 
+uint64_t stat_sum(const cnt_t* c, int stat) {
+    uint64_t s = 0;
+    for (int k = 0; k < kShards; ++k) s += c[kStatBase + stat * kShards + k];
+    return s;
+}
+
 int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t nl, mirt_stats* st) {
     HIP_TRY(hipMemcpyAsync(sl->h_counters, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -318,7 +343,7 @@ int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t
     st->primary_rays = pixels;
     st->hits = sl->h_counters[kCntHits];
     st->shadow_rays = st->hits * nl;
-    st->tri_tests = sl->h_counters[kCntPrimTests] + sl->h_counters[kCntShadowTests];
+    st->tri_tests = stat_sum(sl->h_counters, kStatPrimTests) + stat_sum(sl->h_counters, kStatShadowTests);
     return MIRT_OK;
 }
 
@@ -706,8 +731,12 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->primary_rays += r.pixels;
         out->hits += hits;
         out->shadow_rays += hits * r.nl;
-        out->primary_tri_tests += r.h_cnt[kCntPrimTests];
-        out->shadow_tri_tests += r.h_cnt[kCntShadowTests];
+        out->primary_tri_tests += stat_sum(r.h_cnt, kStatPrimTests);
+        out->shadow_tri_tests += stat_sum(r.h_cnt, kStatShadowTests);
+        out->primary_node_visits += stat_sum(r.h_cnt, kStatPrimNodes);
+        out->primary_leaf_visits += stat_sum(r.h_cnt, kStatPrimLeaves);
+        out->shadow_node_visits += stat_sum(r.h_cnt, kStatShadowNodes);
+        out->shadow_leaf_visits += stat_sum(r.h_cnt, kStatShadowLeaves);
     }
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);

@@ -96,7 +96,15 @@ struct OutPlanes {
 
 // Counters kept in device memory per call slot.
 // 64-bit: hits, ray-triangle tests performed by the primary / shadow kernels.
-enum { kCntHits = 0, kCntPrimTests = 1, kCntShadowTests = 2, kCntN = 4 };
+// counters[0] is the hit count that compaction allocates from (one atomic per wave that
+// has hits).  Statistics live in kShards-way sharded slots, counters[kStatBase +
+// stat*kShards + shard], each wave adding its totals ONCE at the end of a persistent
+// kernel: same-address atomics serialise at ~90 per microsecond on MI355X, so per-unit
+// counting would cost more than the tracing.  The host sums the shards.
+enum { kCntHits = 0, kStatBase = 8, kShards = 8 };
+enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kStatShadowNodes,
+       kStatShadowLeaves, kStatN };
+constexpr int kCntN = kStatBase + kStatN * kShards;
 typedef unsigned long long cnt_t;
 
 enum SecondaryMode { kModeShadow = 0, kModeRays = 1 };

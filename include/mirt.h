@@ -133,6 +133,8 @@ typedef struct {
     double primary_ms_sum, shadow_ms_sum, shade_ms_sum, frame_ms_sum;
     uint64_t primary_tri_tests, shadow_tri_tests;
     uint64_t primary_rays, shadow_rays, hits;
+    /* wave-level BVH traversal work (diagnostic): node boxes tested, leaves entered */
+    uint64_t primary_node_visits, primary_leaf_visits, shadow_node_visits, shadow_leaf_visits;
 } mirt_profile;
 
 int mirt_abi_version(void);
@@ -202,6 +204,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 /* Ask for kernel variants (benchmark ablations).  0 = defaults. */
 #define MIRT_OPT_NO_PREFILTER 1u  /* always take the true fp64 divide for r2 */
 #define MIRT_OPT_BRUTE_FORCE 2u   /* test every triangle (no BVH culling), mesh streamed via LDS */
+#define MIRT_OPT_NONPERSISTENT 4u /* one primary workgroup per 32x16 unit (no persistent loop) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*
