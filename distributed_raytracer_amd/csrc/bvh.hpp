@@ -1,20 +1,22 @@
-// bvh.hpp — host-side BVH build for exact culling (mesh upload time).
+// bvh.hpp — host-side BVH builds for exact culling (mesh upload time).
 //
 // The reference culls with an rtreego R-tree of padded face boxes
 // (shared/state/mesh.go:30-50, :139, :208; shared/geom/box.go:29-68).  On the GPU the
-// same role is played by a binary BVH traversed by whole waves (packet traversal), with
-// one requirement the reference does not have: culling must never change a result, so
-// every box is inflated far beyond the rounding error of the fp64 Möller–Trumbore test
-// and of the fp64 slab test.  Build: recursive median split of the face
-// centroids along the longest axis, leaves of <= kBvhLeaf faces, nodes emitted depth
-// first with a skip index per node.
+// same role is played by an 8-wide BVH that whole waves walk together (packet
+// traversal).  Culling must never change a result, so every box is inflated far beyond
+// the rounding error of the fp64 Möller–Trumbore test and of the fp32 slab test that
+// reads it.
+//
+// Build: binned SAH (16 bins on centroids, longest axis) into a binary tree with leaves
+// of <= kBvhLeaf faces, then collapse to 8-wide nodes by repeatedly opening the child
+// with the largest surface area.  Faces are reordered so that every leaf is one
+// contiguous range.
 #pragma once
 
 #include <stdint.h>
 
 #include <algorithm>
 #include <array>
-#include <functional>
 #include <cmath>
 #include <vector>
 
@@ -23,72 +25,199 @@
 namespace mirt {
 
 struct BvhBuild {
-    std::vector<BvhNode> nodes;
+    std::vector<Bvh8Node> nodes;  // nodes[0] is the root
     std::vector<uint32_t> order;  // position -> original face index
+    uint32_t depth = 0;           // inner levels (stack bound for traversal)
 };
 
-// v: nv*3 vertex array, fv: nf*3 indices.  inflate: absolute padding added to every box.
-inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, double inflate) {
-    BvhBuild b;
-    b.order.resize(nf);
-    for (uint32_t i = 0; i < nf; ++i) b.order[i] = i;
-    if (nf == 0) return b;
-    std::vector<std::array<double, 3>> lo(nf), hi(nf), ce(nf);
-    for (uint32_t f = 0; f < nf; ++f) {
+namespace detail {
+
+struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY};
+    double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box& b) {
         for (int k = 0; k < 3; ++k) {
-            double a = v[3 * (size_t)fv[3 * f] + k], bb = v[3 * (size_t)fv[3 * f + 1] + k],
-                   c = v[3 * (size_t)fv[3 * f + 2] + k];
-            lo[f][k] = std::min(a, std::min(bb, c));
-            hi[f][k] = std::max(a, std::max(bb, c));
-            ce[f][k] = 0.5 * (lo[f][k] + hi[f][k]);
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
         }
     }
-    struct Job {
-        uint32_t begin, end;
-        uint32_t node;
-    };
-    // recursive build with an explicit stack; skip indices patched after the subtree
-    std::vector<uint32_t> parents_pending;
-    std::function<void(uint32_t, uint32_t)> rec;
-    rec = [&](uint32_t begin, uint32_t end) {
-        uint32_t idx = (uint32_t)b.nodes.size();
-        b.nodes.push_back(BvhNode{});
-        double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
-        double cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const double p[3]) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    double area() const {
+        double e[3];
+        for (int k = 0; k < 3; ++k) e[k] = std::max(0.0, hi[k] - lo[k]);
+        return 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+    }
+};
+
+struct BNode {  // binary build node
+    Box box;
+    int left = -1, right = -1;
+    uint32_t first = 0, count = 0;  // leaf range
+};
+
+struct Builder {
+    const std::vector<Box>& fbox;
+    const std::vector<std::array<double, 3>>& ce;
+    std::vector<uint32_t>& order;
+    std::vector<BNode> nodes;
+
+    int build(uint32_t begin, uint32_t end) {
+        BNode n;
+        Box cb;
         for (uint32_t i = begin; i < end; ++i) {
-            uint32_t f = b.order[i];
-            for (int k = 0; k < 3; ++k) {
-                l[k] = std::min(l[k], lo[f][k]);
-                h[k] = std::max(h[k], hi[f][k]);
-                cl[k] = std::min(cl[k], ce[f][k]);
-                ch[k] = std::max(ch[k], ce[f][k]);
+            n.box.grow(fbox[order[i]]);
+            cb.grow(ce[order[i]].data());
+        }
+        const uint32_t cnt = end - begin;
+        int idx = (int)nodes.size();
+        nodes.push_back(n);
+        if (cnt <= (uint32_t)kBvhLeaf) {
+            nodes[idx].first = begin;
+            nodes[idx].count = cnt;
+            return idx;
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+        uint32_t mid = begin + cnt / 2;
+        const double ext = cb.hi[axis] - cb.lo[axis];
+        if (ext > 0) {
+            constexpr int B = 16;
+            Box bb[B];
+            uint32_t bc[B] = {0};
+            auto bin = [&](uint32_t f) {
+                int b = (int)((ce[f][axis] - cb.lo[axis]) / ext * B);
+                return std::min(B - 1, std::max(0, b));
+            };
+            for (uint32_t i = begin; i < end; ++i) {
+                int b = bin(order[i]);
+                bb[b].grow(fbox[order[i]]);
+                bc[b]++;
+            }
+            double best = INFINITY;
+            int best_split = -1;
+            for (int s = 1; s < B; ++s) {
+                Box l, r;
+                uint32_t nl = 0, nr = 0;
+                for (int b = 0; b < s; ++b) if (bc[b]) { l.grow(bb[b]); nl += bc[b]; }
+                for (int b = s; b < B; ++b) if (bc[b]) { r.grow(bb[b]); nr += bc[b]; }
+                if (!nl || !nr) continue;
+                double cost = l.area() * nl + r.area() * nr;
+                if (cost < best) { best = cost; best_split = s; }
+            }
+            if (best_split > 0) {
+                auto it = std::partition(order.begin() + begin, order.begin() + end,
+                                         [&](uint32_t f) { return bin(f) < best_split; });
+                mid = (uint32_t)(it - order.begin());
             }
         }
-        for (int k = 0; k < 3; ++k) {
-            b.nodes[idx].lo[k] = l[k] - inflate;
-            b.nodes[idx].hi[k] = h[k] + inflate;
-        }
-        if (end - begin <= (uint32_t)kBvhLeaf) {
-            b.nodes[idx].first = begin;
-            b.nodes[idx].count = end - begin;
-        } else {
-            int axis = 0;
-            for (int k = 1; k < 3; ++k)
-                if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
-            uint32_t mid = begin + (end - begin) / 2;
-            std::nth_element(b.order.begin() + begin, b.order.begin() + mid, b.order.begin() + end,
+        if (mid == begin || mid == end) {  // degenerate centroids: median by index
+            mid = begin + cnt / 2;
+            std::nth_element(order.begin() + begin, order.begin() + mid, order.begin() + end,
                              [&](uint32_t x, uint32_t y) {
                                  return ce[x][axis] < ce[y][axis] || (ce[x][axis] == ce[y][axis] && x < y);
                              });
-            b.nodes[idx].count = 0;
-            b.nodes[idx].first = 0;
-            rec(begin, mid);
-            rec(mid, end);
         }
-        b.nodes[idx].skip = (uint32_t)b.nodes.size();
-    };
-    rec(0, nf);
-    return b;
+        int l = build(begin, mid);
+        int r = build(mid, end);
+        nodes[idx].left = l;
+        nodes[idx].right = r;
+        return idx;
+    }
+};
+
+inline float round_down(double x) {
+    float f = (float)x;
+    return (double)f > x ? std::nextafter(f, -INFINITY) : f;
+}
+inline float round_up(double x) {
+    float f = (float)x;
+    return (double)f < x ? std::nextafter(f, INFINITY) : f;
+}
+
+}  // namespace detail
+
+// v: nv*3 vertex array, fv: nf*3 indices.  inflate: absolute padding of every box
+// (applied in fp64, then rounded outward to fp32).
+inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, double inflate) {
+    using namespace detail;
+    BvhBuild out;
+    out.order.resize(nf);
+    for (uint32_t i = 0; i < nf; ++i) out.order[i] = i;
+    std::vector<Box> fbox(nf);
+    std::vector<std::array<double, 3>> ce(nf);
+    for (uint32_t f = 0; f < nf; ++f) {
+        for (int c = 0; c < 3; ++c) fbox[f].grow(v + 3 * (size_t)fv[3 * f + c]);
+        for (int k = 0; k < 3; ++k) ce[f][k] = 0.5 * (fbox[f].lo[k] + fbox[f].hi[k]);
+    }
+    Builder b{fbox, ce, out.order, {}};
+    if (nf == 0) {
+        Bvh8Node root;
+        for (int c = 0; c < 8; ++c) root.child[c] = kBvhEmpty;
+        for (int k = 0; k < 3; ++k)
+            for (int c = 0; c < 8; ++c) root.lo[k][c] = root.hi[k][c] = 0.0f;
+        out.nodes.push_back(root);
+        return out;
+    }
+    b.build(0, nf);
+    // collapse the binary tree into 8-wide nodes
+    struct Pending { int bnode; uint32_t slot; uint32_t level; };
+    std::vector<Pending> work;
+    out.nodes.emplace_back();
+    work.push_back({0, 0, 1});
+    while (!work.empty()) {
+        Pending p = work.back();
+        work.pop_back();
+        out.depth = std::max(out.depth, p.level);
+        std::vector<int> kids;
+        const BNode& bn = b.nodes[p.bnode];
+        if (bn.left < 0) {
+            kids.push_back(p.bnode);  // a root that is itself a leaf
+        } else {
+            kids.push_back(bn.left);
+            kids.push_back(bn.right);
+            while (kids.size() < 8) {
+                int best = -1;
+                double ba = -1;
+                for (size_t i = 0; i < kids.size(); ++i) {
+                    const BNode& k = b.nodes[kids[i]];
+                    if (k.left >= 0 && k.box.area() > ba) { ba = k.box.area(); best = (int)i; }
+                }
+                if (best < 0) break;
+                int open = kids[best];
+                kids[best] = b.nodes[open].left;
+                kids.push_back(b.nodes[open].right);
+            }
+        }
+        Bvh8Node nd;  // filled locally: emplace_back below may reallocate out.nodes
+        for (int c = 0; c < 8; ++c) {
+            if (c >= (int)kids.size()) {
+                nd.child[c] = kBvhEmpty;
+                for (int k = 0; k < 3; ++k) { nd.lo[k][c] = 1.0f; nd.hi[k][c] = -1.0f; }
+                continue;
+            }
+            const BNode& k = b.nodes[kids[c]];
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[a][c] = round_down(k.box.lo[a] - inflate);
+                nd.hi[a][c] = round_up(k.box.hi[a] + inflate);
+            }
+            if (k.left < 0) {
+                nd.child[c] = kBvhLeafBit | (k.count << kBvhCountShift) | k.first;
+            } else {
+                uint32_t slot = (uint32_t)out.nodes.size();
+                nd.child[c] = slot;
+                out.nodes.emplace_back();
+                work.push_back({kids[c], slot, p.level + 1});
+            }
+        }
+        out.nodes[p.slot] = nd;
+    }
+    return out;
 }
 
 }  // namespace mirt

@@ -31,7 +31,9 @@ namespace mirt {
 // Wave-uniform reads of immutable device data (BVH nodes, triangles streamed from HBM)
 // go through the constant address space so hipcc emits scalar s_load into SGPRs.
 typedef const __attribute__((address_space(4))) double* cdptr;
-typedef const __attribute__((address_space(4))) BvhNode* cnptr;
+typedef const __attribute__((address_space(4))) Bvh8Node* cnptr;
+typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+typedef const __attribute__((address_space(4))) u32x16* cv16ptr;
 
 __device__ __forceinline__ V3 vload(const double* p) { return V3{p[0], p[1], p[2]}; }
 __device__ __forceinline__ void vstore(double* p, V3 v) {
@@ -195,41 +197,6 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
     }
 }
 
-// Per-ray slab-test constants: 1/D with zero/subnormal components replaced by a huge
-// finite value of the same sign, so (bound - origin) * inv is never 0 * inf = NaN.
-__device__ __forceinline__ V3 ray_inv(V3 d) {
-    V3 r{1.0 / d.x, 1.0 / d.y, 1.0 / d.z};
-    r.x = __builtin_fabs(r.x) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.x) : r.x;
-    r.y = __builtin_fabs(r.y) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.y) : r.y;
-    r.z = __builtin_fabs(r.z) > 0x1p1000 ? __builtin_copysign(0x1p1000, d.z) : r.z;
-    return r;
-}
-__device__ __forceinline__ BvhNode load_node(cnptr p) {
-    BvhNode n;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        n.lo[k] = p->lo[k];
-        n.hi[k] = p->hi[k];
-    }
-    n.skip = p->skip;
-    n.first = p->first;
-    n.count = p->count;
-    n.pad = 0;
-    return n;
-}
-
-// Ray vs inflated node box, t >= 0 half-line.
-__device__ __forceinline__ bool slab_hit(const BvhNode& nd, V3 ro, V3 inv) {
-    const double ax = (nd.lo[0] - ro.x) * inv.x, bx = (nd.hi[0] - ro.x) * inv.x;
-    const double ay = (nd.lo[1] - ro.y) * inv.y, by = (nd.hi[1] - ro.y) * inv.y;
-    const double az = (nd.lo[2] - ro.z) * inv.z, bz = (nd.hi[2] - ro.z) * inv.z;
-    const double tn = fmax(fmax(fmin(ax, bx), fmin(ay, by)), fmax(fmin(az, bz), 0.0));
-    const double tf = fmin(fmin(fmax(ax, bx), fmax(ay, by)), fmax(az, bz));
-    return tn <= tf;
-}
-
-// Wave-uniform stackless BVH walk over one object's mesh.  `lane_on`: this lane has a
-// ray to trace.  Lanes whose origin is far from the mesh (beyond cull_limit) never cull.
 struct Visits {
     uint32_t tests;   // triangles tested by the wave (x active lanes = ray-triangle tests)
     uint32_t nodes;   // BVH nodes whose box the wave tested
@@ -249,31 +216,92 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, int stat_tests, int
     }
 }
 
+// fp32 ray of the conservative slab tests: origin, 1/D with zero or tiny components
+// replaced by +-2^60 (so (bound - o) * inv is never 0 * inf), and o * inv.
+struct Ray32 {
+    float ox, oy, oz, ix, iy, iz, oix, oiy, oiz;
+};
+__device__ __forceinline__ float inv32(double d) {
+    const double r = 1.0 / d;
+    return __builtin_fabs(r) > 0x1p60 ? __builtin_copysignf(0x1p60f, (float)d) : (float)r;
+}
+__device__ __forceinline__ Ray32 ray32(V3 ro, V3 d) {
+    Ray32 r;
+    r.ox = (float)ro.x;
+    r.oy = (float)ro.y;
+    r.oz = (float)ro.z;
+    r.ix = inv32(d.x);
+    r.iy = inv32(d.y);
+    r.iz = inv32(d.z);
+    r.oix = r.ox * r.ix;
+    r.oiy = r.oy * r.iy;
+    r.oiz = r.oz * r.iz;
+    return r;
+}
+// A node in SGPRs: four s_load_dwordx16.  Words 0..23 lo[axis][child], 24..47
+// hi[axis][child], 48..55 child refs.
+struct NodeRegs {
+    u32x16 w0, w1, w2, w3;
+    __device__ __forceinline__ uint32_t word(int i) const {
+        return i < 16 ? w0[i] : i < 32 ? w1[i - 16] : i < 48 ? w2[i - 32] : w3[i - 48];
+    }
+    __device__ __forceinline__ float lo(int a, int c) const { return __uint_as_float(word(a * 8 + c)); }
+    __device__ __forceinline__ float hi(int a, int c) const { return __uint_as_float(word(24 + a * 8 + c)); }
+    __device__ __forceinline__ uint32_t child(int c) const { return word(48 + c); }
+};
+__device__ __forceinline__ NodeRegs load_node(cnptr nd) {
+    const cv16ptr p = (cv16ptr)nd;
+    return NodeRegs{p[0], p[1], p[2], p[3]};
+}
+
+// Ray vs child c's box, t >= 0 half-line.  Boxes are inflated by 2^-12 of the mesh
+// scale, which covers the fp32 rounding of every quantity here for origins within the
+// cull limit (256 x scale) by a factor > 4.
+__device__ __forceinline__ bool slab32(const NodeRegs& nd, int c, const Ray32& r) {
+    const float ax = __builtin_fmaf(nd.lo(0, c), r.ix, -r.oix), bx = __builtin_fmaf(nd.hi(0, c), r.ix, -r.oix);
+    const float ay = __builtin_fmaf(nd.lo(1, c), r.iy, -r.oiy), by = __builtin_fmaf(nd.hi(1, c), r.iy, -r.oiy);
+    const float az = __builtin_fmaf(nd.lo(2, c), r.iz, -r.oiz), bz = __builtin_fmaf(nd.hi(2, c), r.iz, -r.oiz);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn <= tf;
+}
+
+// Wave-uniform walk of one object's 8-wide BVH (packet traversal).  A child is entered
+// when ANY lane's ray hits its box; leaves are tested immediately, inner children go
+// on the wave's LDS stack `stk`.  Lanes whose object-space origin is beyond the cull
+// limit never cull (the inflation argument needs a bounded origin).
 template <bool REL, bool PREFILTER, typename SrcPtr>
-__device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on,
-                                          Best& b, Visits& vis) {
-    const V3 inv = ray_inv(d);
+__device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, uint32_t* __restrict__ stk, V3 ro, V3 d,
+                                          V3 neg, bool lane_on, Best& b, Visits& vis) {
+    const Ray32 r = ray32(ro, d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
     const bool force = lane_on && !(far <= m.cull_limit);
-    uint32_t ni = 0;
-    const uint32_t nn = m.nnodes;
-    while (ni < nn) {
-        ni = __builtin_amdgcn_readfirstlane(ni);
-        const BvhNode nd = load_node((cnptr)m.nodes + ni);
+    uint32_t sp = 0, cur = 0;
+    for (;;) {
+        cur = __builtin_amdgcn_readfirstlane(cur);
+        const NodeRegs nd = load_node((cnptr)m.nodes + cur);
         ++vis.nodes;
-        const bool want = force || (lane_on && slab_hit(nd, ro, inv));
-        if (__ballot(want) == 0) {
-            ni = nd.skip;
-            continue;
+        uint32_t hits = 0;  // per lane: bit c = ray hits child c
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            if (nd.child(c) != kBvhEmpty)  // branch-free: every lane evaluates, masks after
+                hits |= (uint32_t)(force | (lane_on & slab32(nd, c, r))) << c;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t ref = nd.child(c);
+            if (ref == kBvhEmpty || __ballot((hits >> c) & 1u) == 0) continue;
+            if (ref & kBvhLeafBit) {
+                const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
+                ++vis.leaves;
+                test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
+            } else {
+                stk[sp] = ref;
+                ++sp;
+            }
         }
-        if (nd.count == 0) {
-            ++ni;  // depth-first layout: the left child follows its parent
-            continue;
-        }
-        ++vis.leaves;
-        test_range<REL, PREFILTER>(src + (size_t)nd.first * kTriD, m.fidx, nd.first, nd.count, ro, d, neg, b,
-                                   vis.tests);
-        ni = nd.skip;
+        if (sp == 0) break;
+        --sp;
+        cur = stk[sp];
     }
 }
 
@@ -311,8 +339,8 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   RESIDENT: object 0's mesh sits in LDS (`lds`), relative (p1or) when REL.
 //   BRUTE:    sweep every triangle instead of walking the BVH.
 template <bool REL, bool PREFILTER, bool BRUTE>
-__device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal, Visits& vis) {
+__device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, uint32_t* __restrict__ stk,
+                                 bool resident, V3 o, V3 d, bool lane_on, bool want_normal, Visits& vis) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -330,7 +358,7 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
             if (BRUTE)
                 test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
             else
-                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, ro, d, neg, lane_on, b, vis);
+                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, stk, ro, d, neg, lane_on, b, vis);
         } else if (BRUTE) {
             // stream the mesh through LDS in batches (every lane of the workgroup joins)
             for (uint32_t base = 0; base < ntri; base += kLdsTris) {
@@ -341,7 +369,7 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
                 test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b, vis.tests);
             }
         } else {
-            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis);
+            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, stk, ro, d, neg, lane_on, b, vis);
         }
         uint32_t face, pos;
         if (best_result(b, face, pos)) {
@@ -383,6 +411,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
                                                      uint32_t ntiles, uint32_t total_units, OutPlanes out,
                                                      HitRec* __restrict__ hits, cnt_t* __restrict__ counters) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
+    __shared__ uint32_t stacks[kWG / 64][kBvhStack];
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
@@ -410,7 +439,8 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Ti
         V3 d = norm(sub(p, cam));
 
         Visits vis{0, 0, 0};
-        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
+        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, stacks[wave], RESIDENT, cam, d, active, true,
+                                                               vis);
         ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
         ws.nodes += vis.nodes;
         ws.leaves += vis.leaves;
@@ -462,6 +492,7 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
                                                        cnt_t* __restrict__ counters,
                                                        uint8_t* __restrict__ lit, RayIO io) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
+    __shared__ uint32_t stacks[kWG / 64][kBvhStack];
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
@@ -492,7 +523,8 @@ __global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const 
             }
         }
         Visits vis{0, 0, 0};
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, MODE == kModeRays, vis);
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, stacks[threadIdx.x >> 6], RESIDENT, o, d, active,
+                                                           MODE == kModeRays, vis);
         ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
         ws.nodes += vis.nodes;
         ws.leaves += vis.leaves;

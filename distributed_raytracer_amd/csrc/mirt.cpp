@@ -45,9 +45,9 @@ struct MeshDev {
     double* vnrm = nullptr;
     uint32_t* fmat = nullptr;
     uint32_t* fidx = nullptr;
-    BvhNode* nodes = nullptr;
+    Bvh8Node* nodes = nullptr;
     double* mats = nullptr;
-    uint32_t ntri = 0, nmat = 0, nnodes = 0;
+    uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
     bool has_normals = false;
     bool live = false;
@@ -229,6 +229,7 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         o.m.fidx = m.fidx;
         o.m.nodes = m.nodes;
         o.m.nnodes = m.nnodes;
+        o.m.depth = m.depth;
         o.m.cull_limit = 256.0 * m.scale;
         o.m.mats = m.mats;
         o.m.ntri = m.ntri;
@@ -475,12 +476,15 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         if (fmat[f] >= nm) return fail(MIRT_E_INVALID, "face " + std::to_string(f) + " material out of range");
     }
     HIP_TRY(hipSetDevice(c->device));
-    // Culling structure: BVH over the faces, boxes inflated by 2^-24 of the mesh's
-    // largest |coordinate|.  All per-face arrays are stored in BVH order.
+    if (nf > kBvhFirstMask) return fail(MIRT_E_LIMIT, "more than 2^24 faces in one mesh");
+    // Culling structure: 8-wide BVH over the faces, fp32 boxes inflated by 2^-12 of the
+    // mesh's largest |coordinate|.  All per-face arrays in BVH order.
     double scale = 0;
     for (size_t i = 0; i < (size_t)nv * 3; ++i) scale = std::max(scale, std::fabs(v[i]));
-    scale = std::max(scale, 1e-300);
-    BvhBuild bvh = build_bvh(v, fv, nf, std::ldexp(scale, -24));
+    scale = std::max(scale, 1e-30);
+    BvhBuild bvh = build_bvh(v, fv, nf, std::ldexp(scale, -12));
+    if (bvh.depth > (uint32_t)kBvhMaxDepth)
+        return fail(MIRT_E_LIMIT, "BVH deeper than the traversal stack (" + std::to_string(bvh.depth) + " levels)");
     // P1, E1 = P2 - P1, E2 = P3 - P1 (triangle.go:38: single fp64 subtractions, so the
     // precomputed edges are bit-identical to the per-test ones of the reference).
     std::vector<double> tri((size_t)nf * kTriD), vnrm(has_n ? (size_t)nf * kTriD : 0), mt((size_t)nm * 10);
@@ -514,6 +518,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     md.nmat = nm;
     md.has_normals = has_n;
     md.nnodes = (uint32_t)bvh.nodes.size();
+    md.depth = bvh.depth;
     md.scale = scale;
     auto upload = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return MIRT_OK;
@@ -528,7 +533,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         (r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK ||
         (r = upload((void**)&md.fmat, fm.data(), (size_t)nf * 4)) != MIRT_OK ||
         (r = upload((void**)&md.fidx, bvh.order.data(), (size_t)nf * 4)) != MIRT_OK ||
-        (r = upload((void**)&md.nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(BvhNode))) != MIRT_OK ||
+        (r = upload((void**)&md.nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(Bvh8Node))) != MIRT_OK ||
         (r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) {
         mesh_free(md);
         return r;
@@ -559,7 +564,7 @@ int mirt_trace_tiles_async(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_
     Slot* sl = nullptr;
     if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
-    hipStream_t s = stream ? (hipStream_t)stream : sl->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL is the HIP null stream, as in the HIP API
     OutPlanes out{dout->rgb, dout->rgb8, dout->valid, dout->face, dout->object};
     uint64_t pixels = 0, tris = 0;
     if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, nullptr, &pixels, &tris)) != MIRT_OK) {
@@ -631,7 +636,7 @@ int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile
     int r;
     if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
-    hipStream_t s = stream ? (hipStream_t)stream : sl->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL is the HIP null stream, as in the HIP API
     if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
     uint64_t pixels = 0;
     for (uint32_t t = 0; t < n; ++t) {

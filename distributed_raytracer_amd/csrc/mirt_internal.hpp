@@ -19,18 +19,25 @@ constexpr int kTriD = 9;
 // larger meshes stream through it in batches of this size.
 constexpr int kLdsTris = 1024;
 
-// BVH node (64 B), nodes in depth-first order: an inner node's left child is the next
-// node; `skip` is the first node after this node's subtree (stackless traversal).
-// Boxes are inflated so that a ray the fp64 Möller–Trumbore test could report as a hit
-// always passes the box test (see DESIGN.md §4 "Exact culling").
-struct BvhNode {
-    double lo[3], hi[3];
-    uint32_t skip;
-    uint32_t first;   // first triangle (position in the BVH-ordered arrays)
-    uint32_t count;   // 0 for an inner node
-    uint32_t pad;
+// 8-wide BVH node.  Child boxes are fp32, rounded outward and inflated so that
+// a ray the fp64 Möller–Trumbore test could report as a hit always passes the fp32
+// slab test (DESIGN.md §4 "Exact culling").  child[c]: kBvhEmpty, an inner node index,
+// or kBvhLeafBit | count << kBvhCountShift | first (a contiguous triangle range).
+// Non-empty children come first.  256 B, 64-byte aligned: fetched as four
+// s_load_dwordx16 per visit.
+struct alignas(64) Bvh8Node {
+    float lo[3][8];
+    float hi[3][8];
+    uint32_t child[8];
+    uint32_t pad[8];
 };
-constexpr int kBvhLeaf = 8;  // max triangles per leaf
+constexpr uint32_t kBvhEmpty = 0xffffffffu;
+constexpr uint32_t kBvhLeafBit = 0x80000000u;
+constexpr int kBvhCountShift = 24;
+constexpr uint32_t kBvhFirstMask = 0x00ffffffu;
+constexpr int kBvhLeaf = 4;           // max triangles per leaf
+constexpr int kBvhStack = 128;        // per-wave traversal stack entries (LDS)
+constexpr int kBvhMaxDepth = (kBvhStack - 1) / 7;
 
 // One uploaded mesh, device pointers (shared/state/mesh.go:100-106).  Every per-face
 // array is stored in BVH leaf order; fidx maps a position back to the face index of
@@ -40,12 +47,12 @@ struct DevMesh {
     const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
     const uint32_t* fmat;    // ntri     : material index
     const uint32_t* fidx;    // ntri     : original face index
-    const BvhNode* nodes;    // nnodes
+    const Bvh8Node* nodes;   // root first
     const double* mats;      // nmat * 10: ka[3] kd[3] ks[3] ns
     uint32_t ntri;
     uint32_t has_normals;
     uint32_t nnodes;
-    uint32_t pad;
+    uint32_t depth;
     double cull_limit;       // rays whose object-space origin has a coordinate beyond this
                              // are never culled (tolerance scales with |origin|)
 };

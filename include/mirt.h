@@ -174,8 +174,8 @@ int mirt_trace_tile(mirt_ctx *ctx, const mirt_frame *frame, uint32_t x, uint32_t
                     mirt_stats *stats);
 
 /*
- * Trace a list of tiles into DEVICE buffers on `stream` (a hipStream_t; NULL = the
- * context's own stream).  Asynchronous: returns after enqueueing.  If stats is non-NULL
+ * Trace a list of tiles into DEVICE buffers on `stream` (a hipStream_t; NULL = the HIP
+ * null stream).  Asynchronous: returns after enqueueing.  If stats is non-NULL
  * the call synchronises the stream and fills it.  Device buffers must hold
  * sum(w*h) pixels of each requested plane.
  */
