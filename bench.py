@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
-    ap.add_argument("--nonpersistent", action="store_true", help="ablation: one workgroup per primary unit")
+    ap.add_argument("--static-schedule", action="store_true",
+                    help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
@@ -100,7 +101,8 @@ def main():
     W, H = a.width, a.height
     ctx = rt.Context(local)
     opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
-        rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (rt._lib.MIRT_OPT_NONPERSISTENT if a.nonpersistent else 0)
+        rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
+        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     frame = env.mutable().to_frame()

@@ -23,7 +23,9 @@ MIRT_MAX_OBJECTS = 16
 MIRT_MAX_LIGHTS = 16
 MIRT_OPT_NO_PREFILTER = 1
 MIRT_OPT_BRUTE_FORCE = 2
-MIRT_OPT_NONPERSISTENT = 4
+MIRT_OPT_STATIC_SCHEDULE = 4
+MIRT_OPT_TIMELINE = 8
+MIRT_OPT_NO_SEGMENT = 16
 
 D3 = C.c_double * 3
 
@@ -113,6 +115,7 @@ SIGNATURES = {
     "mirt_profile_read": (C.c_int, [_P, C.POINTER(Profile)]),
     "mirt_set_options": (C.c_int, [_P, C.c_uint32]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
+    "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "mirt_scene_free": (None, [_P]),
     "mirt_scene_last_error": (C.c_char_p, []),

@@ -202,19 +202,47 @@ struct Visits {
     uint32_t nodes;   // BVH nodes whose box the wave tested
     uint32_t leaves;  // leaves the wave entered
 };
-// Per-wave totals over a whole persistent kernel, flushed once (see kStatBase).
+// Per-wave totals over a whole persistent kernel.  At the end every wave parks its totals
+// in LDS and one lane of the workgroup adds the sums into shard blockIdx % kStatShards:
+// one atomic per statistic per workgroup (see the counter layout in mirt_internal.hpp).
 struct WaveStats {
     cnt_t tests, nodes, leaves;
 };
-__device__ __forceinline__ void stats_flush(cnt_t* counters, int stat_tests, int stat_nodes, int stat_leaves,
-                                            const WaveStats& w) {
+__device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[3], int stat_tests, int stat_nodes,
+                                            int stat_leaves, const WaveStats& w) {
+    const uint32_t wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        const int shard = (blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) & (kShards - 1);
-        if (w.tests) atomicAdd(&counters[kStatBase + stat_tests * kShards + shard], w.tests);
-        if (w.nodes) atomicAdd(&counters[kStatBase + stat_nodes * kShards + shard], w.nodes);
-        if (w.leaves) atomicAdd(&counters[kStatBase + stat_leaves * kShards + shard], w.leaves);
+        red[wave][0] = w.tests;
+        red[wave][1] = w.nodes;
+        red[wave][2] = w.leaves;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        cnt_t sum = 0;
+        for (int k = 0; k < kWG / 64; ++k) sum += red[k][threadIdx.x];
+        const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes : stat_leaves;
+        if (sum) atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
     }
 }
+
+// Wave-uniform traversal stack held in two VGPRs: entry i lives in lane i % 64 of
+// word i / 64.  Push and pop are v_writelane / v_readlane with the SGPR stack pointer:
+// no memory traffic and no LDS latency on the node-to-node dependency chain.
+struct WaveStack {
+    int a = 0, b = 0;
+    uint32_t sp = 0;
+    __device__ __forceinline__ void push(uint32_t ref) {
+        if (sp < 64)
+            asm("v_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(ref), "{m0}"(sp));
+        else
+            asm("v_writelane_b32 %0, %1, m0" : "+v"(b) : "s"(ref), "{m0}"(sp - 64));
+        ++sp;
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        --sp;
+        return (uint32_t)(sp < 64 ? __builtin_amdgcn_readlane(a, (int)sp) : __builtin_amdgcn_readlane(b, (int)(sp - 64)));
+    }
+};
 
 // fp32 ray of the conservative slab tests: origin, 1/D with zero or tiny components
 // replaced by +-2^60 (so (bound - o) * inv is never 0 * inf), and o * inv.
@@ -257,26 +285,32 @@ __device__ __forceinline__ NodeRegs load_node(cnptr nd) {
 // Ray vs child c's box, t >= 0 half-line.  Boxes are inflated by 2^-12 of the mesh
 // scale, which covers the fp32 rounding of every quantity here for origins within the
 // cull limit (256 x scale) by a factor > 4.
-__device__ __forceinline__ bool slab32(const NodeRegs& nd, int c, const Ray32& r) {
+template <bool SEG>
+__device__ __forceinline__ bool slab32(const NodeRegs& nd, int c, const Ray32& r, float tmax) {
     const float ax = __builtin_fmaf(nd.lo(0, c), r.ix, -r.oix), bx = __builtin_fmaf(nd.hi(0, c), r.ix, -r.oix);
     const float ay = __builtin_fmaf(nd.lo(1, c), r.iy, -r.oiy), by = __builtin_fmaf(nd.hi(1, c), r.iy, -r.oiy);
     const float az = __builtin_fmaf(nd.lo(2, c), r.iz, -r.oiz), bz = __builtin_fmaf(nd.hi(2, c), r.iz, -r.oiz);
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    return tn <= tf;
+    return tn <= (SEG ? fminf(tf, tmax) : tf);
 }
 
 // Wave-uniform walk of one object's 8-wide BVH (packet traversal).  A child is entered
-// when ANY lane's ray hits its box; leaves are tested immediately, inner children go
-// on the wave's LDS stack `stk`.  Lanes whose object-space origin is beyond the cull
+// when ANY live lane's ray hits its box; leaves are tested immediately, inner children
+// go on the wave's register stack.  Lanes whose object-space origin is beyond the cull
 // limit never cull (the inflation argument needs a bounded origin).
-template <bool REL, bool PREFILTER, typename SrcPtr>
-__device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, uint32_t* __restrict__ stk, V3 ro, V3 d,
-                                          V3 neg, bool lane_on, Best& b, Visits& vis) {
+//   SEG (segment query): a lane also skips boxes it enters beyond tmax, and retires once
+//   its nearest candidate is closer than `resolve` (the caller's decision is then made);
+//   the walk ends when no live lane is left.
+template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
+__device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
+                                          Visits& vis, float tmax = 0.0f, double resolve = 0.0) {
     const Ray32 r = ray32(ro, d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-    const bool force = lane_on && !(far <= m.cull_limit);
-    uint32_t sp = 0, cur = 0;
+    const bool force = !(far <= m.cull_limit);
+    bool live = lane_on;
+    WaveStack stk;
+    uint32_t cur = 0;
     for (;;) {
         cur = __builtin_amdgcn_readfirstlane(cur);
         const NodeRegs nd = load_node((cnptr)m.nodes + cur);
@@ -285,7 +319,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, uint32_t
 #pragma unroll
         for (int c = 0; c < 8; ++c)
             if (nd.child(c) != kBvhEmpty)  // branch-free: every lane evaluates, masks after
-                hits |= (uint32_t)(force | (lane_on & slab32(nd, c, r))) << c;
+                hits |= (uint32_t)(live & (force | slab32<SEG>(nd, c, r, tmax))) << c;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const uint32_t ref = nd.child(c);
@@ -294,14 +328,13 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, uint32_t
                 const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
                 ++vis.leaves;
                 test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
+                if (SEG) live = live && !(b.has && b.d < resolve);
             } else {
-                stk[sp] = ref;
-                ++sp;
+                stk.push(ref);
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur = stk[sp];
+        if (stk.sp == 0 || (SEG && __ballot(live) == 0)) break;
+        cur = stk.pop();
     }
 }
 
@@ -339,8 +372,8 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   RESIDENT: object 0's mesh sits in LDS (`lds`), relative (p1or) when REL.
 //   BRUTE:    sweep every triangle instead of walking the BVH.
 template <bool REL, bool PREFILTER, bool BRUTE>
-__device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, uint32_t* __restrict__ stk,
-                                 bool resident, V3 o, V3 d, bool lane_on, bool want_normal, Visits& vis) {
+__device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
+                                 bool lane_on, bool want_normal, Visits& vis) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -356,20 +389,14 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
         const uint32_t ntri = ob.m.ntri;
         if (resident) {
             if (BRUTE)
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+                test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
             else
-                bvh_sweep<REL, PREFILTER>(ob.m, (const double*)lds, stk, ro, d, neg, lane_on, b, vis);
+                bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis);
         } else if (BRUTE) {
-            // stream the mesh through LDS in batches (every lane of the workgroup joins)
-            for (uint32_t base = 0; base < ntri; base += kLdsTris) {
-                uint32_t n = min((uint32_t)kLdsTris, ntri - base);
-                __syncthreads();
-                stage_tris<REL>(lds, ob.m.tri, base, n, ro);
-                __syncthreads();
-                test_range<REL, PREFILTER>((const double*)lds, ob.m.fidx, base, n, ro, d, neg, b, vis.tests);
-            }
+            // every triangle straight from HBM (waves run independently: no LDS staging)
+            test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
         } else {
-            bvh_sweep<false, PREFILTER>(ob.m, (cdptr)ob.m.tri, stk, ro, d, neg, lane_on, b, vis);
+            bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis);
         }
         uint32_t face, pos;
         if (best_result(b, face, pos)) {
@@ -391,193 +418,313 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, double* __restrict__ lds, 
     return best;
 }
 
-__device__ __forceinline__ uint32_t find_tile(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t unit) {
-    uint32_t lo = 0, hi = ntiles - 1;
-    while (lo < hi) {
-        uint32_t mid = (lo + hi + 1) >> 1;
-        if (tiles[mid].unit_begin <= unit)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    return lo;
+// Shadow ray of a one-object frame as a segment query (exact; DESIGN.md §4 "Shadow
+// segments").  Only tracer.go:64's lit flag leaves the kernel:
+//   lit = !shaded || |L - hit| < |occluder - hit|,   occluder = nearest hit from o.
+// With lh = |L - hit| and |o - hit| = 1e-4 (+ rounding), a candidate at distance dist from
+// o lies within dist + 1e-4 + M of hit, and the nearest is no farther, so
+//   dist < lh - 1e-4 - M  =>  not lit (the lane retires: any-hit);
+//   every candidate beyond lh + 1e-4 + M  =>  lit, so boxes entered beyond that are culled;
+// otherwise the nearest candidate found is the true nearest and the reference comparison
+// runs unchanged.  M bounds every fp64 rounding involved with a wide margin.
+template <bool PREFILTER>
+__device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
+                                                  V3 hit, V3 o, V3 d, V3 lpos, bool lane_on, Visits& vis) {
+    const DevObject& ob = fa.obj[0];
+    const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
+    const V3 ro = sub(o, pos);  // object.go:71
+    const V3 neg = scale(d, -1);
+    const double lh = len(sub(lpos, hit));
+    const double mag = fmax(fmax(fmax(__builtin_fabs(o.x), __builtin_fabs(o.y)), __builtin_fabs(o.z)),
+                            fmax(fmax(__builtin_fabs(pos.x), __builtin_fabs(pos.y)), __builtin_fabs(pos.z)));
+    const double M = 0x1p-36 * (1.0 + lh + mag);
+    const double resolve = lh - 1e-4 - M;
+    const float tmax = (float)(lh + 1e-4 + M) * (1.0f + 0x1p-20f);
+    Best b;
+    best_init(b);
+    if (resident)
+        bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve);
+    else
+        bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve);
+    if (b.has && b.d < resolve) return false;
+    uint32_t face, p;
+    if (!best_result(b, face, p)) return true;
+    V3 world, normal;
+    uint32_t mat;
+    winner(ob, p, ro, d, neg, world, normal, mat, false);
+    return lh < len(sub(world, hit));
 }
+
+// ---------------------------------------------------------------- work distribution
+// A wave serves queue shard q = (global wave id) % kQShards (several shards in turn when
+// fewer than kQShards waves run).  dynamic: each ticket of the shard's counter is one work
+// item, the next ticket is requested before the current item is traced so the atomic's
+// latency hides behind the work; static: items q, q + kQShards, ... split round-robin
+// among the waves of the shard (ablation).
+struct ShardCursor {
+    uint32_t gw, nw;  // global wave id, waves in the grid
+    __device__ __forceinline__ ShardCursor() {
+        gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        nw = gridDim.x * (kWG / 64);
+    }
+    __device__ __forceinline__ uint32_t first_shard() const { return nw >= (uint32_t)kQShards ? gw % kQShards : gw; }
+    __device__ __forceinline__ uint32_t shard_step() const { return nw >= (uint32_t)kQShards ? kQShards : nw; }
+    // static mode: this wave's rank among the waves serving its shard, and their count
+    __device__ __forceinline__ uint32_t rank() const { return nw >= (uint32_t)kQShards ? gw / kQShards : 0; }
+    __device__ __forceinline__ uint32_t peers() const {
+        if (nw < (uint32_t)kQShards) return 1;
+        const uint32_t q = gw % kQShards;
+        return nw / kQShards + (q < nw % kQShards ? 1 : 0);
+    }
+};
+// MIRT_OPT_TIMELINE: per-wave stamps (mirt.h mirt_debug_timeline).
+struct WaveClock {
+    uint64_t real0, clk0;
+    __device__ __forceinline__ WaveClock() {
+        real0 = __builtin_amdgcn_s_memrealtime();
+        clk0 = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void record(const WorkArgs& wa, uint32_t kernel, uint32_t items) const {
+        const uint64_t real1 = __builtin_amdgcn_s_memrealtime(), clk1 = __builtin_amdgcn_s_memtime();
+        const uint32_t gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        const uint32_t lane = threadIdx.x & 63;
+        if (gw >= wa.timeline_cap || lane >= kTimelineRec) return;
+        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+        const uint64_t v[kTimelineRec] = {kernel, gw, real0, real1, clk0, clk1, hwid, xcc | ((uint64_t)items << 32)};
+        uint64_t x = 0;
+#pragma unroll
+        for (int k = 0; k < kTimelineRec; ++k) x = lane == (uint32_t)k ? v[k] : x;
+        wa.timeline[((size_t)kernel * wa.timeline_cap + gw) * kTimelineRec + lane] = x;
+    }
+};
+
+// One ticket of counter c, issued by lane 0; resolve() broadcasts it (waits for the atomic).
+__device__ __forceinline__ uint32_t ticket_issue(cnt_t* c) {
+    uint32_t t = 0;
+    if ((threadIdx.x & 63) == 0) t = (uint32_t)atomicAdd(c, (cnt_t)1);
+    return t;
+}
+__device__ __forceinline__ uint32_t ticket_resolve(uint32_t t) { return __builtin_amdgcn_readfirstlane(t); }
 
 // ---------------------------------------------------------------- primary
 // RESIDENT (host-decided): one object whose mesh fits in LDS; it is staged once per
 // persistent workgroup, relative to the camera (p1or), and every sweep reads LDS.
+// Work item: one 8x8 pixel block (BlockDesc), lane -> (x, y) with y fastest so a wave's
+// writes are 8 runs of 8 contiguous pixels of the column-major packed tile.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const TileDesc* __restrict__ tiles,
-                                                     uint32_t ntiles, uint32_t total_units, OutPlanes out,
-                                                     HitRec* __restrict__ hits, cnt_t* __restrict__ counters) {
+__global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    __shared__ uint32_t stacks[kWG / 64][kBvhStack];
+    __shared__ cnt_t red[kWG / 64][3];
+    const WaveClock clock;
+    uint32_t taken = 0;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
         __syncthreads();
     }
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
+    const ShardCursor sc;
     WaveStats ws{0, 0, 0};
-    for (uint32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
-        const uint32_t ti = find_tile(tiles, ntiles, unit);
-        const TileDesc td = tiles[ti];
-        const uint32_t lu = unit - td.unit_begin;
-        const uint32_t ux = lu % td.units_w, uy = lu / td.units_w;
-        // lane -> (x, y) with y fastest so a wave's writes are 8 runs of 8 contiguous pixels
-        const uint32_t lx = ux * kUnitW + (wave & 3) * 8 + (lane >> 3);
-        const uint32_t ly = uy * kUnitH + (wave >> 2) * 8 + (lane & 7);
-        const bool active = lx < td.w && ly < td.h;
-        const int i = (int)(td.x + (active ? lx : 0)), j = (int)(td.y + (active ? ly : 0));
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+        cnt_t* qc = &wa.counters[cnt_queue(0, q)];
+        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        for (;;) {
+            const uint32_t blk = k * kQShards + q;
+            if (blk >= wa.nblocks) break;
+            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;  // in flight while tracing
+            ++taken;
+            const BlockDesc bd = wa.blocks[blk];
+            const uint32_t lx = lane >> 3, ly = lane & 7;
+            const bool active = lx < bd.vw && ly < bd.vh;
+            const int i = (int)(bd.px + (active ? lx : 0)), j = (int)(bd.py + (active ? ly : 0));
 
-        // tracer.go:15-22 pixelToPoint, then tracer.go:86 dir = (p - Cam.Pos).Norm()
-        const double si = fa.phw * ((double)(fa.halfW - i) - 0.5) / (double)fa.halfW;
-        const double sj = fa.phh * ((double)(fa.halfH - j) - 0.5) / (double)fa.halfH;
-        V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}), scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
-                   scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
-        V3 d = norm(sub(p, cam));
+            // tracer.go:15-22 pixelToPoint, then tracer.go:86 dir = (p - Cam.Pos).Norm()
+            const double si = fa.phw * ((double)(fa.halfW - i) - 0.5) / (double)fa.halfW;
+            const double sj = fa.phh * ((double)(fa.halfH - j) - 0.5) / (double)fa.halfH;
+            V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}),
+                           scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
+                       scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
+            V3 d = norm(sub(p, cam));
 
-        Visits vis{0, 0, 0};
-        Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, stacks[wave], RESIDENT, cam, d, active, true,
-                                                               vis);
-        ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-        ws.nodes += vis.nodes;
-        ws.leaves += vis.leaves;
+            Visits vis{0, 0, 0};
+            Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
 
-        const uint64_t oidx = td.out_off + (uint64_t)lx * td.h + ly;
-        const bool is_hit = active && nh.ok;
-        if (active) {
-            if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
-            if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
-            if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
-            if (!is_hit) {
-                if (out.rgb) {
-                    out.rgb[3 * oidx] = 0.0;
-                    out.rgb[3 * oidx + 1] = 0.0;
-                    out.rgb[3 * oidx + 2] = 0.0;
-                }
-                if (out.rgb8) {
-                    out.rgb8[3 * oidx] = 0;
-                    out.rgb8[3 * oidx + 1] = 0;
-                    out.rgb8[3 * oidx + 2] = 0;
+            const uint64_t oidx = bd.out + (uint64_t)lx * bd.th + ly;
+            const bool is_hit = active && nh.ok;
+            if (active) {
+                if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
+                if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
+                if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
+                if (!is_hit) {
+                    if (out.rgb) {
+                        out.rgb[3 * oidx] = 0.0;
+                        out.rgb[3 * oidx + 1] = 0.0;
+                        out.rgb[3 * oidx + 2] = 0.0;
+                    }
+                    if (out.rgb8) {
+                        out.rgb8[3 * oidx] = 0;
+                        out.rgb8[3 * oidx + 1] = 0;
+                        out.rgb8[3 * oidx + 2] = 0;
+                    }
                 }
             }
-        }
-        // wave-aggregated compaction of hits
-        const uint64_t mask = __ballot(is_hit);
-        if (mask) {
-            const uint32_t cnt = __popcll(mask);
-            const uint32_t leader = __ffsll((unsigned long long)mask) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = (uint32_t)atomicAdd(&counters[kCntHits], (cnt_t)cnt);
-            base = __shfl(base, leader);
-            if (is_hit) {
-                const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
-                HitRec& hr = hits[base + rank];
-                vstore(hr.h, nh.hit);
-                vstore(hr.n, nh.normal);
-                hr.out = oidx;
-                hr.obj = nh.obj;
-                hr.mat = nh.mat;
+            // wave-aggregated compaction into hit region q (blocks of shard q only)
+            const uint64_t mask = __ballot(is_hit);
+            if (mask) {
+                const uint32_t cnt = __popcll(mask);
+                uint32_t base = 0;
+                if (lane == 0) base = (uint32_t)atomicAdd(&wa.counters[cnt_hits(q)], (cnt_t)cnt);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (is_hit) {
+                    const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
+                    HitRec& hr = wa.hits[(size_t)q * wa.hit_cap + base + rank];
+                    vstore(hr.h, nh.hit);
+                    vstore(hr.n, nh.normal);
+                    hr.out = oidx;
+                    hr.obj = nh.obj;
+                    hr.mat = nh.mat;
+                }
             }
+            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
-    stats_flush(counters, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, ws);
+    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, ws);
+    if (wa.timeline) clock.record(wa, 0, taken);
 }
 
-// ---------------------------------------------------------------- secondary rays
-template <int MODE, bool PREFILTER, bool BRUTE, bool RESIDENT>
-__global__ __launch_bounds__(kWG, 4) void k_secondary(const FrameArgs fa, const HitRec* __restrict__ hits,
-                                                       cnt_t* __restrict__ counters,
-                                                       uint8_t* __restrict__ lit, RayIO io) {
+// ---------------------------------------------------------------- shadow rays
+// Work item: 64 consecutive hits of one region and one light (consecutive lanes =
+// neighbouring pixels towards the same light: coherent rays).  Tickets of shard q
+// enumerate (light, chunk) of region q.
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__global__ __launch_bounds__(kWG, 4) void k_shadow(const FrameArgs fa, const WorkArgs wa) {
+    // segment query for one-object frames (BVH kernels only; brute force stays literal)
+    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    __shared__ uint32_t stacks[kWG / 64][kBvhStack];
+    __shared__ cnt_t red[kWG / 64][3];
+    const WaveClock clock;
+    uint32_t taken = 0;
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
-    const uint32_t nh = MODE == kModeShadow ? (uint32_t)counters[kCntHits] : io.n;
-    const uint64_t items = MODE == kModeShadow ? (uint64_t)nh * fa.n_lights : (uint64_t)io.n;
-    const uint64_t nchunks = (items + kWG - 1) / kWG;
+    const uint32_t lane = threadIdx.x & 63;
+    const ShardCursor sc;
     WaveStats ws{0, 0, 0};
-    for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-        const uint64_t item = chunk * kWG + threadIdx.x;
-        const bool active = item < items;
-        V3 o{0, 0, 0}, d{1, 0, 0};
-        uint32_t h = 0, l = 0;
-        V3 hit{0, 0, 0}, lpos{0, 0, 0};
-        if (active) {
-            if (MODE == kModeShadow) {
-                // consecutive lanes = consecutive hits of one light: coherent rays
-                l = (uint32_t)(item / nh);
-                h = (uint32_t)(item - (uint64_t)l * nh);
-                hit = vload(hits[h].h);
-                lpos = V3{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
-                V3 ldir = norm(sub(lpos, hit));       // tracer.go:61
-                o = add(hit, scale(ldir, 0.0001));    // tracer.go:64
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+        const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
+        const uint32_t nch = (nh + 63) / 64;
+        const uint32_t items = nch * fa.n_lights;
+        cnt_t* qc = &wa.counters[cnt_queue(1, q)];
+        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        while (k < items) {
+            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
+            ++taken;
+            const uint32_t l = k / nch, c = k - l * nch;
+            const uint32_t h = c * 64 + lane;
+            const bool active = h < nh;
+            V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
+            const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+            if (active) {
+                hit = vload(wa.hits[(size_t)q * wa.hit_cap + h].h);
+                V3 ldir = norm(sub(lpos, hit));     // tracer.go:61
+                o = add(hit, scale(ldir, 0.0001));  // tracer.go:64
                 d = ldir;
-            } else {
-                o = vload(io.orig + 3 * item);
-                d = vload(io.dir + 3 * item);
             }
-        }
-        Visits vis{0, 0, 0};
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, stacks[threadIdx.x >> 6], RESIDENT, o, d, active,
-                                                           MODE == kModeRays, vis);
-        ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-        ws.nodes += vis.nodes;
-        ws.leaves += vis.leaves;
-        if (active) {
-            if (MODE == kModeShadow) {
+            Visits vis{0, 0, 0};
+            bool is_lit;
+            if (segment) {
+                is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, hit, o, d, lpos, active, vis);
+            } else {
+                Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, false, vis);
                 // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
-                const bool is_lit = !r.ok || len(sub(lpos, hit)) < len(sub(r.hit, hit));
-                lit[(uint64_t)l * nh + h] = is_lit ? 1 : 0;
-            } else {
-                io.ok[item] = r.ok ? 1 : 0;
-                vstore(io.hit + 3 * item, r.ok ? r.hit : V3{0, 0, 0});
-                vstore(io.normal + 3 * item, r.ok ? r.normal : V3{0, 0, 0});
-                io.face[item] = r.ok ? (int32_t)r.face : -1;
-                io.object[item] = r.ok ? (int32_t)r.obj : -1;
+                is_lit = !r.ok || len(sub(lpos, hit)) < len(sub(r.hit, hit));
             }
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            if (active) wa.lit[((size_t)q * fa.n_lights + l) * wa.hit_cap + h] = is_lit ? 1 : 0;
+            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
-    if (MODE == kModeShadow) stats_flush(counters, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, ws);
+    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, ws);
+    if (wa.timeline) clock.record(wa, 1, taken);
+}
+
+// ---------------------------------------------------------------- arbitrary rays
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__global__ __launch_bounds__(kWG, 4) void k_rays(const FrameArgs fa, RayIO io) {
+    __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
+    if (RESIDENT) {
+        stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
+        __syncthreads();
+    }
+    const uint64_t nchunks = ((uint64_t)io.n + kWG - 1) / kWG;
+    for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const uint64_t item = chunk * kWG + threadIdx.x;
+        const bool active = item < io.n;
+        V3 o{0, 0, 0}, d{1, 0, 0};
+        if (active) {
+            o = vload(io.orig + 3 * item);
+            d = vload(io.dir + 3 * item);
+        }
+        Visits vis{0, 0, 0};
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, true, vis);
+        if (active) {
+            io.ok[item] = r.ok ? 1 : 0;
+            vstore(io.hit + 3 * item, r.ok ? r.hit : V3{0, 0, 0});
+            vstore(io.normal + 3 * item, r.ok ? r.normal : V3{0, 0, 0});
+            io.face[item] = r.ok ? (int32_t)r.face : -1;
+            io.object[item] = r.ok ? (int32_t)r.obj : -1;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- shade
-__global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const HitRec* __restrict__ hits,
-                                               const cnt_t* __restrict__ counters,
-                                               const uint8_t* __restrict__ lit, OutPlanes out) {
-    const uint32_t nh = (uint32_t)counters[kCntHits];
+// tracer.go:53-76 phong for every hit; waves walk (region, 64-hit chunk) round-robin.
+__global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (256 / 64) + (threadIdx.x >> 6), nw = gridDim.x * (256 / 64);
+    const uint32_t chunks_per_region = wa.hit_cap / 64;
+    const uint64_t nchunks = (uint64_t)kQShards * chunks_per_region;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
-        const HitRec hr = hits[h];
+    for (uint64_t ck = gw; ck < nchunks; ck += nw) {
+        const uint32_t q = (uint32_t)(ck % kQShards), c = (uint32_t)(ck / kQShards);
+        const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
+        if (c * 64 >= nh) continue;
+        const uint32_t h = c * 64 + lane;
+        if (h >= nh) continue;
+        const HitRec hr = wa.hits[(size_t)q * wa.hit_cap + h];
         const DevMesh& m = fa.obj[hr.obj].m;
         const double* mt = m.mats + (size_t)hr.mat * 10;
         RGB ka{mt[0], mt[1], mt[2]}, kd{mt[3], mt[4], mt[5]}, ks{mt[6], mt[7], mt[8]};
         const double ns = mt[9];
         const V3 hit = vload(hr.h), n = vload(hr.n);
-        RGB c = ka;  // tracer.go:56
+        RGB col = ka;  // tracer.go:56
         for (uint32_t l = 0; l < fa.n_lights; ++l) {
-            if (!lit[(uint64_t)l * nh + h]) continue;
+            if (!wa.lit[((size_t)q * fa.n_lights + l) * wa.hit_cap + h]) continue;
             const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
             const RGB lcol{fa.lcol[l][0], fa.lcol[l][1], fa.lcol[l][2]};
             const V3 ldir = norm(sub(lpos, hit));                         // tracer.go:61
             const V3 refl = sub(scale(n, 2 * dot(ldir, n)), ldir);        // tracer.go:65
             const V3 camdir = norm(sub(cam, hit));                        // tracer.go:66
-            c = c_add(c, c_mul(c_scale(kd, go_max(dot(ldir, n), 0.0)), lcol));                // :69
-            c = c_add(c, c_mul(c_scale(ks, go_pow(go_max(dot(refl, camdir), 0.0), ns)), lcol));  // :72
+            col = c_add(col, c_mul(c_scale(kd, go_max(dot(ldir, n), 0.0)), lcol));                // :69
+            col = c_add(col, c_mul(c_scale(ks, go_pow(go_max(dot(refl, camdir), 0.0), ns)), lcol));  // :72
         }
         if (out.rgb) {
-            out.rgb[3 * hr.out] = c.r;
-            out.rgb[3 * hr.out + 1] = c.g;
-            out.rgb[3 * hr.out + 2] = c.b;
+            out.rgb[3 * hr.out] = col.r;
+            out.rgb[3 * hr.out + 1] = col.g;
+            out.rgb[3 * hr.out + 2] = col.b;
         }
         if (out.rgb8) {
-            out.rgb8[3 * hr.out] = c_u8(c.r);
-            out.rgb8[3 * hr.out + 1] = c_u8(c.g);
-            out.rgb8[3 * hr.out + 2] = c_u8(c.b);
+            out.rgb8[3 * hr.out] = c_u8(col.r);
+            out.rgb8[3 * hr.out + 1] = c_u8(col.g);
+            out.rgb8[3 * hr.out + 2] = c_u8(col.b);
         }
     }
 }
@@ -632,7 +779,6 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
 }
 
 // ---------------------------------------------------------------- launchers
-// opts: MIRT_OPT_* bits (mirt.h)
 // opts: MIRT_OPT_* bits (mirt.h); resident: one object whose mesh fits in LDS.
 #define MIRT_DISPATCH(KERNEL)                                                                      \
     do {                                                                                           \
@@ -654,23 +800,18 @@ static bool is_resident(const FrameArgs& fa) {
     return fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
 }
 
-hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, cnt_t* counters, int grid, uint32_t opts,
+hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_PRIM(P, B, R) \
-    hipLaunchKernelGGL((k_primary<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, tiles, ntiles, total_units, out, hits, counters)
+#define K_PRIM(P, B, R) hipLaunchKernelGGL((k_primary<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
     MIRT_DISPATCH(K_PRIM);
 #undef K_PRIM
     return hipGetLastError();
 }
 
-hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, cnt_t* counters, uint8_t* lit, int grid,
-                         uint32_t opts, hipStream_t s) {
-    RayIO none{};
+hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, int grid, uint32_t opts, hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_SHADOW(P, B, R) \
-    hipLaunchKernelGGL((k_secondary<kModeShadow, P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, hits, counters, lit, none)
+#define K_SHADOW(P, B, R) hipLaunchKernelGGL((k_shadow<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa)
     MIRT_DISPATCH(K_SHADOW);
 #undef K_SHADOW
     return hipGetLastError();
@@ -678,17 +819,14 @@ hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, cnt_t* counter
 
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_RAYS(P, B, R)                                                                                        \
-    hipLaunchKernelGGL((k_secondary<kModeRays, P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, (const HitRec*)nullptr, \
-                       (cnt_t*)nullptr, (uint8_t*)nullptr, io)
+#define K_RAYS(P, B, R) hipLaunchKernelGGL((k_rays<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, io)
     MIRT_DISPATCH(K_RAYS);
 #undef K_RAYS
     return hipGetLastError();
 }
 
-hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const cnt_t* counters, const uint8_t* lit,
-                        const OutPlanes& out, uint64_t /*lit_stride*/, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(256), 0, s, fa, hits, counters, lit, out);
+hipError_t launch_shade(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(256), 0, s, fa, wa, out);
     return hipGetLastError();
 }
 

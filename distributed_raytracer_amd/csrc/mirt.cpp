@@ -66,6 +66,13 @@ struct Slot {
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
     size_t tiles_cap = 0, h_tiles_cap = 0;
+    // per-block work items of the last tile list traced on this slot (reused while the
+    // caller keeps sending the same list: no host rebuild, no upload)
+    BlockDesc* d_blocks = nullptr;
+    BlockDesc* h_blocks = nullptr;  // pinned staging
+    size_t blocks_cap = 0, h_blocks_cap = 0;
+    std::vector<mirt_tile> blocks_key;
+    uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0;
     cnt_t* h_counters = nullptr;  // pinned
     // device-side outputs for the host-buffer API
     void* out_buf = nullptr;
@@ -91,6 +98,8 @@ struct mirt_ctx {
     bool profiling = false;
     std::vector<ProfRec> prof_pending;
     std::vector<ProfRec> prof_free;
+    uint64_t* timeline = nullptr;  // MIRT_OPT_TIMELINE buffer (2 kernels x timeline_cap waves)
+    uint32_t timeline_cap = 0;
 };
 
 namespace {
@@ -219,6 +228,7 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
     fa.halfH = (int32_t)(H / 2);
     fa.n_objects = f->n_objects;
     fa.n_lights = f->n_lights;
+    fa.flags = c->flags;
     tris = 0;
     for (uint32_t i = 0; i < f->n_objects; ++i) {
         const MeshDev& m = c->meshes[f->objects[i].mesh_id];
@@ -257,70 +267,120 @@ int prof_get(mirt_ctx* c, ProfRec& r) {
 }
 
 // Enqueue primary -> shadow -> shade for a tile list on stream s.
+// Block table of a tile list: one BlockDesc per 8x8 block, tiles in list order, blocks of
+// a tile column-major.  Rebuilt and uploaded only when the list changes.
+int blocks_prepare(Slot* sl, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n, hipStream_t s) {
+    if (sl->blocks_W == W && sl->blocks_H == H && sl->blocks_key.size() == n &&
+        memcmp(sl->blocks_key.data(), tiles, sizeof(mirt_tile) * n) == 0)
+        return MIRT_OK;
+    sl->blocks_key.clear();
+    uint64_t nb = 0;
+    for (uint32_t t = 0; t < n; ++t)
+        nb += (uint64_t)((tiles[t].w + kBlk - 1) / kBlk) * ((tiles[t].h + kBlk - 1) / kBlk);
+    if (nb > 0x7fffffffull) return fail(MIRT_E_LIMIT, "too many 8x8 blocks in one call");
+    int r = dev_grow(sl->d_blocks, sl->blocks_cap, nb);
+    if (r != MIRT_OK) return r;
+    if (sl->h_blocks_cap < nb) {
+        if (sl->h_blocks) (void)hipHostFree(sl->h_blocks);
+        sl->h_blocks = nullptr;
+        sl->h_blocks_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&sl->h_blocks, sizeof(BlockDesc) * nb));
+        sl->h_blocks_cap = nb;
+    }
+    uint64_t off = 0, k = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        const mirt_tile& tl = tiles[t];
+        for (uint32_t bx = 0; bx < tl.w; bx += kBlk)
+            for (uint32_t by = 0; by < tl.h; by += kBlk) {
+                BlockDesc& b = sl->h_blocks[k++];
+                b.out = off + (uint64_t)bx * tl.h + by;
+                b.px = tl.x + bx;
+                b.py = tl.y + by;
+                b.th = tl.h;
+                b.vw = std::min<uint32_t>(kBlk, tl.w - bx);
+                b.vh = std::min<uint32_t>(kBlk, tl.h - by);
+                b.pad = 0;
+            }
+        off += (uint64_t)tl.w * tl.h;
+    }
+    HIP_TRY(hipMemcpyAsync(sl->d_blocks, sl->h_blocks, sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, s));
+    sl->blocks_key.assign(tiles, tiles + n);
+    sl->blocks_W = W;
+    sl->blocks_H = H;
+    sl->nblocks = (uint32_t)nb;
+    return MIRT_OK;
+}
+
+// Enqueue primary -> shadow -> shade for a tile list on stream s.
 int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
                   uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel, uint64_t* pixels_out,
                   uint64_t* tris_out) {
     if (W == 0 || H == 0) return fail(MIRT_E_INVALID, "screen width/height must be > 0");
     if (n == 0 || !tiles) return fail(MIRT_E_INVALID, "empty tile list");
     uint64_t pixels = 0;
-    uint32_t units = 0;
     int r = MIRT_OK;
-    if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
     for (uint32_t t = 0; t < n; ++t) {
         const mirt_tile& tl = tiles[t];
         if (tl.w == 0 || tl.h == 0) return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty");
         if ((uint64_t)tl.x + tl.w > W || (uint64_t)tl.y + tl.h > H)
             return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " exceeds the screen");
-        TileDesc& d = sl->h_tiles[t];
-        d.x = tl.x;
-        d.y = tl.y;
-        d.w = tl.w;
-        d.h = tl.h;
-        d.out_off = pixels;
-        d.unit_begin = units;
-        d.units_w = (tl.w + kUnitW - 1) / kUnitW;
-        uint64_t u = (uint64_t)d.units_w * ((tl.h + kUnitH - 1) / kUnitH);
-        if ((uint64_t)units + u > 0xffffffffull) return fail(MIRT_E_LIMIT, "too many work units");
-        units += (uint32_t)u;
         pixels += (uint64_t)tl.w * tl.h;
     }
     if (pixels > 0xffffffffull) return fail(MIRT_E_LIMIT, "more than 2^32 pixels in one call");
     FrameArgs fa;
     uint64_t tris = 0;
     fill_args(c, f, W, H, fa, tris);
-    if ((r = dev_grow(sl->hits, sl->hits_cap, pixels)) != MIRT_OK) return r;
-    if ((r = dev_grow(sl->lit, sl->lit_cap, pixels * std::max<uint32_t>(f->n_lights, 1))) != MIRT_OK) return r;
+    if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
+    const uint32_t nl = f->n_lights;
+    WorkArgs wa{};
+    wa.blocks = sl->d_blocks;
+    wa.nblocks = sl->nblocks;
+    wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
+    const uint64_t hit_slots = (uint64_t)kQShards * wa.hit_cap;
+    if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
+    if ((r = dev_grow(sl->lit, sl->lit_cap, hit_slots * std::max<uint32_t>(nl, 1))) != MIRT_OK) return r;
+    wa.hits = sl->hits;
+    wa.lit = sl->lit;
+    wa.counters = sl->counters;
+    wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE) ? 0u : 1u;
+    if (c->flags & MIRT_OPT_TIMELINE) {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->timeline) {
+            const uint32_t cap = (uint32_t)(2 * c->cus * (kWG / 64));
+            HIP_TRY(hipMalloc((void**)&c->timeline, sizeof(uint64_t) * kTimelineRec * 2 * cap));
+            c->timeline_cap = cap;
+        }
+        HIP_TRY(hipMemsetAsync(c->timeline, 0, sizeof(uint64_t) * kTimelineRec * 2 * c->timeline_cap, s));
+        wa.timeline = c->timeline;
+        wa.timeline_cap = c->timeline_cap;
+    }
 
     ProfRec pr;
     const bool prof = c->profiling;
     if (prof && (r = prof_get(c, pr)) != MIRT_OK) return r;
 
-    HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(cnt_t), s));
-    // persistent: two 512-thread workgroups per CU walk the units; MIRT_OPT_NONPERSISTENT
-    // launches one workgroup per unit and lets the dispatcher balance the load.
-    const int pgrid = (c->flags & MIRT_OPT_NONPERSISTENT) ? (int)units
-                                                           : (int)std::min<uint64_t>(units, (uint64_t)2 * c->cus);
+    // persistent: two 512-thread workgroups per CU; waves take work from the queues
+    const int pgrid = (int)std::max<uint64_t>(
+        1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
     const int sgrid = (int)std::max<uint64_t>(
-        1, std::min<uint64_t>((pixels * std::max<uint32_t>(f->n_lights, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
+        1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((pixels + 255) / 256, (uint64_t)8 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    HIP_TRY(launch_primary(fa, sl->d_tiles, n, units, out, sl->hits, sl->counters, pgrid, c->flags, s));
+    HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
     if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-    if (f->n_lights) {
-        HIP_TRY(launch_shadow(fa, sl->hits, sl->counters, sl->lit, sgrid, c->flags, s));
-    }
+    if (nl) HIP_TRY(launch_shadow(fa, wa, sgrid, c->flags, s));
     if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-    HIP_TRY(launch_shade(fa, sl->hits, sl->counters, sl->lit, out, pixels, hgrid, s));
+    HIP_TRY(launch_shade(fa, wa, out, hgrid, s));
     if (prof) {
         HIP_TRY(hipEventRecord(pr.ev[3], s));
         HIP_TRY(hipMemcpyAsync(pr.h_cnt, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
         pr.pixels = pixels;
         pr.tris = tris;
-        pr.nl = f->n_lights;
+        pr.nl = nl;
         std::lock_guard<std::mutex> g(c->mu);
         c->prof_pending.push_back(pr);
     }
@@ -333,7 +393,12 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 
 uint64_t stat_sum(const cnt_t* c, int stat) {
     uint64_t s = 0;
-    for (int k = 0; k < kShards; ++k) s += c[kStatBase + stat * kShards + k];
+    for (int k = 0; k < kStatShards; ++k) s += c[cnt_stat(stat, k)];
+    return s;
+}
+uint64_t hits_sum(const cnt_t* c) {
+    uint64_t s = 0;
+    for (int k = 0; k < kQShards; ++k) s += c[cnt_hits(k)];
     return s;
 }
 
@@ -342,7 +407,7 @@ int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t
     HIP_TRY(hipStreamSynchronize(s));
     memset(st, 0, sizeof(*st));
     st->primary_rays = pixels;
-    st->hits = sl->h_counters[kCntHits];
+    st->hits = hits_sum(sl->h_counters);
     st->shadow_rays = st->hits * nl;
     st->tri_tests = stat_sum(sl->h_counters, kStatPrimTests) + stat_sum(sl->h_counters, kStatShadowTests);
     return MIRT_OK;
@@ -384,6 +449,8 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->lit) (void)hipFree(s->lit);
         if (s->counters) (void)hipFree(s->counters);
         if (s->d_tiles) (void)hipFree(s->d_tiles);
+        if (s->d_blocks) (void)hipFree(s->d_blocks);
+        if (s->h_blocks) (void)hipHostFree(s->h_blocks);
         if (s->h_tiles) (void)hipHostFree(s->h_tiles);
         if (s->h_counters) (void)hipHostFree(s->h_counters);
         if (s->out_buf) (void)hipFree(s->out_buf);
@@ -397,6 +464,7 @@ void mirt_destroy(mirt_ctx* c) {
             if (r.h_cnt) (void)hipHostFree(r.h_cnt);
         }
     for (auto& m : c->meshes) mesh_free(m);
+    if (c->timeline) (void)hipFree(c->timeline);
     delete c;
 }
 
@@ -644,7 +712,7 @@ int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile
             !tiles[t].h)
             return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty or exceeds the screen");
         TileDesc& d = sl->h_tiles[t];
-        d = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, pixels, 0, 0};
+        d = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, pixels, {0, 0}};
         pixels += (uint64_t)tiles[t].w * tiles[t].h;
     }
     HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
@@ -732,7 +800,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->shadow_ms_sum += b;
         out->shade_ms_sum += d;
         out->frame_ms_sum += t;
-        const uint64_t hits = r.h_cnt[kCntHits];
+        const uint64_t hits = hits_sum(r.h_cnt);
         out->primary_rays += r.pixels;
         out->hits += hits;
         out->shadow_rays += hits * r.nl;
@@ -746,6 +814,23 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);
     return MIRT_OK;
+}
+
+int mirt_debug_timeline(mirt_ctx* c, uint64_t* out, uint32_t max_records) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->timeline) return 0;
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<uint64_t> all((size_t)kTimelineRec * 2 * c->timeline_cap);
+    HIP_TRY(hipMemcpy(all.data(), c->timeline, all.size() * 8, hipMemcpyDeviceToHost));
+    uint32_t n = 0;
+    for (size_t r = 0; r < (size_t)2 * c->timeline_cap && n < max_records; ++r) {
+        const uint64_t* rec = &all[r * kTimelineRec];
+        if (rec[2] == 0) continue;  // wave slot not launched
+        memcpy(out + (size_t)n * kTimelineRec, rec, kTimelineRec * 8);
+        ++n;
+    }
+    return (int)n;
 }
 
 int mirt_debug_fp64(mirt_ctx* c, int op, uint32_t n, const double* a, const double* b, double* out) {

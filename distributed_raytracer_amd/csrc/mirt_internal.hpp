@@ -8,10 +8,11 @@
 
 namespace mirt {
 
-// Launch geometry.  One workgroup = 8 waves; each wave traces an 8x8 pixel block, so a
-// workgroup's unit of primary work is a 32x16 pixel block of one tile.
+// Launch geometry.  Persistent workgroups of 8 waves (two per CU: the LDS mesh copy is
+// 72 KiB).  A wave's unit of primary work is one 8x8 pixel block; waves take blocks
+// from a sharded work queue independently of each other (see the counter layout below).
 constexpr int kWG = 512;
-constexpr int kUnitW = 32, kUnitH = 16;
+constexpr int kBlk = 8;
 // Doubles per triangle record in HBM and LDS: P1, E1 = P2-P1, E2 = P3-P1 (72 B).
 constexpr int kTriD = 9;
 // Triangles one workgroup holds in LDS (73,728 B; two workgroups per CU fit in 160 KiB).
@@ -36,7 +37,7 @@ constexpr uint32_t kBvhLeafBit = 0x80000000u;
 constexpr int kBvhCountShift = 24;
 constexpr uint32_t kBvhFirstMask = 0x00ffffffu;
 constexpr int kBvhLeaf = 4;           // max triangles per leaf
-constexpr int kBvhStack = 128;        // per-wave traversal stack entries (LDS)
+constexpr int kBvhStack = 128;        // per-wave traversal stack entries (two VGPRs, one per lane)
 constexpr int kBvhMaxDepth = (kBvhStack - 1) / 7;
 
 // One uploaded mesh, device pointers (shared/state/mesh.go:100-106).  Every per-face
@@ -80,8 +81,26 @@ struct FrameArgs {
 struct TileDesc {
     uint32_t x, y, w, h;
     uint64_t out_off;      // first packed pixel of this tile
-    uint32_t unit_begin;   // first 32x16 work unit of this tile
-    uint32_t units_w;      // ceil(w / 32)
+    uint32_t pad[2];
+};
+
+// One 8x8 pixel block of one tile: the primary kernel's work item.  Built on the host
+// per tile list (cached while the list does not change), so a wave finds its pixels with
+// one scalar load instead of a search over the tile list.
+struct alignas(32) BlockDesc {
+    uint64_t out;          // packed index of the block's (0, 0) pixel
+    uint32_t px, py;       // screen pixel of (0, 0)
+    uint32_t th;           // height of the tile (column stride of the packed tile)
+    uint32_t vw, vh;       // valid columns / rows (<= 8)
+    uint32_t pad;
+};
+
+struct OutPlanes {
+    double* rgb;
+    uint8_t* rgb8;
+    uint8_t* valid;
+    int32_t* face;
+    int32_t* object;
 };
 
 // A primary hit handed from the primary kernel to the shadow and shade kernels.
@@ -93,28 +112,39 @@ struct HitRec {
     uint32_t mat;    // material index inside that object's mesh
 };
 
-struct OutPlanes {
-    double* rgb;
-    uint8_t* rgb8;
-    uint8_t* valid;
-    int32_t* face;
-    int32_t* object;
-};
-
-// Counters kept in device memory per call slot.
-// 64-bit: hits, ray-triangle tests performed by the primary / shadow kernels.
-// counters[0] is the hit count that compaction allocates from (one atomic per wave that
-// has hits).  Statistics live in kShards-way sharded slots, counters[kStatBase +
-// stat*kShards + shard], each wave adding its totals ONCE at the end of a persistent
-// kernel: same-address atomics serialise at ~90 per microsecond on MI355X, so per-unit
-// counting would cost more than the tracing.  The host sums the shards.
-enum { kCntHits = 0, kStatBase = 8, kShards = 8 };
+// Counters kept in device memory per call slot, zeroed before every frame.  Each counter
+// owns a 128-byte line: same-line atomics serialise (~90 per microsecond on MI355X), so
+// every contended counter is split kQShards ways.
+//   queue(q, s): work-queue tickets of kernel q (0 primary, 1 shadow) for shard s.
+//     Primary block b belongs to shard b % kQShards; a wave serves the shard
+//     (global wave id % kQShards) and takes one block per ticket.
+//   hits(s):     hit compaction of shard s.  Hits of the blocks of shard s are packed into
+//     region s (capacity hit_cap = ceil(blocks / kQShards) * 64 records), so the shadow
+//     and shade kernels walk regions without any cross-shard prefix sum.
+//   stat(k, s):  statistics (ray-triangle tests, BVH node/leaf visits), reduced per
+//     workgroup in LDS and added once per workgroup into shard blockIdx % kStatShards.
+constexpr int kQShards = 64, kStatShards = 8, kLine = 16;
 enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kStatShadowNodes,
        kStatShadowLeaves, kStatN };
-constexpr int kCntN = kStatBase + kStatN * kShards;
+__host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
+__host__ __device__ constexpr int cnt_hits(int s) { return (2 * kQShards + s) * kLine; }
+__host__ __device__ constexpr int cnt_stat(int k, int s) { return (3 * kQShards + k * kStatShards + s) * kLine; }
+constexpr int kCntN = (3 * kQShards + kStatN * kStatShards) * kLine;
 typedef unsigned long long cnt_t;
 
-enum SecondaryMode { kModeShadow = 0, kModeRays = 1 };
+// Per-frame work description shared by the primary, shadow and shade kernels.
+struct WorkArgs {
+    const BlockDesc* blocks;
+    uint32_t nblocks;
+    uint32_t hit_cap;      // records per hit region (multiple of 64)
+    HitRec* hits;          // kQShards regions of hit_cap records
+    uint8_t* lit;          // kQShards x n_lights regions of hit_cap flags
+    cnt_t* counters;
+    uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
+    uint32_t timeline_cap; // records the timeline buffer holds per kernel
+    uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
+};
+constexpr int kTimelineRec = 8;
 
 // Arbitrary-ray inputs/outputs for mirt_trace_rays.
 struct RayIO {
@@ -128,13 +158,10 @@ struct RayIO {
     uint32_t n;
 };
 
-hipError_t launch_primary(const FrameArgs& fa, const TileDesc* tiles, uint32_t ntiles, uint32_t total_units,
-                          const OutPlanes& out, HitRec* hits, cnt_t* counters, int grid, uint32_t opts,
+hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
-hipError_t launch_shadow(const FrameArgs& fa, const HitRec* hits, cnt_t* counters, uint8_t* lit,
-                         int grid, uint32_t opts, hipStream_t s);
-hipError_t launch_shade(const FrameArgs& fa, const HitRec* hits, const cnt_t* counters, const uint8_t* lit,
-                        const OutPlanes& out, uint64_t lit_stride, int grid, hipStream_t s);
+hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, int grid, uint32_t opts, hipStream_t s);
+hipError_t launch_shade(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,

@@ -118,6 +118,13 @@ class Context:
         L.check(L.lib().mirt_debug_fp64(self.handle, op, len(a), a.ctypes.data, b.ctypes.data, out.ctypes.data))
         return out
 
+    def debug_timeline(self, max_records: int = 1 << 16) -> np.ndarray:
+        """Per-wave stamps of the last frame traced with MIRT_OPT_TIMELINE (mirt.h)."""
+        out = np.zeros((max_records, 8), np.uint64)
+        n = L.lib().mirt_debug_timeline(self.handle, out.ctypes.data, max_records)
+        L.check(min(n, 0))
+        return out[:n]
+
 
 # --------------------------------------------------------------------- scene
 @dataclass

@@ -204,7 +204,9 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 /* Ask for kernel variants (benchmark ablations).  0 = defaults. */
 #define MIRT_OPT_NO_PREFILTER 1u  /* always take the true fp64 divide for r2 */
 #define MIRT_OPT_BRUTE_FORCE 2u   /* test every triangle (no BVH culling), mesh streamed via LDS */
-#define MIRT_OPT_NONPERSISTENT 4u /* one primary workgroup per 32x16 unit (no persistent loop) */
+#define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split instead of the dynamic work queues */
+#define MIRT_OPT_TIMELINE 8u        /* record per-wave start/end stamps (mirt_debug_timeline) */
+#define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*
@@ -213,6 +215,18 @@ int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
  *   op 0: sqrt(a)   op 1: a / b   op 2: Go math.Pow(a, b)   op 3: Go math.Max(a, b)
  */
 int mirt_debug_fp64(mirt_ctx *ctx, int op, uint32_t n, const double *a, const double *b, double *out);
+
+/*
+ * Diagnostic: per-wave timeline of the last traced frame while MIRT_OPT_TIMELINE is set
+ * (one context-wide buffer: concurrent calls overwrite each other).  Synchronises the
+ * device, copies up to max_records records of 8 uint64 each into out and returns the
+ * number of records (>= 0) or a negative MIRT_E_* code.  Record:
+ *   [0] kernel (0 primary, 1 shadow)  [1] global wave id
+ *   [2] s_memrealtime at wave start   [3] at wave end (100 MHz constant clock)
+ *   [4] s_memtime at wave start       [5] at wave end (shader clock)
+ *   [6] HW_ID register                [7] XCC id | work items taken << 32
+ */
+int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,83 @@
+"""Per-wave timeline of one frame (MIRT_OPT_TIMELINE): when waves start and end, the
+shader clock they ran at, work items per wave, per-XCD spread.
+
+usage (GPU box): python tools/timeline.py [--width W --height H --frames N --static]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def summarize(rec: np.ndarray) -> dict:
+    out = {}
+    for kern, name in ((0, "primary"), (1, "shadow")):
+        r = rec[rec[:, 0] == kern].astype(np.float64)
+        if not len(r):
+            continue
+        t0 = r[:, 2].min()
+        start = (r[:, 2] - t0) * 10.0  # 100 MHz ticks -> ns
+        end = (r[:, 3] - t0) * 10.0
+        life = end - start
+        clk_ghz = (r[:, 5] - r[:, 4]) / np.maximum(life, 1.0)
+        items = (r[:, 7].astype(np.uint64) >> np.uint64(32)).astype(np.float64)
+        xcc = (r[:, 7].astype(np.uint64) & np.uint64(0xffff)).astype(np.int64)
+        q = lambda a: [round(float(np.percentile(a, p)) / 1e3, 2) for p in (0, 10, 50, 90, 100)]
+        out[name] = {
+            "waves": int(len(r)),
+            "span_us": round(float(end.max()) / 1e3, 2),
+            "start_us_p0_10_50_90_100": q(start),
+            "end_us_p0_10_50_90_100": q(end),
+            "mean_life_frac_of_span": round(float(life.mean() / end.max()), 3),
+            "shader_clock_ghz_median": round(float(np.median(clk_ghz)), 3),
+            "items_per_wave_p0_50_100": [int(np.percentile(items, p)) for p in (0, 50, 100)],
+            "per_xcc_end_us_max": {int(x): round(float(end[xcc == x].max()) / 1e3, 2) for x in np.unique(xcc)},
+        }
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--static", action="store_true")
+    ap.add_argument("--save", default="")
+    a = ap.parse_args()
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import FrameSharder
+    ctx = rt.Context(0)
+    env = rt.Environment.from_file(os.path.join(ROOT, "tests", "golden", "example", "scene.json"), ctx)
+    frame = env.mutable().to_frame()
+    sh = FrameSharder(ctx, a.width, a.height, 0, 1, 64)
+    opts = rt._lib.MIRT_OPT_TIMELINE | (rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static else 0)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        ctx.set_options(0)
+        for _ in range(3):
+            sh.render(frame)
+        torch.cuda.synchronize()
+        ctx.set_options(opts)
+        res = []
+        for _ in range(a.frames):
+            sh.render(frame)
+            torch.cuda.synchronize()
+            rec = ctx.debug_timeline()
+            res.append(summarize(rec))
+            if a.save:
+                np.save(a.save, rec)
+        ctx.set_options(0)
+    for r in res[-2:]:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
