@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmirt.so")
+# MIRT_LIB: load another build of the library (A/B experiments with kernel variants)
+LIB_PATH = os.environ.get("MIRT_LIB") or os.path.join(_HERE, "libmirt.so")
 
 MIRT_OK = 0
 MIRT_E_INVALID = -1
@@ -73,7 +74,8 @@ class Profile(C.Structure):
                 ("primary_tri_tests", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
                 ("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
                 ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
-                ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64)]
+                ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64),
+                ("stack_overflows", C.c_uint64)]
 
 
 class MeshView(C.Structure):

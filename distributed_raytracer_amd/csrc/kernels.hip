@@ -198,30 +198,34 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
 }
 
 struct Visits {
-    uint32_t tests;   // triangles tested by the wave (x active lanes = ray-triangle tests)
-    uint32_t nodes;   // BVH nodes whose box the wave tested
-    uint32_t leaves;  // leaves the wave entered
+    uint32_t tests;     // triangles tested by the wave (x active lanes = ray-triangle tests)
+    uint32_t nodes;     // BVH nodes whose children the wave tested
+    uint32_t leaves;    // leaves the wave entered
+    uint32_t overflow;  // wide-traversal stack overflows (never expected; tests assert 0)
 };
 // Per-wave totals over a whole persistent kernel.  At the end every wave parks its totals
 // in LDS and one lane of the workgroup adds the sums into shard blockIdx % kStatShards:
 // one atomic per statistic per workgroup (see the counter layout in mirt_internal.hpp).
 struct WaveStats {
-    cnt_t tests, nodes, leaves;
+    cnt_t tests, nodes, leaves, hits, overflow;
 };
-__device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[3], int stat_tests, int stat_nodes,
-                                            int stat_leaves, const WaveStats& w) {
+__device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], int stat_tests, int stat_nodes,
+                                            int stat_leaves, int stat_hits, const WaveStats& w) {
     const uint32_t wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[wave][0] = w.tests;
         red[wave][1] = w.nodes;
         red[wave][2] = w.leaves;
+        red[wave][3] = w.hits;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if ((threadIdx.x & 63) == 0 && w.overflow) atomicAdd(&counters[cnt_stat(kStatOverflow, 0)], w.overflow);
+    if (threadIdx.x < 4) {
         cnt_t sum = 0;
         for (int k = 0; k < kWG / 64; ++k) sum += red[k][threadIdx.x];
-        const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes : stat_leaves;
-        if (sum) atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
+        const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes
+                       : threadIdx.x == 2 ? stat_leaves : stat_hits;
+        if (sum && stat >= 0) atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
     }
 }
 
@@ -338,6 +342,190 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
     }
 }
 
+// Occupancy target of the tracing kernels (waves per SIMD) and LDS-resident meshes.
+#ifndef MIRT_WAVES_PER_EU
+#define MIRT_WAVES_PER_EU 4
+#endif
+#ifndef MIRT_LDS_MESH
+#define MIRT_LDS_MESH 1
+#endif
+// Traversal per kernel: 1 = wide cone traversal (shared-origin packets), 0 = per-lane
+// 8-child sweep with scalar node loads.  Measured on MI355X (suzanne 1080p): the sweep is
+// faster for both (profiles/r01_*); the wide walk stays for meshes where it wins.
+#ifndef MIRT_PRIMARY_WIDE
+#define MIRT_PRIMARY_WIDE 0
+#endif
+#ifndef MIRT_SHADOW_WIDE
+#define MIRT_SHADOW_WIDE 0
+#endif
+#define MIRT_TRACE_KERNEL __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_WAVES_PER_EU)))
+
+// ---------------------------------------------------------------- wide traversal
+#ifndef MIRT_LEAF_LANE_TEST
+#define MIRT_LEAF_LANE_TEST 1
+#endif
+// Wave reductions over 64 lanes (DPP row shifts + row broadcasts; every lane active,
+// lanes without data hold the identity).  Result read from lane 63: wave-uniform.
+template <bool MIN, int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ float dpp_step(float v) {
+    const float id = MIN ? __builtin_inff() : -__builtin_inff();
+    const int t = __builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), CTRL, ROW_MASK, BANK_MASK, false);
+    return MIN ? fminf(v, __int_as_float(t)) : fmaxf(v, __int_as_float(t));
+}
+template <bool MIN>
+__device__ __forceinline__ float wave_reduce(float v) {
+    v = dpp_step<MIN, 0x111, 0xf, 0xf>(v);  // row_shr:1
+    v = dpp_step<MIN, 0x112, 0xf, 0xf>(v);  // row_shr:2
+    v = dpp_step<MIN, 0x113, 0xf, 0xf>(v);  // row_shr:3
+    v = dpp_step<MIN, 0x114, 0xf, 0xe>(v);  // row_shr:4
+    v = dpp_step<MIN, 0x118, 0xf, 0xc>(v);  // row_shr:8
+    v = dpp_step<MIN, 0x142, 0xa, 0xf>(v);  // row_bcast:15
+    v = dpp_step<MIN, 0x143, 0xc, 0xf>(v);  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// A packet of rays through one common point C (object space): the camera for primary
+// rays, the light for shadow rays walked backwards.  Lane ray: C + s * e_lane with s in
+// [smin, smax].  The cone keeps, per axis, the range of the lanes' fp32 1/e; a child box
+// is entered iff the interval slab test passes:
+//   (bound - C) * (1/e) is linear in 1/e, so over the packet every lane's plane crossing
+//   lies between the values at the two endpoints of the range; the per-axis minimum of
+//   those four products bounds every lane's near crossing from below and the maximum
+//   bounds its far crossing from above.  If any lane's ray meets the box, the bounds pass.
+// fp32 rounding is covered by the 2^-12 x scale box inflation exactly as for the per-lane
+// test.  all = accept everything (origin beyond the cull limit, or a lane
+// with a non-finite direction).
+struct Cone {
+    float ixlo, ixhi, iylo, iyhi, izlo, izhi;      // range of 1/e over live lanes
+    float cxlo, cxhi, cylo, cyhi, czlo, czhi;      // C * each endpoint
+    float smin, smax;
+    bool all, none;
+};
+__device__ __forceinline__ float u_f(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ float u_lane(float x, uint32_t lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), (int)lane));
+}
+__device__ __forceinline__ Cone make_cone(V3 corig, float ix, float iy, float iz, bool live, bool force,
+                                          float smin_lane, float smax_lane, double cull_limit) {
+    Cone c;
+    c.none = __ballot(live) == 0;
+    const float cx = u_f((float)corig.x), cy = u_f((float)corig.y), cz = u_f((float)corig.z);
+    const double far = fmax(fmax(__builtin_fabs(corig.x), __builtin_fabs(corig.y)), __builtin_fabs(corig.z));
+    const bool bad = live && (force || !(__builtin_fabsf(ix) <= 0x1p61f && __builtin_fabsf(iy) <= 0x1p61f &&
+                                         __builtin_fabsf(iz) <= 0x1p61f && smax_lane >= smin_lane));
+    c.all = __ballot(bad) != 0 || !(u_f((float)far) <= (float)cull_limit && far <= cull_limit);
+    const float inf = __builtin_inff();
+    c.ixlo = wave_reduce<true>(live ? ix : inf);
+    c.ixhi = wave_reduce<false>(live ? ix : -inf);
+    c.iylo = wave_reduce<true>(live ? iy : inf);
+    c.iyhi = wave_reduce<false>(live ? iy : -inf);
+    c.izlo = wave_reduce<true>(live ? iz : inf);
+    c.izhi = wave_reduce<false>(live ? iz : -inf);
+    c.cxlo = cx * c.ixlo;
+    c.cxhi = cx * c.ixhi;
+    c.cylo = cy * c.iylo;
+    c.cyhi = cy * c.iyhi;
+    c.czlo = cz * c.izlo;
+    c.czhi = cz * c.izhi;
+    c.smin = wave_reduce<true>(live ? smin_lane : inf);
+    c.smax = wave_reduce<false>(live ? smax_lane : -inf);
+    return c;
+}
+__device__ __forceinline__ bool cone_box(const Cone& c, float lx, float ly, float lz, float hx, float hy, float hz) {
+    const float l0 = __builtin_fmaf(lx, c.ixlo, -c.cxlo), l1 = __builtin_fmaf(lx, c.ixhi, -c.cxhi);
+    const float h0 = __builtin_fmaf(hx, c.ixlo, -c.cxlo), h1 = __builtin_fmaf(hx, c.ixhi, -c.cxhi);
+    const float m0 = __builtin_fmaf(ly, c.iylo, -c.cylo), m1 = __builtin_fmaf(ly, c.iyhi, -c.cyhi);
+    const float k0 = __builtin_fmaf(hy, c.iylo, -c.cylo), k1 = __builtin_fmaf(hy, c.iyhi, -c.cyhi);
+    const float p0 = __builtin_fmaf(lz, c.izlo, -c.czlo), p1 = __builtin_fmaf(lz, c.izhi, -c.czhi);
+    const float q0 = __builtin_fmaf(hz, c.izlo, -c.czlo), q1 = __builtin_fmaf(hz, c.izhi, -c.czhi);
+    const float nx = fminf(fminf(l0, l1), fminf(h0, h1)), fx = fmaxf(fmaxf(l0, l1), fmaxf(h0, h1));
+    const float ny = fminf(fminf(m0, m1), fminf(k0, k1)), fy = fmaxf(fmaxf(m0, m1), fmaxf(k0, k1));
+    const float nz = fminf(fminf(p0, p1), fminf(q0, q1)), fz = fmaxf(fmaxf(p0, p1), fmaxf(q0, q1));
+    const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, c.smin));
+    const float tf = fminf(fminf(fx, fy), fminf(fz, c.smax));
+    return tn <= tf;
+}
+
+// Per-lane test of one box held in SGPRs (leaf boxes accepted by the cone: skip the
+// leaf when no lane's own ray meets it).
+template <bool SEG>
+__device__ __forceinline__ bool lane_box(const Ray32& r, float lx, float ly, float lz, float hx, float hy, float hz,
+                                         float tmax) {
+    const float ax = __builtin_fmaf(lx, r.ix, -r.oix), bx = __builtin_fmaf(hx, r.ix, -r.oix);
+    const float ay = __builtin_fmaf(ly, r.iy, -r.oiy), by = __builtin_fmaf(hy, r.iy, -r.oiy);
+    const float az = __builtin_fmaf(lz, r.iz, -r.oiz), bz = __builtin_fmaf(hz, r.iz, -r.oiz);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn <= (SEG ? fminf(tf, tmax) : tf);
+}
+
+// Walk one object's BVH for a shared-origin packet.  Each pass pops up to kWideBatch
+// nodes from the wave's LDS stack `stk`; lane L tests child L % 8 of node L / 8 against
+// the cone; accepted inner children are pushed (one ds_write per lane), accepted leaves
+// are tested per lane (box, then triangles).  Lanes whose own origin is beyond the cull
+// limit force every leaf (and the cone accepts everything for them via `all`).
+//   SEG: as bvh_sweep (retire lanes whose nearest candidate is below `resolve`, skip
+//   leaf boxes entered beyond tmax).
+template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
+__device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t* __restrict__ stk, const Cone& cone,
+                                         const Ray32& r, bool force, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
+                                         Visits& vis, uint32_t& overflow, float tmax = 0.0f, double resolve = 0.0) {
+    if (cone.none) return;
+    const uint32_t lane = threadIdx.x & 63;
+    bool live = lane_on;
+    uint32_t sp = 1;
+    if (lane == 0) stk[0] = 0;  // root
+    while (sp > 0) {
+        uint32_t k = ((int32_t)sp <= m.wide_thresh) ? min(sp, (uint32_t)kWideBatch) : 1u;
+        const uint32_t slot = lane >> 3, c = lane & 7;
+        const bool on = slot < k;
+        uint32_t node = 0;
+        if (on) node = stk[sp - 1 - slot];
+        sp -= k;
+        vis.nodes += k;
+        float lx = 0, ly = 0, lz = 0, hx = 0, hy = 0, hz = 0;
+        uint32_t ref = kBvhEmpty;
+        if (on) {
+            const float* nb = (const float*)(m.nodes + node);
+            ref = ((const uint32_t*)nb)[48 + c];
+            lx = nb[c];
+            ly = nb[8 + c];
+            lz = nb[16 + c];
+            hx = nb[24 + c];
+            hy = nb[32 + c];
+            hz = nb[40 + c];
+        }
+        const bool acc = ref != kBvhEmpty && (cone.all || cone_box(cone, lx, ly, lz, hx, hy, hz));
+        const bool is_leaf = (ref & kBvhLeafBit) != 0;
+        const uint64_t inner = __ballot(acc && !is_leaf);
+        uint64_t leaves = __ballot(acc && is_leaf);
+        const uint32_t npush = __popcll(inner);
+        if (sp + npush > (uint32_t)kBvhStack) {  // cannot happen (wide_thresh bound); counted
+            ++overflow;
+            break;
+        }
+        if (acc && !is_leaf) stk[sp + __popcll(inner & ((1ull << lane) - 1ull))] = ref;
+        sp += npush;
+        while (leaves) {
+            const uint32_t bit = __ffsll((unsigned long long)leaves) - 1;
+            leaves &= leaves - 1;
+            const uint32_t lref = __builtin_amdgcn_readlane(ref, bit);
+#if MIRT_LEAF_LANE_TEST
+            const float blx = u_lane(lx, bit), bly = u_lane(ly, bit), blz = u_lane(lz, bit);
+            const float bhx = u_lane(hx, bit), bhy = u_lane(hy, bit), bhz = u_lane(hz, bit);
+            if (__ballot(live && (force || lane_box<SEG>(r, blx, bly, blz, bhx, bhy, bhz, tmax))) == 0) continue;
+#endif
+            const uint32_t first = lref & kBvhFirstMask, cnt = (lref & ~kBvhLeafBit) >> kBvhCountShift;
+            ++vis.leaves;
+            test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
+            if (SEG) live = live && !(b.has && b.d < resolve);
+        }
+        if (SEG && __ballot(live) == 0) break;
+    }
+}
+
 struct Nearest {
     bool ok;
     uint32_t obj, face, mat;
@@ -371,9 +559,10 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 // first object in order wins ties (strict <).
 //   RESIDENT: object 0's mesh sits in LDS (`lds`), relative (p1or) when REL.
 //   BRUTE:    sweep every triangle instead of walking the BVH.
-template <bool REL, bool PREFILTER, bool BRUTE>
+//   COMMON:   every lane's ray starts at o (primary rays): wide cone traversal.
+template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
 __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal, Visits& vis) {
+                                 bool lane_on, bool want_normal, Visits& vis, uint32_t* __restrict__ stk = nullptr) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -387,14 +576,23 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
         Best b;
         best_init(b);
         const uint32_t ntri = ob.m.ntri;
-        if (resident) {
-            if (BRUTE)
+        if (BRUTE) {
+            if (resident)
                 test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+            else  // every triangle straight from HBM (waves run independently: no LDS staging)
+                test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+        } else if (COMMON) {
+            const Ray32 r = ray32(ro, d);
+            const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+            const bool force = !(far <= ob.m.cull_limit);
+            const Cone cone = make_cone(ro, r.ix, r.iy, r.iz, lane_on, force, 0.0f, __builtin_inff(), ob.m.cull_limit);
+            if (resident)
+                bvh_wide<REL, PREFILTER, false>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow);
             else
-                bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis);
-        } else if (BRUTE) {
-            // every triangle straight from HBM (waves run independently: no LDS staging)
-            test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+                bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                                  vis.overflow);
+        } else if (resident) {
+            bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis);
         } else {
             bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis);
         }
@@ -429,7 +627,8 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
 // runs unchanged.  M bounds every fp64 rounding involved with a wide margin.
 template <bool PREFILTER>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
-                                                  V3 hit, V3 o, V3 d, V3 lpos, bool lane_on, Visits& vis) {
+                                                  uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, bool lane_on,
+                                                  Visits& vis) {
     const DevObject& ob = fa.obj[0];
     const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
     const V3 ro = sub(o, pos);  // object.go:71
@@ -442,10 +641,28 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     const float tmax = (float)(lh + 1e-4 + M) * (1.0f + 0x1p-20f);
     Best b;
     best_init(b);
-    if (resident)
+    // Culling cone: the packet's rays walked backwards from the light, L + s * (-d), over
+    // s in [-(2e-4 + M), lh]: it covers o + t * d for t in [0, tmax] (o, L and d are
+    // collinear up to fp64 rounding, far inside the box inflation).
+    const Ray32 r = ray32(ro, d);
+    const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+    const bool force = !(far <= ob.m.cull_limit);
+    const float smin = -(float)(2e-4 + M) * (1.0f + 0x1p-20f);
+    const float smax = (float)lh * (1.0f + 0x1p-20f);
+    Cone cone;
+    if (MIRT_SHADOW_WIDE) cone = make_cone(sub(lpos, pos), -r.ix, -r.iy, -r.iz, lane_on, force, smin, smax, ob.m.cull_limit);
+    if (MIRT_SHADOW_WIDE) {
+        if (resident)
+            bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
+                                             tmax, resolve);
+        else
+            bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                             vis.overflow, tmax, resolve);
+    } else if (resident) {
         bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve);
-    else
+    } else {
         bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve);
+    }
     if (b.has && b.d < resolve) return false;
     uint32_t face, p;
     if (!best_result(b, face, p)) return true;
@@ -513,12 +730,15 @@ __device__ __forceinline__ uint32_t ticket_resolve(uint32_t t) { return __builti
 // Work item: one 8x8 pixel block (BlockDesc), lane -> (x, y) with y fastest so a wave's
 // writes are 8 runs of 8 contiguous pixels of the column-major packed tile.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    __shared__ cnt_t red[kWG / 64][3];
+MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
+    __shared__ cnt_t red[kWG / 64][4];
     const WaveClock clock;
     uint32_t taken = 0;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
+        for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
     if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
@@ -526,7 +746,7 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Wo
     }
     const uint32_t lane = threadIdx.x & 63;
     const ShardCursor sc;
-    WaveStats ws{0, 0, 0};
+    WaveStats ws{0, 0, 0, 0, 0};
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         cnt_t* qc = &wa.counters[cnt_queue(0, q)];
         uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
@@ -548,11 +768,13 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Wo
                        scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
             V3 d = norm(sub(p, cam));
 
-            Visits vis{0, 0, 0};
-            Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
+            Visits vis{0, 0, 0, 0};
+            Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, RESIDENT, cam, d, active, true, vis,
+                                                                          wstk[threadIdx.x >> 6]);
             ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
             ws.nodes += vis.nodes;
             ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
 
             const uint64_t oidx = bd.out + (uint64_t)lx * bd.th + ly;
             const bool is_hit = active && nh.ok;
@@ -573,27 +795,28 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Wo
                     }
                 }
             }
-            // wave-aggregated compaction into hit region q (blocks of shard q only)
+            // blocks with hits take 64 slots of hit region q (slot = lane)
             const uint64_t mask = __ballot(is_hit);
             if (mask) {
-                const uint32_t cnt = __popcll(mask);
+                ws.hits += __popcll(mask);
                 uint32_t base = 0;
-                if (lane == 0) base = (uint32_t)atomicAdd(&wa.counters[cnt_hits(q)], (cnt_t)cnt);
+                if (lane == 0) base = (uint32_t)atomicAdd(&wa.counters[cnt_hits(q)], (cnt_t)64);
                 base = __builtin_amdgcn_readfirstlane(base);
+                HitRec& hr = wa.hits[(size_t)q * wa.hit_cap + base + lane];
                 if (is_hit) {
-                    const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
-                    HitRec& hr = wa.hits[(size_t)q * wa.hit_cap + base + rank];
                     vstore(hr.h, nh.hit);
                     vstore(hr.n, nh.normal);
                     hr.out = oidx;
                     hr.obj = nh.obj;
                     hr.mat = nh.mat;
+                } else {
+                    hr.obj = kNoHit;
                 }
             }
             k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
-    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, ws);
+    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
     if (wa.timeline) clock.record(wa, 0, taken);
 }
 
@@ -602,11 +825,12 @@ __global__ __launch_bounds__(kWG, 4) void k_primary(const FrameArgs fa, const Wo
 // neighbouring pixels towards the same light: coherent rays).  Tickets of shard q
 // enumerate (light, chunk) of region q.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__global__ __launch_bounds__(kWG, 4) void k_shadow(const FrameArgs fa, const WorkArgs wa) {
+MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa) {
+    __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
     // segment query for one-object frames (BVH kernels only; brute force stays literal)
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
-    __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
-    __shared__ cnt_t red[kWG / 64][3];
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    __shared__ cnt_t red[kWG / 64][4];
     const WaveClock clock;
     uint32_t taken = 0;
     if (RESIDENT) {
@@ -615,7 +839,7 @@ __global__ __launch_bounds__(kWG, 4) void k_shadow(const FrameArgs fa, const Wor
     }
     const uint32_t lane = threadIdx.x & 63;
     const ShardCursor sc;
-    WaveStats ws{0, 0, 0};
+    WaveStats ws{0, 0, 0, 0, 0};
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
         const uint32_t nch = (nh + 63) / 64;
@@ -626,20 +850,22 @@ __global__ __launch_bounds__(kWG, 4) void k_shadow(const FrameArgs fa, const Wor
             const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            const uint32_t h = c * 64 + lane;
-            const bool active = h < nh;
+            const uint32_t h = c * 64 + lane;  // nh is a multiple of 64
+            const HitRec* hr = &wa.hits[(size_t)q * wa.hit_cap + h];
+            const bool active = hr->obj != kNoHit;
             V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
             const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
             if (active) {
-                hit = vload(wa.hits[(size_t)q * wa.hit_cap + h].h);
+                hit = vload(hr->h);
                 V3 ldir = norm(sub(lpos, hit));     // tracer.go:61
                 o = add(hit, scale(ldir, 0.0001));  // tracer.go:64
                 d = ldir;
             }
-            Visits vis{0, 0, 0};
+            Visits vis{0, 0, 0, 0};
             bool is_lit;
             if (segment) {
-                is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, hit, o, d, lpos, active, vis);
+                is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, wstk[threadIdx.x >> 6], hit, o, d, lpos, active,
+                                                      vis);
             } else {
                 Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, false, vis);
                 // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
@@ -648,18 +874,19 @@ __global__ __launch_bounds__(kWG, 4) void k_shadow(const FrameArgs fa, const Wor
             ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
             ws.nodes += vis.nodes;
             ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
             if (active) wa.lit[((size_t)q * fa.n_lights + l) * wa.hit_cap + h] = is_lit ? 1 : 0;
             k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
-    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, ws);
+    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
 }
 
 // ---------------------------------------------------------------- arbitrary rays
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__global__ __launch_bounds__(kWG, 4) void k_rays(const FrameArgs fa, RayIO io) {
-    __shared__ __attribute__((aligned(16))) double lds[kLdsTris * kTriD];
+MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
@@ -673,7 +900,7 @@ __global__ __launch_bounds__(kWG, 4) void k_rays(const FrameArgs fa, RayIO io) {
             o = vload(io.orig + 3 * item);
             d = vload(io.dir + 3 * item);
         }
-        Visits vis{0, 0, 0};
+        Visits vis{0, 0, 0, 0};
         Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, true, vis);
         if (active) {
             io.ok[item] = r.ok ? 1 : 0;
@@ -688,6 +915,19 @@ __global__ __launch_bounds__(kWG, 4) void k_rays(const FrameArgs fa, RayIO io) {
 // ---------------------------------------------------------------- shade
 // tracer.go:53-76 phong for every hit; waves walk (region, 64-hit chunk) round-robin.
 __global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    // frame statistics: the primary and shadow kernels are complete
+    if (blockIdx.x == 0 && threadIdx.x < kStatN) {
+        const int k = threadIdx.x;
+        cnt_t sum = 0;
+        if (k == kStatShadowRays) {
+            for (int sh = 0; sh < kStatShards; ++sh) sum += wa.counters[cnt_stat(kStatHits, sh)];
+            sum *= fa.n_lights;
+        } else {
+            for (int sh = 0; sh < kStatShards; ++sh) sum += wa.counters[cnt_stat(k, sh)];
+        }
+        wa.summary[k] = sum;
+        if (wa.prof_acc && sum) atomicAdd(&wa.prof_acc[k], sum);
+    }
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (256 / 64) + (threadIdx.x >> 6), nw = gridDim.x * (256 / 64);
     const uint32_t chunks_per_region = wa.hit_cap / 64;
@@ -698,8 +938,8 @@ __global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const WorkArg
         const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
         if (c * 64 >= nh) continue;
         const uint32_t h = c * 64 + lane;
-        if (h >= nh) continue;
         const HitRec hr = wa.hits[(size_t)q * wa.hit_cap + h];
+        if (hr.obj == kNoHit) continue;
         const DevMesh& m = fa.obj[hr.obj].m;
         const double* mt = m.mats + (size_t)hr.mat * 10;
         RGB ka{mt[0], mt[1], mt[2]}, kd{mt[3], mt[4], mt[5]}, ks{mt[6], mt[7], mt[8]};
@@ -797,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
     } while (0)
 
 static bool is_resident(const FrameArgs& fa) {
-    return fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
+    return MIRT_LDS_MESH && fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
 }
 
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,

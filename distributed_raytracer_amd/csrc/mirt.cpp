@@ -73,7 +73,10 @@ struct Slot {
     size_t blocks_cap = 0, h_blocks_cap = 0;
     std::vector<mirt_tile> blocks_key;
     uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0;
-    cnt_t* h_counters = nullptr;  // pinned
+    cnt_t* summary = nullptr;     // kStatN totals of the last frame (device)
+    cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
+    bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
+    uint32_t parity = 0;          // counter set of the next frame (two sets of kCntN)
     // device-side outputs for the host-buffer API
     void* out_buf = nullptr;
     size_t out_cap = 0;
@@ -81,8 +84,7 @@ struct Slot {
 
 struct ProfRec {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    cnt_t* h_cnt = nullptr;  // pinned kCntN counters, written by an async D2H copy
-    uint64_t pixels = 0, tris = 0, nl = 0;
+    uint64_t pixels = 0;
 };
 
 }  // namespace
@@ -98,6 +100,7 @@ struct mirt_ctx {
     bool profiling = false;
     std::vector<ProfRec> prof_pending;
     std::vector<ProfRec> prof_free;
+    cnt_t* prof_acc = nullptr;     // kStatN device totals accumulated while profiling
     uint64_t* timeline = nullptr;  // MIRT_OPT_TIMELINE buffer (2 kernels x timeline_cap waves)
     uint32_t timeline_cap = 0;
 };
@@ -154,8 +157,11 @@ int slot_acquire(mirt_ctx* c, Slot*& out) {
     if (!s->stream) {
         HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
-        HIP_TRY(hipMalloc((void**)&s->counters, kCntN * sizeof(cnt_t)));
-        HIP_TRY(hipHostMalloc((void**)&s->h_counters, kCntN * sizeof(cnt_t)));
+        HIP_TRY(hipMalloc((void**)&s->counters, 2 * kCntN * sizeof(cnt_t)));
+        HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
+        HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
+        HIP_TRY(hipMemsetAsync(s->counters, 0, 2 * kCntN * sizeof(cnt_t), s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
     }
     // previous asynchronous use of this slot's staging/workspace must be finished
     if (s->pending) {
@@ -240,7 +246,9 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         o.m.nodes = m.nodes;
         o.m.nnodes = m.nnodes;
         o.m.depth = m.depth;
-        o.m.cull_limit = 256.0 * m.scale;
+        // culling needs bounded coordinates (fp32 slab arithmetic); beyond 2^40 never cull
+        o.m.cull_limit = (m.scale <= 0x1p40) ? 256.0 * m.scale : -1.0;
+        o.m.wide_thresh = (int32_t)kBvhStack - 64 - 7 * (int32_t)m.depth;
         o.m.mats = m.mats;
         o.m.ntri = m.ntri;
         o.m.has_normals = m.has_normals ? 1u : 0u;
@@ -262,7 +270,6 @@ int prof_get(mirt_ctx* c, ProfRec& r) {
         return MIRT_OK;
     }
     for (int k = 0; k < 4; ++k) HIP_TRY(hipEventCreate(&r.ev[k]));
-    HIP_TRY(hipHostMalloc((void**)&r.h_cnt, kCntN * sizeof(cnt_t)));
     return MIRT_OK;
 }
 
@@ -341,7 +348,9 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if ((r = dev_grow(sl->lit, sl->lit_cap, hit_slots * std::max<uint32_t>(nl, 1))) != MIRT_OK) return r;
     wa.hits = sl->hits;
     wa.lit = sl->lit;
-    wa.counters = sl->counters;
+    wa.counters = sl->counters + (size_t)sl->parity * kCntN;
+    wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
+    wa.summary = sl->summary;
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE) ? 0u : 1u;
     if (c->flags & MIRT_OPT_TIMELINE) {
         std::lock_guard<std::mutex> g(c->mu);
@@ -356,10 +365,15 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     }
 
     ProfRec pr;
-    const bool prof = c->profiling;
+    const bool prof = c->profiling && c->prof_acc;
     if (prof && (r = prof_get(c, pr)) != MIRT_OK) return r;
+    wa.prof_acc = prof ? c->prof_acc : nullptr;
 
-    HIP_TRY(hipMemsetAsync(sl->counters, 0, kCntN * sizeof(cnt_t), s));
+    // this frame's counter set was zeroed by the previous frame's k_primary; only a frame
+    // that stopped half-way leaves the sets dirty
+    if (sl->dirty) HIP_TRY(hipMemsetAsync(sl->counters, 0, 2 * kCntN * sizeof(cnt_t), s));
+    sl->dirty = true;
+    sl->parity ^= 1u;
     // persistent: two 512-thread workgroups per CU; waves take work from the queues
     const int pgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
@@ -375,12 +389,10 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     HIP_TRY(launch_shade(fa, wa, out, hgrid, s));
+    sl->dirty = false;
     if (prof) {
         HIP_TRY(hipEventRecord(pr.ev[3], s));
-        HIP_TRY(hipMemcpyAsync(pr.h_cnt, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
         pr.pixels = pixels;
-        pr.tris = tris;
-        pr.nl = nl;
         std::lock_guard<std::mutex> g(c->mu);
         c->prof_pending.push_back(pr);
     }
@@ -391,25 +403,15 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     return MIRT_OK;
 }
 
-uint64_t stat_sum(const cnt_t* c, int stat) {
-    uint64_t s = 0;
-    for (int k = 0; k < kStatShards; ++k) s += c[cnt_stat(stat, k)];
-    return s;
-}
-uint64_t hits_sum(const cnt_t* c) {
-    uint64_t s = 0;
-    for (int k = 0; k < kQShards; ++k) s += c[cnt_hits(k)];
-    return s;
-}
 
 int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t nl, mirt_stats* st) {
-    HIP_TRY(hipMemcpyAsync(sl->h_counters, sl->counters, kCntN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(sl->h_summary, sl->summary, kStatN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memset(st, 0, sizeof(*st));
     st->primary_rays = pixels;
-    st->hits = hits_sum(sl->h_counters);
-    st->shadow_rays = st->hits * nl;
-    st->tri_tests = stat_sum(sl->h_counters, kStatPrimTests) + stat_sum(sl->h_counters, kStatShadowTests);
+    st->hits = sl->h_summary[kStatHits];
+    st->shadow_rays = sl->h_summary[kStatShadowRays];
+    st->tri_tests = sl->h_summary[kStatPrimTests] + sl->h_summary[kStatShadowTests];
     return MIRT_OK;
 }
 
@@ -452,7 +454,8 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->d_blocks) (void)hipFree(s->d_blocks);
         if (s->h_blocks) (void)hipHostFree(s->h_blocks);
         if (s->h_tiles) (void)hipHostFree(s->h_tiles);
-        if (s->h_counters) (void)hipHostFree(s->h_counters);
+        if (s->summary) (void)hipFree(s->summary);
+        if (s->h_summary) (void)hipHostFree(s->h_summary);
         if (s->out_buf) (void)hipFree(s->out_buf);
         if (s->done) (void)hipEventDestroy(s->done);
         if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -461,10 +464,10 @@ void mirt_destroy(mirt_ctx* c) {
         for (auto& r : *v) {
             for (auto e : r.ev)
                 if (e) (void)hipEventDestroy(e);
-            if (r.h_cnt) (void)hipHostFree(r.h_cnt);
         }
     for (auto& m : c->meshes) mesh_free(m);
     if (c->timeline) (void)hipFree(c->timeline);
+    if (c->prof_acc) (void)hipFree(c->prof_acc);
     delete c;
 }
 
@@ -775,6 +778,11 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* 
 
 int mirt_profile_enable(mirt_ctx* c, int enable) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    HIP_TRY(hipSetDevice(c->device));
+    if (enable && !c->prof_acc) {
+        HIP_TRY(hipMalloc((void**)&c->prof_acc, kStatN * sizeof(cnt_t)));
+        HIP_TRY(hipMemset(c->prof_acc, 0, kStatN * sizeof(cnt_t)));
+    }
     c->profiling = enable != 0;
     return MIRT_OK;
 }
@@ -800,16 +808,21 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->shadow_ms_sum += b;
         out->shade_ms_sum += d;
         out->frame_ms_sum += t;
-        const uint64_t hits = hits_sum(r.h_cnt);
         out->primary_rays += r.pixels;
-        out->hits += hits;
-        out->shadow_rays += hits * r.nl;
-        out->primary_tri_tests += stat_sum(r.h_cnt, kStatPrimTests);
-        out->shadow_tri_tests += stat_sum(r.h_cnt, kStatShadowTests);
-        out->primary_node_visits += stat_sum(r.h_cnt, kStatPrimNodes);
-        out->primary_leaf_visits += stat_sum(r.h_cnt, kStatPrimLeaves);
-        out->shadow_node_visits += stat_sum(r.h_cnt, kStatShadowNodes);
-        out->shadow_leaf_visits += stat_sum(r.h_cnt, kStatShadowLeaves);
+    }
+    if (c->prof_acc) {
+        cnt_t acc[kStatN];
+        HIP_TRY(hipMemcpy(acc, c->prof_acc, sizeof(acc), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(c->prof_acc, 0, sizeof(acc)));
+        out->hits = acc[kStatHits];
+        out->shadow_rays = acc[kStatShadowRays];
+        out->primary_tri_tests = acc[kStatPrimTests];
+        out->shadow_tri_tests = acc[kStatShadowTests];
+        out->primary_node_visits = acc[kStatPrimNodes];
+        out->primary_leaf_visits = acc[kStatPrimLeaves];
+        out->shadow_node_visits = acc[kStatShadowNodes];
+        out->shadow_leaf_visits = acc[kStatShadowLeaves];
+        out->stack_overflows = acc[kStatOverflow];
     }
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);

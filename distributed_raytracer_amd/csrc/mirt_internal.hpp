@@ -37,8 +37,12 @@ constexpr uint32_t kBvhLeafBit = 0x80000000u;
 constexpr int kBvhCountShift = 24;
 constexpr uint32_t kBvhFirstMask = 0x00ffffffu;
 constexpr int kBvhLeaf = 4;           // max triangles per leaf
-constexpr int kBvhStack = 128;        // per-wave traversal stack entries (two VGPRs, one per lane)
+constexpr int kBvhStack = 128;        // per-wave traversal stack entries (two VGPRs / LDS)
 constexpr int kBvhMaxDepth = (kBvhStack - 1) / 7;
+// Wide traversal (shared-origin packets): up to 8 nodes per pass, one lane per child box.
+// Batching is allowed only while the stack holds <= DevMesh::wide_thresh entries
+// (= kBvhStack - 64 - 7 * depth), which bounds the stack by kBvhStack.
+constexpr int kWideBatch = 8;
 
 // One uploaded mesh, device pointers (shared/state/mesh.go:100-106).  Every per-face
 // array is stored in BVH leaf order; fidx maps a position back to the face index of
@@ -54,6 +58,8 @@ struct DevMesh {
     uint32_t has_normals;
     uint32_t nnodes;
     uint32_t depth;
+    int32_t wide_thresh;     // wide traversal batches nodes only while sp <= this (< 0: never)
+    uint32_t pad;
     double cull_limit;       // rays whose object-space origin has a coordinate beyond this
                              // are never culled (tolerance scales with |origin|)
 };
@@ -104,11 +110,12 @@ struct OutPlanes {
 };
 
 // A primary hit handed from the primary kernel to the shadow and shade kernels.
+constexpr uint32_t kNoHit = 0xffffffffu;
 struct HitRec {
     double h[3];     // world-space intersection
     double n[3];     // interpolated (or flat) normal
     uint64_t out;    // packed output pixel index
-    uint32_t obj;    // object index
+    uint32_t obj;    // object index (kNoHit: empty slot)
     uint32_t mat;    // material index inside that object's mesh
 };
 
@@ -118,14 +125,21 @@ struct HitRec {
 //   queue(q, s): work-queue tickets of kernel q (0 primary, 1 shadow) for shard s.
 //     Primary block b belongs to shard b % kQShards; a wave serves the shard
 //     (global wave id % kQShards) and takes one block per ticket.
-//   hits(s):     hit compaction of shard s.  Hits of the blocks of shard s are packed into
-//     region s (capacity hit_cap = ceil(blocks / kQShards) * 64 records), so the shadow
-//     and shade kernels walk regions without any cross-shard prefix sum.
+//   hits(s):     hit slots of shard s.  A block with at least one hit takes 64 slots of
+//     region s (capacity hit_cap = ceil(blocks / kQShards) * 64 records), slot = lane =
+//     pixel of the 8x8 block, so a 64-slot shadow chunk is one block: a 2D-coherent packet.
+//     Slots of pixels that missed carry obj = kNoHit.  The shadow and shade kernels walk
+//     regions without any cross-shard prefix sum.
 //   stat(k, s):  statistics (ray-triangle tests, BVH node/leaf visits), reduced per
 //     workgroup in LDS and added once per workgroup into shard blockIdx % kStatShards.
+// Each slot holds two such sets and alternates between them frame by frame: workgroup 0
+// of k_primary zeroes the set the NEXT frame will use (its last user, the frame before,
+// has finished: frames on one slot never overlap), so no frame needs a memset; workgroup
+// 0 of k_shade folds this frame's statistics into WorkArgs::summary (and the profiling
+// accumulator) once the producing kernels are done.
 constexpr int kQShards = 64, kStatShards = 8, kLine = 16;
 enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kStatShadowNodes,
-       kStatShadowLeaves, kStatN };
+       kStatShadowLeaves, kStatHits, kStatOverflow, kStatShadowRays, kStatN };
 __host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_hits(int s) { return (2 * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_stat(int k, int s) { return (3 * kQShards + k * kStatShards + s) * kLine; }
@@ -140,9 +154,12 @@ struct WorkArgs {
     HitRec* hits;          // kQShards regions of hit_cap records
     uint8_t* lit;          // kQShards x n_lights regions of hit_cap flags
     cnt_t* counters;
+    cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
     uint32_t timeline_cap; // records the timeline buffer holds per kernel
     uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
+    cnt_t* summary;        // kStatN totals of this frame (written by k_shade's last workgroup)
+    cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
 };
 constexpr int kTimelineRec = 8;
 

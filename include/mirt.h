@@ -135,6 +135,8 @@ typedef struct {
     uint64_t primary_rays, shadow_rays, hits;
     /* wave-level BVH traversal work (diagnostic): node boxes tested, leaves entered */
     uint64_t primary_node_visits, primary_leaf_visits, shadow_node_visits, shadow_leaf_visits;
+    /* traversal stack overflows (provably impossible; a non-zero value is a library bug) */
+    uint64_t stack_overflows;
 } mirt_profile;
 
 int mirt_abi_version(void);

@@ -380,3 +380,4 @@ def test_profile_counters(ctx, env):
     assert b["primary_tri_tests"] == 76800 * 968 and b["shadow_tri_tests"] == 3 * 5820 * 968
     assert 0 < p["primary_tri_tests"] < 2 * 76800 * 968 / 5
     assert p["primary_ms_sum"] > 0 and p["frame_ms_sum"] >= p["primary_ms_sum"]
+    assert p["stack_overflows"] == 0 and b["stack_overflows"] == 0
