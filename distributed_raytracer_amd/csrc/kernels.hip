@@ -672,6 +672,57 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     return lh < len(sub(world, hit));
 }
 
+// ---------------------------------------------------------------- Phong
+// tracer.go:53-76 for one hit; bit l of lit = light l reaches the point.
+__device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restrict__ mt, V3 hit, V3 n, uint32_t lit) {
+    RGB ka{mt[0], mt[1], mt[2]}, kd{mt[3], mt[4], mt[5]}, ks{mt[6], mt[7], mt[8]};
+    const double ns = mt[9];
+    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    RGB col = ka;  // tracer.go:56
+    for (uint32_t l = 0; l < fa.n_lights; ++l) {
+        if (!((lit >> l) & 1u)) continue;
+        const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+        const RGB lcol{fa.lcol[l][0], fa.lcol[l][1], fa.lcol[l][2]};
+        const V3 ldir = norm(sub(lpos, hit));                         // tracer.go:61
+        const V3 refl = sub(scale(n, 2 * dot(ldir, n)), ldir);        // tracer.go:65
+        const V3 camdir = norm(sub(cam, hit));                        // tracer.go:66
+        col = c_add(col, c_mul(c_scale(kd, go_max(dot(ldir, n), 0.0)), lcol));                // :69
+        col = c_add(col, c_mul(c_scale(ks, go_pow(go_max(dot(refl, camdir), 0.0), ns)), lcol));  // :72
+    }
+    return col;
+}
+
+// ---------------------------------------------------------------- frame statistics
+// Called by every workgroup of the frame's last kernel after its statistics are flushed:
+// the last workgroup (two-level done count, <= 64 same-address atomics per level) folds
+// the statistic shards into WorkArgs::summary and the profiling accumulator.  Shards are
+// read with atomics (device-coherent across the XCDs' L2s).
+__device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& wa) {
+    __shared__ bool last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t sh = blockIdx.x % kStatShards;
+        const uint32_t in_shard = (gridDim.x - sh + kStatShards - 1) / kStatShards;
+        bool l = atomicAdd(&wa.counters[cnt_done(sh)], (cnt_t)1) == (cnt_t)in_shard - 1;
+        if (l) {
+            const uint32_t shards = min((uint32_t)kStatShards, gridDim.x);
+            l = atomicAdd(&wa.counters[cnt_done(kStatShards)], (cnt_t)1) == (cnt_t)shards - 1;
+        }
+        last = l;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x >= kStatN) return;
+    __threadfence();
+    const int st = threadIdx.x;
+    cnt_t sum = 0;
+    for (int sh = 0; sh < kStatShards; ++sh)
+        sum += atomicAdd(&wa.counters[cnt_stat(st == kStatShadowRays ? kStatHits : st, sh)], (cnt_t)0);
+    if (st == kStatShadowRays) sum *= fa.n_lights;
+    wa.summary[st] = sum;
+    if (wa.prof_acc && sum) atomicAdd(&wa.prof_acc[st], sum);
+}
+
 // ---------------------------------------------------------------- work distribution
 // A wave serves queue shard q = (global wave id) % kQShards (several shards in turn when
 // fewer than kQShards waves run).  dynamic: each ticket of the shard's counter is one work
@@ -802,7 +853,10 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
                 uint32_t base = 0;
                 if (lane == 0) base = (uint32_t)atomicAdd(&wa.counters[cnt_hits(q)], (cnt_t)64);
                 base = __builtin_amdgcn_readfirstlane(base);
-                HitRec& hr = wa.hits[(size_t)q * wa.hit_cap + base + lane];
+                const size_t slot = (size_t)q * wa.hit_cap + base + lane;
+                HitRec& hr = wa.hits[slot];
+                wa.litw[slot] = 0;
+                if (lane == 0) wa.blkdone[slot / 64] = 0;
                 if (is_hit) {
                     vstore(hr.h, nh.hit);
                     vstore(hr.n, nh.normal);
@@ -825,7 +879,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
 // neighbouring pixels towards the same light: coherent rays).  Tickets of shard q
 // enumerate (light, chunk) of region q.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa) {
+MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
     // segment query for one-object frames (BVH kernels only; brute force stays literal)
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
@@ -837,13 +891,16 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
+    // frame statistics of the primary kernel (complete); the shadow kernel's own are folded
+    // by its last workgroup below
     const uint32_t lane = threadIdx.x & 63;
     const ShardCursor sc;
     WaveStats ws{0, 0, 0, 0, 0};
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
         const uint32_t nch = (nh + 63) / 64;
-        const uint32_t items = nch * fa.n_lights;
+        const uint32_t nl = max(fa.n_lights, 1u);  // no lights: one pass that only shades
+        const uint32_t items = nch * nl;
         cnt_t* qc = &wa.counters[cnt_queue(1, q)];
         uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
         while (k < items) {
@@ -862,8 +919,10 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa) {
                 d = ldir;
             }
             Visits vis{0, 0, 0, 0};
-            bool is_lit;
-            if (segment) {
+            bool is_lit = false;
+            if (fa.n_lights == 0) {
+                // no lights: nothing to trace, the pass only shades (ambient)
+            } else if (segment) {
                 is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, wstk[threadIdx.x >> 6], hit, o, d, lpos, active,
                                                       vis);
             } else {
@@ -875,12 +934,153 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa) {
             ws.nodes += vis.nodes;
             ws.leaves += vis.leaves;
             ws.overflow += vis.overflow;
-            if (active) wa.lit[((size_t)q * fa.n_lights + l) * wa.hit_cap + h] = is_lit ? 1 : 0;
+            // publish this light's bits, then count the light done for the block; the wave
+            // finishing the block's last light shades it (tracer.go:53-76).  Device-scope
+            // atomics are coherent across XCDs; the wait orders the two atomics.
+            const size_t slot = (size_t)q * wa.hit_cap + h;
+            if (active && is_lit) {
+                // returning atomic: its completion (vmcnt) means it has been performed
+                const uint32_t old = __hip_atomic_fetch_or(&wa.litw[slot], 1u << l, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("" ::"v"(old));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t done = 0;
+            if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
+            done = __builtin_amdgcn_readfirstlane(done);
+            if (done == nl - 1 && active) {
+                const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
+                const HitRec rec = *hr;
+                const RGB col = phong(fa, fa.obj[rec.obj].m.mats + (size_t)rec.mat * 10, hit, vload(rec.n), lit);
+                if (out.rgb) {
+                    out.rgb[3 * rec.out] = col.r;
+                    out.rgb[3 * rec.out + 1] = col.g;
+                    out.rgb[3 * rec.out + 2] = col.b;
+                }
+                if (out.rgb8) {
+                    out.rgb8[3 * rec.out] = c_u8(col.r);
+                    out.rgb8[3 * rec.out + 1] = c_u8(col.g);
+                    out.rgb8[3 * rec.out + 2] = c_u8(col.b);
+                }
+            }
             k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
+    frame_fold(fa, wa);
+}
+
+// ---------------------------------------------------------------- fused frame
+// One work item = one 8x8 pixel block, traced start to finish by one wave: primary rays,
+// then for each light one shadow packet over the block's hit lanes (converging on the
+// light: coherent), then Phong, all in registers.  No hit slots, no lit flags, one
+// launch per frame and one tail instead of three.  The mesh sits in LDS in absolute
+// coordinates (both ray kinds read it).
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+MIRT_TRACE_KERNEL void k_frame(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    __shared__ cnt_t red[kWG / 64][4];
+    const WaveClock clock;
+    uint32_t taken = 0;
+    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
+        for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
+    if (RESIDENT) {
+        stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const ShardCursor sc;
+    WaveStats ws{0, 0, 0, 0, 0};
+    WaveStats wsh{0, 0, 0, 0, 0};
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+        cnt_t* qc = &wa.counters[cnt_queue(0, q)];
+        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        for (;;) {
+            const uint32_t blk = k * kQShards + q;
+            if (blk >= wa.nblocks) break;
+            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;  // in flight while tracing
+            ++taken;
+            const BlockDesc bd = wa.blocks[blk];
+            const uint32_t lx = lane >> 3, ly = lane & 7;
+            const bool active = lx < bd.vw && ly < bd.vh;
+            const int i = (int)(bd.px + (active ? lx : 0)), j = (int)(bd.py + (active ? ly : 0));
+
+            // tracer.go:15-22 pixelToPoint, then tracer.go:86 dir = (p - Cam.Pos).Norm()
+            const double si = fa.phw * ((double)(fa.halfW - i) - 0.5) / (double)fa.halfW;
+            const double sj = fa.phh * ((double)(fa.halfH - j) - 0.5) / (double)fa.halfH;
+            V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}),
+                           scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
+                       scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
+            V3 d = norm(sub(p, cam));
+
+            Visits vis{0, 0, 0, 0};
+            Nearest nh = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
+
+            const uint64_t oidx = bd.out + (uint64_t)lx * bd.th + ly;
+            const bool is_hit = active && nh.ok;
+            if (active) {
+                if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
+                if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
+                if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
+            }
+            const uint64_t mask = __ballot(is_hit);
+            RGB col{0, 0, 0};
+            if (mask) {
+                ws.hits += __popcll(mask);
+                uint32_t lit = 0;
+                for (uint32_t l = 0; l < fa.n_lights; ++l) {
+                    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+                    V3 o{0, 0, 0}, sd{1, 0, 0};
+                    if (is_hit) {
+                        const V3 ldir = norm(sub(lpos, nh.hit));  // tracer.go:61
+                        o = add(nh.hit, scale(ldir, 0.0001));     // tracer.go:64
+                        sd = ldir;
+                    }
+                    Visits sv{0, 0, 0, 0};
+                    bool is_lit;
+                    if (segment) {
+                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, nh.hit, o, sd, lpos, is_hit, sv);
+                    } else {
+                        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, sd, is_hit, false, sv);
+                        // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
+                        is_lit = !r.ok || len(sub(lpos, nh.hit)) < len(sub(r.hit, nh.hit));
+                    }
+                    wsh.tests += (cnt_t)sv.tests * __popcll(mask);
+                    wsh.nodes += sv.nodes;
+                    wsh.leaves += sv.leaves;
+                    wsh.overflow += sv.overflow;
+                    lit |= (uint32_t)is_lit << l;
+                }
+                if (is_hit) col = phong(fa, fa.obj[nh.obj].m.mats + (size_t)nh.mat * 10, nh.hit, nh.normal, lit);
+            }
+            if (active) {
+                if (out.rgb) {
+                    out.rgb[3 * oidx] = col.r;
+                    out.rgb[3 * oidx + 1] = col.g;
+                    out.rgb[3 * oidx + 2] = col.b;
+                }
+                if (out.rgb8) {
+                    out.rgb8[3 * oidx] = c_u8(col.r);
+                    out.rgb8[3 * oidx + 1] = c_u8(col.g);
+                    out.rgb8[3 * oidx + 2] = c_u8(col.b);
+                }
+            }
+            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+        }
+    }
+    wsh.hits = 0;
+    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
+    __syncthreads();
+    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
+    if (wa.timeline) clock.record(wa, 0, taken);
+    frame_fold(fa, wa);
 }
 
 // ---------------------------------------------------------------- arbitrary rays
@@ -908,63 +1108,6 @@ MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
             vstore(io.normal + 3 * item, r.ok ? r.normal : V3{0, 0, 0});
             io.face[item] = r.ok ? (int32_t)r.face : -1;
             io.object[item] = r.ok ? (int32_t)r.obj : -1;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- shade
-// tracer.go:53-76 phong for every hit; waves walk (region, 64-hit chunk) round-robin.
-__global__ __launch_bounds__(256) void k_shade(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    // frame statistics: the primary and shadow kernels are complete
-    if (blockIdx.x == 0 && threadIdx.x < kStatN) {
-        const int k = threadIdx.x;
-        cnt_t sum = 0;
-        if (k == kStatShadowRays) {
-            for (int sh = 0; sh < kStatShards; ++sh) sum += wa.counters[cnt_stat(kStatHits, sh)];
-            sum *= fa.n_lights;
-        } else {
-            for (int sh = 0; sh < kStatShards; ++sh) sum += wa.counters[cnt_stat(k, sh)];
-        }
-        wa.summary[k] = sum;
-        if (wa.prof_acc && sum) atomicAdd(&wa.prof_acc[k], sum);
-    }
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t gw = blockIdx.x * (256 / 64) + (threadIdx.x >> 6), nw = gridDim.x * (256 / 64);
-    const uint32_t chunks_per_region = wa.hit_cap / 64;
-    const uint64_t nchunks = (uint64_t)kQShards * chunks_per_region;
-    V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    for (uint64_t ck = gw; ck < nchunks; ck += nw) {
-        const uint32_t q = (uint32_t)(ck % kQShards), c = (uint32_t)(ck / kQShards);
-        const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
-        if (c * 64 >= nh) continue;
-        const uint32_t h = c * 64 + lane;
-        const HitRec hr = wa.hits[(size_t)q * wa.hit_cap + h];
-        if (hr.obj == kNoHit) continue;
-        const DevMesh& m = fa.obj[hr.obj].m;
-        const double* mt = m.mats + (size_t)hr.mat * 10;
-        RGB ka{mt[0], mt[1], mt[2]}, kd{mt[3], mt[4], mt[5]}, ks{mt[6], mt[7], mt[8]};
-        const double ns = mt[9];
-        const V3 hit = vload(hr.h), n = vload(hr.n);
-        RGB col = ka;  // tracer.go:56
-        for (uint32_t l = 0; l < fa.n_lights; ++l) {
-            if (!wa.lit[((size_t)q * fa.n_lights + l) * wa.hit_cap + h]) continue;
-            const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
-            const RGB lcol{fa.lcol[l][0], fa.lcol[l][1], fa.lcol[l][2]};
-            const V3 ldir = norm(sub(lpos, hit));                         // tracer.go:61
-            const V3 refl = sub(scale(n, 2 * dot(ldir, n)), ldir);        // tracer.go:65
-            const V3 camdir = norm(sub(cam, hit));                        // tracer.go:66
-            col = c_add(col, c_mul(c_scale(kd, go_max(dot(ldir, n), 0.0)), lcol));                // :69
-            col = c_add(col, c_mul(c_scale(ks, go_pow(go_max(dot(refl, camdir), 0.0), ns)), lcol));  // :72
-        }
-        if (out.rgb) {
-            out.rgb[3 * hr.out] = col.r;
-            out.rgb[3 * hr.out + 1] = col.g;
-            out.rgb[3 * hr.out + 2] = col.b;
-        }
-        if (out.rgb8) {
-            out.rgb8[3 * hr.out] = c_u8(col.r);
-            out.rgb8[3 * hr.out + 1] = c_u8(col.g);
-            out.rgb8[3 * hr.out + 2] = c_u8(col.b);
         }
     }
 }
@@ -1049,9 +1192,10 @@ hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
     return hipGetLastError();
 }
 
-hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, int grid, uint32_t opts, hipStream_t s) {
+hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                         hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_SHADOW(P, B, R) hipLaunchKernelGGL((k_shadow<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa)
+#define K_SHADOW(P, B, R) hipLaunchKernelGGL((k_shadow<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
     MIRT_DISPATCH(K_SHADOW);
 #undef K_SHADOW
     return hipGetLastError();
@@ -1065,8 +1209,12 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
     return hipGetLastError();
 }
 
-hipError_t launch_shade(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(256), 0, s, fa, wa, out);
+hipError_t launch_frame(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                        hipStream_t s) {
+    const bool resident = is_resident(fa);
+#define K_FRAME(P, B, R) hipLaunchKernelGGL((k_frame<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    MIRT_DISPATCH(K_FRAME);
+#undef K_FRAME
     return hipGetLastError();
 }
 

@@ -60,8 +60,10 @@ struct Slot {
     bool pending = false;
     HitRec* hits = nullptr;
     size_t hits_cap = 0;
-    uint8_t* lit = nullptr;
-    size_t lit_cap = 0;
+    uint32_t* litw = nullptr;
+    size_t litw_cap = 0;
+    uint32_t* blkdone = nullptr;
+    size_t blkdone_cap = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
@@ -345,9 +347,11 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
     const uint64_t hit_slots = (uint64_t)kQShards * wa.hit_cap;
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
-    if ((r = dev_grow(sl->lit, sl->lit_cap, hit_slots * std::max<uint32_t>(nl, 1))) != MIRT_OK) return r;
+    if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
+    if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
     wa.hits = sl->hits;
-    wa.lit = sl->lit;
+    wa.litw = sl->litw;
+    wa.blkdone = sl->blkdone;
     wa.counters = sl->counters + (size_t)sl->parity * kCntN;
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
@@ -379,16 +383,24 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
-    const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((pixels + 255) / 256, (uint64_t)8 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
-    if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
-    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-    if (nl) HIP_TRY(launch_shadow(fa, wa, sgrid, c->flags, s));
-    if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
-    if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-    HIP_TRY(launch_shade(fa, wa, out, hgrid, s));
+    if (c->flags & MIRT_OPT_FUSED_FRAME) {
+        // one fused launch per frame (k_frame); profile times land in the primary slot
+        HIP_TRY(launch_frame(fa, wa, out, pgrid, c->flags, s));
+        if (prof) {
+            HIP_TRY(hipEventRecord(pr.ev[1], s));
+            HIP_TRY(hipEventRecord(pr.ev[2], s));
+        }
+    } else {
+        HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
+        if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
+        if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+        // shadow rays + Phong (the wave finishing a block's last light shades it); also
+        // launched with no lights, to shade every hit with the ambient term
+        HIP_TRY(launch_shadow(fa, wa, out, sgrid, c->flags, s));
+        if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
+    }
     sl->dirty = false;
     if (prof) {
         HIP_TRY(hipEventRecord(pr.ev[3], s));
@@ -448,7 +460,8 @@ void mirt_destroy(mirt_ctx* c) {
         Slot* s = sp.get();
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->hits) (void)hipFree(s->hits);
-        if (s->lit) (void)hipFree(s->lit);
+        if (s->litw) (void)hipFree(s->litw);
+        if (s->blkdone) (void)hipFree(s->blkdone);
         if (s->counters) (void)hipFree(s->counters);
         if (s->d_tiles) (void)hipFree(s->d_tiles);
         if (s->d_blocks) (void)hipFree(s->d_blocks);

@@ -143,7 +143,10 @@ enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kS
 __host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_hits(int s) { return (2 * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_stat(int k, int s) { return (3 * kQShards + k * kStatShards + s) * kLine; }
-constexpr int kCntN = (3 * kQShards + kStatN * kStatShards) * kLine;
+// done(s), s < kStatShards: workgroups of k_frame finished per shard; done(kStatShards):
+// shards finished (two levels keep every same-address atomic count <= 64).
+__host__ __device__ constexpr int cnt_done(int s) { return (3 * kQShards + kStatN * kStatShards + s) * kLine; }
+constexpr int kCntN = (3 * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
 typedef unsigned long long cnt_t;
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
@@ -152,7 +155,8 @@ struct WorkArgs {
     uint32_t nblocks;
     uint32_t hit_cap;      // records per hit region (multiple of 64)
     HitRec* hits;          // kQShards regions of hit_cap records
-    uint8_t* lit;          // kQShards x n_lights regions of hit_cap flags
+    uint32_t* litw;        // per hit slot: bit l = light l reaches the hit (atomicOr by k_shadow)
+    uint32_t* blkdone;     // per 64-slot hit block: lights finished (the last one shades the block)
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
@@ -177,8 +181,10 @@ struct RayIO {
 
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
-hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, int grid, uint32_t opts, hipStream_t s);
-hipError_t launch_shade(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, hipStream_t s);
+hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                         hipStream_t s);
+hipError_t launch_frame(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                        hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,

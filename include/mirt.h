@@ -121,9 +121,9 @@ typedef struct {
     uint64_t shadow_rays;
     uint64_t hits;
     uint64_t tri_tests;     /* ray-triangle tests performed (brute force: rays * tris) */
-    double ms_primary;      /* raygen + nearest-hit kernel */
-    double ms_shadow;       /* shadow-ray kernel */
-    double ms_shade;        /* Phong + output kernel */
+    double ms_primary;      /* raygen + nearest-hit kernel (MIRT_OPT_FUSED_FRAME: the whole frame) */
+    double ms_shadow;       /* shadow-ray + Phong kernel */
+    double ms_shade;        /* separate shading kernel if any (0 when shading is folded in) */
     double ms_total;        /* first kernel start -> last kernel end */
 } mirt_stats;
 
@@ -209,6 +209,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split instead of the dynamic work queues */
 #define MIRT_OPT_TIMELINE 8u        /* record per-wave start/end stamps (mirt_debug_timeline) */
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
+#define MIRT_OPT_FUSED_FRAME 32u    /* one fused kernel per frame (primary + shadow + shade per 8x8 block) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*
