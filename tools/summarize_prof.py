@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    for k in ("k_primary", "k_secondary", "k_shade", "k_unpack", "k_debug_fp64"):
+    for k in ("k_primary", "k_shadow", "k_frame", "k_rays", "k_unpack", "k_debug_fp64"):
         if k in name:
             return k + ("<nopre>" if "false>" in name and k != "k_shade" else "")
     return name.split("(")[0][:40]
