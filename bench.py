@@ -30,6 +30,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"] if os.pa
 BYTES_PER_TRI_TEST = 72  # fp64 P1, E1, E2 read per ray-triangle test
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec, vector FP64 (FMA = 2 flops)
+HOST_CORES = 16  # the GPU box's CPU share for one GPU (os.cpu_count() shows the whole machine)
 
 
 def parse():
@@ -44,6 +45,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
+    ap.add_argument("--one-kernel", action="store_true", help="variant: one k_trace launch per frame")
     ap.add_argument("--static-schedule", action="store_true",
                     help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--brute-force", action="store_true",
@@ -54,27 +56,38 @@ def parse():
 
 
 def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
-    """The oracle's faithful variant (R-tree culling like rtreego, 1 thread, fp64,
-    worker/sequential's serial i/j loop) timed on this host over the full frame."""
+    """SURVEY.md §8(d) CPU baselines, timed on this host: (i) the oracle's faithful variant
+    (rtreego-style R-tree, 1 thread, fp64, worker/sequential's serial i/j loop) over one
+    full frame — the reported value; (ii) the same code on the box's host cores
+    (column-interleaved threads)."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
     orc = Oracle(load_scene(scene_path), use_rtree=True)
-    t0 = time.perf_counter()
-    r = orc.frame(W, H, nthreads=1)
-    dt = time.perf_counter() - t0
-    rays = r["stats"]["primary_rays"] + r["stats"]["shadow_rays"]
-    return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"one full {W}x{H} frame ({rays} primary+shadow rays), oracle/rt_oracle.c with "
-                      f"rtreego-style R-tree culling, single thread, {dt:.2f} s",
-            "ms_per_frame": round(dt * 1e3, 1)}
+    out = None
+    for threads in (1, HOST_CORES):
+        t0 = time.perf_counter()
+        r = orc.frame(W, H, nthreads=threads)
+        dt = time.perf_counter() - t0
+        rays = r["stats"]["primary_rays"] + r["stats"]["shadow_rays"]
+        v = {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+             "sample": f"one full {W}x{H} frame ({rays} primary+shadow rays), oracle/rt_oracle.c with "
+                       f"rtreego-style R-tree culling, {threads} thread(s), {dt:.2f} s",
+             "ms_per_frame": round(dt * 1e3, 1)}
+        if out is None:
+            out = v
+        else:
+            out["all_cores"] = {k: v[k] for k in ("value", "cores", "ms_per_frame")}
+    out["nproc"] = os.cpu_count()
+    return out
 
 
 def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int) -> dict:
-    """Bounded check of the timed frame: every 64th column vs the oracle (bit-exact)."""
+    """Parity gate of the timed frame: a 1/16 subsample — every 16th
+    column — against the oracle, valid mask and rgb8 bit-exact."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
-    cols = list(range(5, W, 64))
-    ref = Oracle(load_scene(scene_path)).trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=8)
+    cols = list(range(5, W, 16))
+    ref = Oracle(load_scene(scene_path)).trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=HOST_CORES)
     sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
     ok = bool(np.array_equal(fb_valid[sub], ref["valid"]) and np.array_equal(fb_rgb8[sub], ref["rgb8"]))
     return {"columns_checked": len(cols), "bit_exact": ok, "hits": int(fb_valid.sum())}
@@ -102,7 +115,7 @@ def main():
     ctx = rt.Context(local)
     opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
-        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0)
+        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_ONE_KERNEL if a.one_kernel else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     frame = env.mutable().to_frame()
@@ -159,12 +172,13 @@ def main():
         prim_ms = prof["primary_ms_sum"] / launches
         prim_tests = prof["primary_tri_tests"] / launches
         achieved = prim_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
-        traffic = None
+        traffic = fp64_flops = None
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
                 if tj.get("width") == W and tj.get("height") == H and tj.get("gpus", 1) == world:
                     traffic = tj.get("k_primary_hbm_bytes_per_launch")
+                    fp64_flops = tj.get("k_primary_fp64_flops_per_launch")
             except (OSError, ValueError):
                 traffic = None
         line = {
@@ -202,6 +216,13 @@ def main():
                          "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
                                  "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
                                  "VALU, see DESIGN.md"},
+            "roofline_fp64_valu": None if fp64_flops is None else {
+                "bound": "fp64-valu", "kernel": "k_primary", "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFLOPS,
+                "achieved": round(fp64_flops / (prim_ms / 1e3) / 1e12, 3),
+                "frac": round(fp64_flops / (prim_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
+                "flops_per_launch": fp64_flops,
+                "note": "SQ_INSTS_VALU_FLOPS_FP64 per launch from the committed rocprofv3 pass (profiles/), over "
+                        "this run's k_primary HIP-event time"},
         }
         if not a.no_parity:
             fr = sh.frame

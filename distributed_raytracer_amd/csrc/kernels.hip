@@ -34,6 +34,8 @@ typedef const __attribute__((address_space(4))) double* cdptr;
 typedef const __attribute__((address_space(4))) Bvh8Node* cnptr;
 typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
 typedef const __attribute__((address_space(4))) u32x16* cv16ptr;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) u32x4* cv4ptr;
 
 __device__ __forceinline__ V3 vload(const double* p) { return V3{p[0], p[1], p[2]}; }
 __device__ __forceinline__ void vstore(double* p, V3 v) {
@@ -209,6 +211,26 @@ struct Visits {
 struct WaveStats {
     cnt_t tests, nodes, leaves, hits, overflow;
 };
+// MIRT_PHASE_TIMING (diagnostic builds only): shader-clock cycles per phase of the primary
+// blocks, reported in the timeline record instead of the wave's start/end clocks.
+#ifndef MIRT_PHASE_TIMING
+#define MIRT_PHASE_TIMING 0
+#endif
+struct PhaseClock {
+    uint64_t acc[4] = {0, 0, 0, 0};
+    uint64_t t = 0;
+    __device__ __forceinline__ void start() {
+        if (MIRT_PHASE_TIMING) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int k) {
+        if (MIRT_PHASE_TIMING) {
+            const uint64_t n = __builtin_amdgcn_s_memtime();
+            acc[k] += n - t;
+            t = n;
+        }
+    }
+};
+
 __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], int stat_tests, int stat_nodes,
                                             int stat_leaves, int stat_hits, const WaveStats& w) {
     const uint32_t wave = threadIdx.x >> 6;
@@ -219,14 +241,23 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], in
         red[wave][3] = w.hits;
     }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0 && w.overflow) atomicAdd(&counters[cnt_stat(kStatOverflow, 0)], w.overflow);
+    // returning atomics: once the wave's vmcnt drains they have been performed, which is
+    // what frame_fold's done count relies on (no L2-flushing fence needed)
+    if ((threadIdx.x & 63) == 0 && w.overflow) {
+        const cnt_t old = atomicAdd(&counters[cnt_stat(kStatOverflow, 0)], w.overflow);
+        asm volatile("" ::"v"(old));
+    }
     if (threadIdx.x < 4) {
         cnt_t sum = 0;
         for (int k = 0; k < kWG / 64; ++k) sum += red[k][threadIdx.x];
         const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes
                        : threadIdx.x == 2 ? stat_leaves : stat_hits;
-        if (sum && stat >= 0) atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
+        if (sum && stat >= 0) {
+            const cnt_t old = atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
+            asm volatile("" ::"v"(old));
+        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Wave-uniform traversal stack held in two VGPRs: entry i lives in lane i % 64 of
@@ -253,8 +284,12 @@ struct WaveStack {
 struct Ray32 {
     float ox, oy, oz, ix, iy, iz, oix, oiy, oiz;
 };
+// 1/d from v_rcp_f64 refined by one Newton step (relative error far below fp32's 2^-24;
+// the slab tests only need ~2^-20).
 __device__ __forceinline__ float inv32(double d) {
-    const double r = 1.0 / d;
+    if (!(__builtin_fabs(d) >= 0x1p-60)) return __builtin_copysignf(0x1p60f, (float)d);  // tiny, zero or NaN
+    double r = __builtin_amdgcn_rcp(d);
+    r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
     return __builtin_fabs(r) > 0x1p60 ? __builtin_copysignf(0x1p60f, (float)d) : (float)r;
 }
 __device__ __forceinline__ Ray32 ray32(V3 ro, V3 d) {
@@ -324,18 +359,29 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
         for (int c = 0; c < 8; ++c)
             if (nd.child(c) != kBvhEmpty)  // branch-free: every lane evaluates, masks after
                 hits |= (uint32_t)(live & (force | slab32<SEG>(nd, c, r, tmax))) << c;
+        // classify the entered children (unrolled: SALU only), then test the leaves in ONE
+        // loop so the triangle test is instantiated once (code size: instruction cache)
+        uint32_t leafmask = 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const uint32_t ref = nd.child(c);
             if (ref == kBvhEmpty || __ballot((hits >> c) & 1u) == 0) continue;
-            if (ref & kBvhLeafBit) {
-                const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
-                ++vis.leaves;
-                test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
-                if (SEG) live = live && !(b.has && b.d < resolve);
-            } else {
+            if (ref & kBvhLeafBit)
+                leafmask |= 1u << c;
+            else
                 stk.push(ref);
-            }
+        }
+        const uint32_t r0 = nd.child(0), r1 = nd.child(1), r2 = nd.child(2), r3 = nd.child(3);
+        const uint32_t r4 = nd.child(4), r5 = nd.child(5), r6 = nd.child(6), r7 = nd.child(7);
+        while (leafmask) {
+            const uint32_t c = __builtin_ctz(leafmask);
+            leafmask &= leafmask - 1;
+            const uint32_t ref = c < 4 ? (c < 2 ? (c == 0 ? r0 : r1) : (c == 2 ? r2 : r3))
+                                       : (c < 6 ? (c == 4 ? r4 : r5) : (c == 6 ? r6 : r7));
+            const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
+            ++vis.leaves;
+            test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
+            if (SEG) live = live && !(b.has && b.d < resolve);
         }
         if (stk.sp == 0 || (SEG && __ballot(live) == 0)) break;
         cur = stk.pop();
@@ -699,9 +745,9 @@ __device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restri
 // read with atomics (device-coherent across the XCDs' L2s).
 __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& wa) {
     __shared__ bool last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics performed
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
         const uint32_t sh = blockIdx.x % kStatShards;
         const uint32_t in_shard = (gridDim.x - sh + kStatShards - 1) / kStatShards;
         bool l = atomicAdd(&wa.counters[cnt_done(sh)], (cnt_t)1) == (cnt_t)in_shard - 1;
@@ -713,7 +759,6 @@ __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& 
     }
     __syncthreads();
     if (!last || threadIdx.x >= kStatN) return;
-    __threadfence();
     const int st = threadIdx.x;
     cnt_t sum = 0;
     for (int sh = 0; sh < kStatShards; ++sh)
@@ -747,19 +792,22 @@ struct ShardCursor {
 };
 // MIRT_OPT_TIMELINE: per-wave stamps (mirt.h mirt_debug_timeline).
 struct WaveClock {
-    uint64_t real0, clk0;
+    uint64_t real0, clk0, staged = 0;
+    bool real0_override = false;
+    uint64_t phase_setup = 0, phase_trace = 0;
     __device__ __forceinline__ WaveClock() {
         real0 = __builtin_amdgcn_s_memrealtime();
         clk0 = __builtin_amdgcn_s_memtime();
     }
+    __device__ __forceinline__ void mark_staged() { staged = __builtin_amdgcn_s_memrealtime(); }
     __device__ __forceinline__ void record(const WorkArgs& wa, uint32_t kernel, uint32_t items) const {
         const uint64_t real1 = __builtin_amdgcn_s_memrealtime(), clk1 = __builtin_amdgcn_s_memtime();
         const uint32_t gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
         const uint32_t lane = threadIdx.x & 63;
         if (gw >= wa.timeline_cap || lane >= kTimelineRec) return;
-        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
-        const uint64_t v[kTimelineRec] = {kernel, gw, real0, real1, clk0, clk1, hwid, xcc | ((uint64_t)items << 32)};
+        const uint64_t v[kTimelineRec] = {kernel, gw, real0, real1, real0_override ? phase_setup : clk0,
+                                          real0_override ? phase_trace : clk1, staged, xcc | ((uint64_t)items << 32)};
         uint64_t x = 0;
 #pragma unroll
         for (int k = 0; k < kTimelineRec; ++k) x = lane == (uint32_t)k ? v[k] : x;
@@ -768,26 +816,224 @@ struct WaveClock {
 };
 
 // One ticket of counter c, issued by lane 0; resolve() broadcasts it (waits for the atomic).
+// Queue, hit-slot and primary-done counters are used through the low 32-bit word of
+// their line: a 32-bit returning atomic lands in one VGPR (a 64-bit one whose unused high
+// half gets reused forces an immediate wait for the atomic).
+__device__ __forceinline__ uint32_t* lo32(cnt_t* c) { return (uint32_t*)c; }
 __device__ __forceinline__ uint32_t ticket_issue(cnt_t* c) {
     uint32_t t = 0;
-    if ((threadIdx.x & 63) == 0) t = (uint32_t)atomicAdd(c, (cnt_t)1);
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(lo32(c), 1u);
     return t;
 }
 __device__ __forceinline__ uint32_t ticket_resolve(uint32_t t) { return __builtin_amdgcn_readfirstlane(t); }
 
-// ---------------------------------------------------------------- primary
+// ---------------------------------------------------------------- hit slots
+// A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.  COH: device-scope
+// atomic stores / loads (coherent across the XCDs' L2s without cache flushes), used when
+// the producer and the consumer of a slot run in the same kernel (k_trace).
+template <bool COH>
+__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
+    if (COH)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+template <bool COH>
+__device__ __forceinline__ uint64_t ld64(const uint64_t* p) {
+    if (COH) return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
+    if (COH)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+__device__ __forceinline__ double bitsd(uint64_t x) { return __longlong_as_double((long long)x); }
+
+// Descriptor of block k of shard q (shard-major table; scalar load; zero if past the end).
+__device__ __forceinline__ BlockDesc block_desc(const WorkArgs& wa, uint32_t q, uint32_t k) {
+    // readfirstlane: the index is provably uniform, so this is one s_load_dwordx4 (lgkmcnt),
+    // not a vector load whose vmcnt wait would also wait for the in-flight ticket atomic
+    const uint32_t kk = __builtin_amdgcn_readfirstlane(min(k, wa.per_shard - 1));
+    const uint32_t qq = __builtin_amdgcn_readfirstlane(q);
+    const u32x4 v = ((cv4ptr)wa.blocks)[(size_t)qq * wa.per_shard + kk];
+    return k < wa.per_shard ? BlockDesc{v[0], v[1], v[2], v[3]} : BlockDesc{0, 0, 0, 0};
+}
+
+// ---------------------------------------------------------------- primary block
+// One 8x8 pixel block: raygen (tracer.go:15-22, :86), nearest hit, outputs of misses,
+// and, if any lane hit, 64 hit slots of region q (slot = lane) with their lit word and
+// the block's light counter zeroed.  REL: the LDS mesh is stored relative to the camera.
+template <bool REL, bool PREFILTER, bool BRUTE, bool COH>
+__device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
+                                              const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
+                                              const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc) {
+    pc.start();
+    const uint32_t lane = threadIdx.x & 63;
+    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    const uint32_t lx = lane >> 3, ly = lane & 7;
+    const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
+    const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
+    const bool active = lx < vw && ly < vh;
+    const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
+
+    // tracer.go:15-22 pixelToPoint (its two divisions, per column and per row, come from
+    // the host-built table: same fp64 operations), then tracer.go:86 (p - Cam.Pos).Norm()
+    const double si = wa.sij[i];
+    const double sj = wa.sij[fa.W + j];
+    V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}), scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
+               scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
+    V3 d = norm(sub(p, cam));
+
+    Visits vis{0, 0, 0, 0};
+    pc.lap(0);
+    Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d, active, true, vis, stk);
+    pc.lap(1);
+    ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+    ws.nodes += vis.nodes;
+    ws.leaves += vis.leaves;
+    ws.overflow += vis.overflow;
+
+    const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
+    const bool is_hit = active && nh.ok;
+    if (active) {
+        if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
+        if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
+        if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
+        if (!is_hit) {
+            if (out.rgb) {
+                out.rgb[3 * oidx] = 0.0;
+                out.rgb[3 * oidx + 1] = 0.0;
+                out.rgb[3 * oidx + 2] = 0.0;
+            }
+            if (out.rgb8) {
+                out.rgb8[3 * oidx] = 0;
+                out.rgb8[3 * oidx + 1] = 0;
+                out.rgb8[3 * oidx + 2] = 0;
+            }
+        }
+    }
+    const uint64_t mask = __ballot(is_hit);
+    if (!mask) {
+        pc.lap(2);
+        return;
+    }
+    ws.hits += __popcll(mask);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    const size_t slot = (size_t)q * wa.hit_cap + base + lane;
+    uint64_t* w = (uint64_t*)&wa.hits[slot];
+    if (is_hit) {
+        st64<COH>(w + 0, dbits(nh.hit.x));
+        st64<COH>(w + 1, dbits(nh.hit.y));
+        st64<COH>(w + 2, dbits(nh.hit.z));
+        st64<COH>(w + 3, dbits(nh.normal.x));
+        st64<COH>(w + 4, dbits(nh.normal.y));
+        st64<COH>(w + 5, dbits(nh.normal.z));
+        st64<COH>(w + 6, oidx);
+        st64<COH>(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
+    } else {
+        st64<COH>(w + 7, (uint64_t)kNoHit);
+    }
+    st32<COH>(&wa.litw[slot], 0u);
+    if (lane == 0) st32<COH>(&wa.blkdone[slot / 64], 0u);
+    if (COH) {
+        // publish: every lane's stores are performed before the chunk is marked ready
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) st32<true>(&wa.rdy[slot / 64], wa.frame_tag);
+    }
+    pc.lap(2);
+}
+
+// ---------------------------------------------------------------- shadow item
+// 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
+// (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
+// the wave that finishes the chunk's last light.  n_lights == 0: one pass that shades.
+template <bool PREFILTER, bool BRUTE, bool COH>
+__device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
+                                            const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
+                                            bool segment, uint32_t q, uint32_t c, uint32_t l, WaveStats& ws) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nl = max(fa.n_lights, 1u);
+    const size_t slot = (size_t)q * wa.hit_cap + (size_t)c * 64 + lane;
+    const uint64_t* w = (const uint64_t*)&wa.hits[slot];
+    const uint64_t w7 = ld64<COH>(w + 7);
+    const bool active = (uint32_t)w7 != kNoHit;
+    V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
+    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+    if (active) {
+        hit = V3{bitsd(ld64<COH>(w)), bitsd(ld64<COH>(w + 1)), bitsd(ld64<COH>(w + 2))};
+        V3 ldir = norm(sub(lpos, hit));     // tracer.go:61
+        o = add(hit, scale(ldir, 0.0001));  // tracer.go:64
+        d = ldir;
+    }
+    Visits vis{0, 0, 0, 0};
+    bool is_lit = false;
+    if (fa.n_lights == 0) {
+        // no lights: nothing to trace, the pass only shades (ambient)
+    } else if (segment) {
+        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis);
+    } else {
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis);
+        // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
+        is_lit = !r.ok || len(sub(lpos, hit)) < len(sub(r.hit, hit));
+    }
+    ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+    ws.nodes += vis.nodes;
+    ws.leaves += vis.leaves;
+    ws.overflow += vis.overflow;
+    // publish this light's bit, then count the light done for the chunk; device-scope
+    // atomics are coherent across XCDs and the wait orders the two atomics
+    if (active && is_lit) {
+        const uint32_t old =
+            __hip_atomic_fetch_or(&wa.litw[slot], 1u << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t done = 0;
+    if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done != nl - 1 || !active) return;
+    const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
+    const V3 n{bitsd(ld64<COH>(w + 3)), bitsd(ld64<COH>(w + 4)), bitsd(ld64<COH>(w + 5))};
+    const uint64_t oidx = ld64<COH>(w + 6);
+    const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
+    const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+    if (out.rgb) {
+        out.rgb[3 * oidx] = col.r;
+        out.rgb[3 * oidx + 1] = col.g;
+        out.rgb[3 * oidx + 2] = col.b;
+    }
+    if (out.rgb8) {
+        out.rgb8[3 * oidx] = c_u8(col.r);
+        out.rgb8[3 * oidx + 1] = c_u8(col.g);
+        out.rgb8[3 * oidx + 2] = c_u8(col.b);
+    }
+}
+
+// ---------------------------------------------------------------- primary kernel
 // RESIDENT (host-decided): one object whose mesh fits in LDS; it is staged once per
 // persistent workgroup, relative to the camera (p1or), and every sweep reads LDS.
-// Work item: one 8x8 pixel block (BlockDesc), lane -> (x, y) with y fastest so a wave's
-// writes are 8 runs of 8 contiguous pixels of the column-major packed tile.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
-    const WaveClock clock;
+    WaveClock clock;
     uint32_t taken = 0;
-    V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    const ShardCursor sc;
+    // the first two tickets are in flight while the mesh is staged
+    uint32_t q = sc.first_shard();
+    uint32_t t0 = 0, t1 = 0;
+    if (wa.dynamic && q < (uint32_t)kQShards) {
+        t0 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
+        t1 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
+    }
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
     if (RESIDENT) {
@@ -795,111 +1041,73 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
         __syncthreads();
     }
-    const uint32_t lane = threadIdx.x & 63;
-    const ShardCursor sc;
+    clock.mark_staged();
     WaveStats ws{0, 0, 0, 0, 0};
-    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+    PhaseClock pc;
+    for (; q < (uint32_t)kQShards; q += sc.shard_step()) {
         cnt_t* qc = &wa.counters[cnt_queue(0, q)];
-        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
-        for (;;) {
-            const uint32_t blk = k * kQShards + q;
-            if (blk >= wa.nblocks) break;
-            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;  // in flight while tracing
+        // Ticket pipeline two deep: when block k starts, ticket k+1 is already known, so
+        // its descriptor is fetched (scalar loads, no wait) while block k is traced.
+        uint32_t k, kn;
+        if (wa.dynamic) {
+            if (q != sc.first_shard()) {
+                t0 = ticket_issue(qc);
+                t1 = ticket_issue(qc);
+            }
+            k = ticket_resolve(t0);
+            kn = ticket_resolve(t1);
+        } else {
+            k = sc.rank();
+            kn = k + sc.peers();
+        }
+        uint32_t blk = k * kQShards + q;
+        BlockDesc bd = block_desc(wa, q, k);
+        while (blk < wa.nblocks) {
+            const uint32_t t2 = wa.dynamic ? ticket_issue(qc) : 0;
+            const uint32_t nblk = kn * kQShards + q;
+            const BlockDesc nbd = block_desc(wa, q, kn);  // scalar loads, used next iteration
             ++taken;
-            const BlockDesc bd = wa.blocks[blk];
-            const uint32_t lx = lane >> 3, ly = lane & 7;
-            const bool active = lx < bd.vw && ly < bd.vh;
-            const int i = (int)(bd.px + (active ? lx : 0)), j = (int)(bd.py + (active ? ly : 0));
-
-            // tracer.go:15-22 pixelToPoint, then tracer.go:86 dir = (p - Cam.Pos).Norm()
-            const double si = fa.phw * ((double)(fa.halfW - i) - 0.5) / (double)fa.halfW;
-            const double sj = fa.phh * ((double)(fa.halfH - j) - 0.5) / (double)fa.halfH;
-            V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}),
-                           scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
-                       scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
-            V3 d = norm(sub(p, cam));
-
-            Visits vis{0, 0, 0, 0};
-            Nearest nh = trace_nearest<RESIDENT, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, RESIDENT, cam, d, active, true, vis,
-                                                                          wstk[threadIdx.x >> 6]);
-            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-            ws.nodes += vis.nodes;
-            ws.leaves += vis.leaves;
-            ws.overflow += vis.overflow;
-
-            const uint64_t oidx = bd.out + (uint64_t)lx * bd.th + ly;
-            const bool is_hit = active && nh.ok;
-            if (active) {
-                if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
-                if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
-                if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
-                if (!is_hit) {
-                    if (out.rgb) {
-                        out.rgb[3 * oidx] = 0.0;
-                        out.rgb[3 * oidx + 1] = 0.0;
-                        out.rgb[3 * oidx + 2] = 0.0;
-                    }
-                    if (out.rgb8) {
-                        out.rgb8[3 * oidx] = 0;
-                        out.rgb8[3 * oidx + 1] = 0;
-                        out.rgb8[3 * oidx + 2] = 0;
-                    }
-                }
-            }
-            // blocks with hits take 64 slots of hit region q (slot = lane)
-            const uint64_t mask = __ballot(is_hit);
-            if (mask) {
-                ws.hits += __popcll(mask);
-                uint32_t base = 0;
-                if (lane == 0) base = (uint32_t)atomicAdd(&wa.counters[cnt_hits(q)], (cnt_t)64);
-                base = __builtin_amdgcn_readfirstlane(base);
-                const size_t slot = (size_t)q * wa.hit_cap + base + lane;
-                HitRec& hr = wa.hits[slot];
-                wa.litw[slot] = 0;
-                if (lane == 0) wa.blkdone[slot / 64] = 0;
-                if (is_hit) {
-                    vstore(hr.h, nh.hit);
-                    vstore(hr.n, nh.normal);
-                    hr.out = oidx;
-                    hr.obj = nh.obj;
-                    hr.mat = nh.mat;
-                } else {
-                    hr.obj = kNoHit;
-                }
-            }
-            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+            primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd, q,
+                                                             ws, pc);
+            blk = nblk;
+            bd = nbd;
+            kn = wa.dynamic ? ticket_resolve(t2) : kn + sc.peers();
+            pc.lap(3);
         }
     }
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
+    if (MIRT_PHASE_TIMING) {  // record [4], [5], [6] = cycles in setup+raygen, trace, outputs
+        clock.clk0 = 0;
+        clock.staged = pc.acc[3];
+        clock.real0_override = true;
+        clock.phase_trace = pc.acc[2];
+        clock.phase_setup = pc.acc[0] + pc.acc[1];
+    }
     if (wa.timeline) clock.record(wa, 0, taken);
 }
 
-// ---------------------------------------------------------------- shadow rays
-// Work item: 64 consecutive hits of one region and one light (consecutive lanes =
-// neighbouring pixels towards the same light: coherent rays).  Tickets of shard q
-// enumerate (light, chunk) of region q.
+// ---------------------------------------------------------------- shadow kernel
+// Work item: the 64 slots of one hit block x one light.  Tickets of shard q enumerate
+// (light, chunk) of region q.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
+    __shared__ cnt_t red[kWG / 64][4];
     // segment query for one-object frames (BVH kernels only; brute force stays literal)
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
-    __shared__ cnt_t red[kWG / 64][4];
-    const WaveClock clock;
+    WaveClock clock;
     uint32_t taken = 0;
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
-    // frame statistics of the primary kernel (complete); the shadow kernel's own are folded
-    // by its last workgroup below
-    const uint32_t lane = threadIdx.x & 63;
+    clock.mark_staged();
     const ShardCursor sc;
     WaveStats ws{0, 0, 0, 0, 0};
+    const uint32_t nl = max(fa.n_lights, 1u);
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        const uint32_t nh = (uint32_t)wa.counters[cnt_hits(q)];
-        const uint32_t nch = (nh + 63) / 64;
-        const uint32_t nl = max(fa.n_lights, 1u);  // no lights: one pass that only shades
+        const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
         const uint32_t items = nch * nl;
         cnt_t* qc = &wa.counters[cnt_queue(1, q)];
         uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
@@ -907,62 +1115,7 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            const uint32_t h = c * 64 + lane;  // nh is a multiple of 64
-            const HitRec* hr = &wa.hits[(size_t)q * wa.hit_cap + h];
-            const bool active = hr->obj != kNoHit;
-            V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
-            const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
-            if (active) {
-                hit = vload(hr->h);
-                V3 ldir = norm(sub(lpos, hit));     // tracer.go:61
-                o = add(hit, scale(ldir, 0.0001));  // tracer.go:64
-                d = ldir;
-            }
-            Visits vis{0, 0, 0, 0};
-            bool is_lit = false;
-            if (fa.n_lights == 0) {
-                // no lights: nothing to trace, the pass only shades (ambient)
-            } else if (segment) {
-                is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, wstk[threadIdx.x >> 6], hit, o, d, lpos, active,
-                                                      vis);
-            } else {
-                Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, false, vis);
-                // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
-                is_lit = !r.ok || len(sub(lpos, hit)) < len(sub(r.hit, hit));
-            }
-            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-            ws.nodes += vis.nodes;
-            ws.leaves += vis.leaves;
-            ws.overflow += vis.overflow;
-            // publish this light's bits, then count the light done for the block; the wave
-            // finishing the block's last light shades it (tracer.go:53-76).  Device-scope
-            // atomics are coherent across XCDs; the wait orders the two atomics.
-            const size_t slot = (size_t)q * wa.hit_cap + h;
-            if (active && is_lit) {
-                // returning atomic: its completion (vmcnt) means it has been performed
-                const uint32_t old = __hip_atomic_fetch_or(&wa.litw[slot], 1u << l, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("" ::"v"(old));
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t done = 0;
-            if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
-            done = __builtin_amdgcn_readfirstlane(done);
-            if (done == nl - 1 && active) {
-                const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
-                const HitRec rec = *hr;
-                const RGB col = phong(fa, fa.obj[rec.obj].m.mats + (size_t)rec.mat * 10, hit, vload(rec.n), lit);
-                if (out.rgb) {
-                    out.rgb[3 * rec.out] = col.r;
-                    out.rgb[3 * rec.out + 1] = col.g;
-                    out.rgb[3 * rec.out + 2] = col.b;
-                }
-                if (out.rgb8) {
-                    out.rgb8[3 * rec.out] = c_u8(col.r);
-                    out.rgb8[3 * rec.out + 1] = c_u8(col.g);
-                    out.rgb8[3 * rec.out + 2] = c_u8(col.b);
-                }
-            }
+            shadow_item<PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment, q, c, l, ws);
             k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
@@ -971,112 +1124,99 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
     frame_fold(fa, wa);
 }
 
-// ---------------------------------------------------------------- fused frame
-// One work item = one 8x8 pixel block, traced start to finish by one wave: primary rays,
-// then for each light one shadow packet over the block's hit lanes (converging on the
-// light: coherent), then Phong, all in registers.  No hit slots, no lit flags, one
-// launch per frame and one tail instead of three.  The mesh sits in LDS in absolute
-// coordinates (both ray kinds read it).
+// ---------------------------------------------------------------- one-launch frame
+// k_trace: primary blocks and shadow items in ONE persistent kernel.  A wave serves shard
+// q; shadow items (chunk, light) of region q become available as primary blocks of shard
+// q publish their hit slots (allocation counter + per-chunk ready tag), so the shadow
+// work of early blocks overlaps the primary work of late ones and the frame has one tail.
+// Waves prefer available shadow items, then primary blocks, and otherwise sleep until
+// either appears; a wave leaves the shard when every primary block of the shard is done
+// and its shadow ticket is past the final item count.  Nothing waits on a wave that has
+// not started (tickets are only taken by running waves), so progress does not depend on
+// every workgroup being resident.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-MIRT_TRACE_KERNEL void k_frame(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    __shared__ uint32_t wstk[kWG / 64][(MIRT_PRIMARY_WIDE || MIRT_SHADOW_WIDE) ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
-    const WaveClock clock;
-    uint32_t taken = 0;
-    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    WaveClock clock;
+    uint32_t taken = 0;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
-    const uint32_t lane = threadIdx.x & 63;
+    clock.mark_staged();
+    uint32_t* stk = wstk[threadIdx.x >> 6];
     const ShardCursor sc;
-    WaveStats ws{0, 0, 0, 0, 0};
-    WaveStats wsh{0, 0, 0, 0, 0};
-    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        cnt_t* qc = &wa.counters[cnt_queue(0, q)];
-        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+    WaveStats wp{0, 0, 0, 0, 0}, wsh{0, 0, 0, 0, 0};
+    const uint32_t nl = max(fa.n_lights, 1u);
+    constexpr uint32_t kNone = 0xffffffffu;
+    // Every wait is bounded (~1 s): should progress ever stall, the wave records it in the
+    // overflow statistic (tests assert 0) and leaves, so the kernel always drains.
+    constexpr uint32_t kSpinLimit = 1u << 24;
+    uint32_t spins = 0;
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards && spins < kSpinLimit; q += sc.shard_step()) {
+        const uint32_t nprim = (wa.nblocks > q) ? (wa.nblocks - q + kQShards - 1) / kQShards : 0;
+        cnt_t* pq = &wa.counters[cnt_queue(0, q)];
+        cnt_t* sqc = &wa.counters[cnt_queue(1, q)];
+        uint32_t* sq = lo32(sqc);
+        uint32_t* alloc = lo32(&wa.counters[cnt_hits(q)]);
+        uint32_t* pdone = lo32(&wa.counters[cnt_pdone(q)]);
+        uint32_t pk = ticket_resolve(ticket_issue(pq));
+        uint32_t pend = kNone;
         for (;;) {
-            const uint32_t blk = k * kQShards + q;
-            if (blk >= wa.nblocks) break;
-            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;  // in flight while tracing
-            ++taken;
-            const BlockDesc bd = wa.blocks[blk];
-            const uint32_t lx = lane >> 3, ly = lane & 7;
-            const bool active = lx < bd.vw && ly < bd.vh;
-            const int i = (int)(bd.px + (active ? lx : 0)), j = (int)(bd.py + (active ? ly : 0));
-
-            // tracer.go:15-22 pixelToPoint, then tracer.go:86 dir = (p - Cam.Pos).Norm()
-            const double si = fa.phw * ((double)(fa.halfW - i) - 0.5) / (double)fa.halfW;
-            const double sj = fa.phh * ((double)(fa.halfH - j) - 0.5) / (double)fa.halfH;
-            V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}),
-                           scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
-                       scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
-            V3 d = norm(sub(p, cam));
-
-            Visits vis{0, 0, 0, 0};
-            Nearest nh = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, cam, d, active, true, vis);
-            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-            ws.nodes += vis.nodes;
-            ws.leaves += vis.leaves;
-            ws.overflow += vis.overflow;
-
-            const uint64_t oidx = bd.out + (uint64_t)lx * bd.th + ly;
-            const bool is_hit = active && nh.ok;
-            if (active) {
-                if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
-                if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
-                if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
+            // 1. a shadow item whose chunk has been allocated
+            const uint32_t avail =
+                (uint32_t)(__hip_atomic_load(alloc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 64) * nl;
+            if (pend == kNone &&
+                (uint32_t)__hip_atomic_load(sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < avail)
+                pend = ticket_resolve(ticket_issue(sqc));
+            if (pend != kNone && pend < avail) {
+                const uint32_t c = pend / nl, l = pend - c * nl;
+                // the allocating wave is still writing the chunk: wait for its ready tag
+                while (__hip_atomic_load(&wa.rdy[(size_t)q * (wa.hit_cap / 64) + c], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) != wa.frame_tag &&
+                       ++spins < kSpinLimit)
+                    __builtin_amdgcn_s_sleep(1);
+                if (spins >= kSpinLimit) break;
+                ++taken;
+                shadow_item<PREFILTER, BRUTE, true>(fa, wa, out, lds, stk, RESIDENT, segment, q, c, l, wsh);
+                pend = kNone;
+                continue;
             }
-            const uint64_t mask = __ballot(is_hit);
-            RGB col{0, 0, 0};
-            if (mask) {
-                ws.hits += __popcll(mask);
-                uint32_t lit = 0;
-                for (uint32_t l = 0; l < fa.n_lights; ++l) {
-                    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
-                    V3 o{0, 0, 0}, sd{1, 0, 0};
-                    if (is_hit) {
-                        const V3 ldir = norm(sub(lpos, nh.hit));  // tracer.go:61
-                        o = add(nh.hit, scale(ldir, 0.0001));     // tracer.go:64
-                        sd = ldir;
-                    }
-                    Visits sv{0, 0, 0, 0};
-                    bool is_lit;
-                    if (segment) {
-                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, nh.hit, o, sd, lpos, is_hit, sv);
-                    } else {
-                        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, sd, is_hit, false, sv);
-                        // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
-                        is_lit = !r.ok || len(sub(lpos, nh.hit)) < len(sub(r.hit, nh.hit));
-                    }
-                    wsh.tests += (cnt_t)sv.tests * __popcll(mask);
-                    wsh.nodes += sv.nodes;
-                    wsh.leaves += sv.leaves;
-                    wsh.overflow += sv.overflow;
-                    lit |= (uint32_t)is_lit << l;
-                }
-                if (is_hit) col = phong(fa, fa.obj[nh.obj].m.mats + (size_t)nh.mat * 10, nh.hit, nh.normal, lit);
+            // 2. a primary block
+            if (pk < nprim) {
+                const uint32_t nxt = ticket_issue(pq);
+                ++taken;
+                const BlockDesc bd = block_desc(wa, q, pk);
+                PhaseClock pc;
+                primary_block<false, PREFILTER, BRUTE, true>(fa, wa, out, lds, stk, RESIDENT, bd, q, wp, pc);
+                // count the block done after its slots are published (allocation first)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if ((threadIdx.x & 63) == 0) atomicAdd(pdone, 1u);
+                pk = ticket_resolve(nxt);
+                continue;
             }
-            if (active) {
-                if (out.rgb) {
-                    out.rgb[3 * oidx] = col.r;
-                    out.rgb[3 * oidx + 1] = col.g;
-                    out.rgb[3 * oidx + 2] = col.b;
+            // 3. nothing available now
+            if ((uint32_t)__hip_atomic_load(pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nprim) {
+                const uint32_t total =
+                    (uint32_t)(__hip_atomic_load(alloc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 64) * nl;
+                if (pend == kNone) {
+                    if ((uint32_t)__hip_atomic_load(sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) break;
+                    pend = ticket_resolve(ticket_issue(sqc));
                 }
-                if (out.rgb8) {
-                    out.rgb8[3 * oidx] = c_u8(col.r);
-                    out.rgb8[3 * oidx + 1] = c_u8(col.g);
-                    out.rgb8[3 * oidx + 2] = c_u8(col.b);
-                }
+                if (pend >= total) break;
+                continue;
             }
-            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+            if (++spins >= kSpinLimit) break;
+            __builtin_amdgcn_s_sleep(2);
         }
     }
-    wsh.hits = 0;
-    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
+    if (spins >= kSpinLimit) wp.overflow += 1;
+    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, wp);
     __syncthreads();
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
     if (wa.timeline) clock.record(wa, 0, taken);
@@ -1209,12 +1349,12 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
     return hipGetLastError();
 }
 
-hipError_t launch_frame(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                         hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_FRAME(P, B, R) hipLaunchKernelGGL((k_frame<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
-    MIRT_DISPATCH(K_FRAME);
-#undef K_FRAME
+#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    MIRT_DISPATCH(K_TRACE);
+#undef K_TRACE
     return hipGetLastError();
 }
 

@@ -64,6 +64,9 @@ struct Slot {
     size_t litw_cap = 0;
     uint32_t* blkdone = nullptr;
     size_t blkdone_cap = 0;
+    uint32_t* rdy = nullptr;
+    size_t rdy_cap = 0;
+    uint32_t frame_tag = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
@@ -74,7 +77,13 @@ struct Slot {
     BlockDesc* h_blocks = nullptr;  // pinned staging
     size_t blocks_cap = 0, h_blocks_cap = 0;
     std::vector<mirt_tile> blocks_key;
-    uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0;
+    uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0, per_shard = 0;
+    // pixelToPoint per column / per row (tracer.go:19-20), cached per (fov, W, H)
+    double* d_sij = nullptr;
+    double* h_sij = nullptr;  // pinned staging
+    size_t sij_cap = 0, h_sij_cap = 0;
+    double sij_phw = 0, sij_phh = 0;
+    uint32_t sij_W = 0, sij_H = 0;
     cnt_t* summary = nullptr;     // kStatN totals of the last frame (device)
     cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
     bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
@@ -275,9 +284,10 @@ int prof_get(mirt_ctx* c, ProfRec& r) {
     return MIRT_OK;
 }
 
-// Enqueue primary -> shadow -> shade for a tile list on stream s.
-// Block table of a tile list: one BlockDesc per 8x8 block, tiles in list order, blocks of
-// a tile column-major.  Rebuilt and uploaded only when the list changes.
+// Block table of a tile list: linear block number k runs over the tiles in list order and
+// over each tile's blocks column-major; entry (k % kQShards) * per_shard + k / kQShards
+// holds block k (shard-major, mirt_internal.hpp).  Rebuilt and uploaded only when the
+// list changes.
 int blocks_prepare(Slot* sl, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n, hipStream_t s) {
     if (sl->blocks_W == W && sl->blocks_H == H && sl->blocks_key.size() == n &&
         memcmp(sl->blocks_key.data(), tiles, sizeof(mirt_tile) * n) == 0)
@@ -287,36 +297,63 @@ int blocks_prepare(Slot* sl, uint32_t W, uint32_t H, const mirt_tile* tiles, uin
     for (uint32_t t = 0; t < n; ++t)
         nb += (uint64_t)((tiles[t].w + kBlk - 1) / kBlk) * ((tiles[t].h + kBlk - 1) / kBlk);
     if (nb > 0x7fffffffull) return fail(MIRT_E_LIMIT, "too many 8x8 blocks in one call");
-    int r = dev_grow(sl->d_blocks, sl->blocks_cap, nb);
+    const uint64_t per_shard = (nb + kQShards - 1) / kQShards;
+    const uint64_t entries = per_shard * kQShards;
+    int r = dev_grow(sl->d_blocks, sl->blocks_cap, entries);
     if (r != MIRT_OK) return r;
-    if (sl->h_blocks_cap < nb) {
+    if (sl->h_blocks_cap < entries) {
         if (sl->h_blocks) (void)hipHostFree(sl->h_blocks);
         sl->h_blocks = nullptr;
         sl->h_blocks_cap = 0;
-        HIP_TRY(hipHostMalloc((void**)&sl->h_blocks, sizeof(BlockDesc) * nb));
-        sl->h_blocks_cap = nb;
+        HIP_TRY(hipHostMalloc((void**)&sl->h_blocks, sizeof(BlockDesc) * entries));
+        sl->h_blocks_cap = entries;
     }
-    uint64_t off = 0, k = 0;
+    memset(sl->h_blocks, 0, sizeof(BlockDesc) * entries);
+    uint64_t off = 0, k = 0;  // k: linear block number, tiles in list order, blocks column-major
     for (uint32_t t = 0; t < n; ++t) {
         const mirt_tile& tl = tiles[t];
         for (uint32_t bx = 0; bx < tl.w; bx += kBlk)
-            for (uint32_t by = 0; by < tl.h; by += kBlk) {
-                BlockDesc& b = sl->h_blocks[k++];
-                b.out = off + (uint64_t)bx * tl.h + by;
-                b.px = tl.x + bx;
-                b.py = tl.y + by;
-                b.th = tl.h;
-                b.vw = std::min<uint32_t>(kBlk, tl.w - bx);
-                b.vh = std::min<uint32_t>(kBlk, tl.h - by);
+            for (uint32_t by = 0; by < tl.h; by += kBlk, ++k) {
+                BlockDesc& b = sl->h_blocks[(k % kQShards) * per_shard + k / kQShards];
+                b.out = (uint32_t)(off + (uint64_t)bx * tl.h + by);
+                b.pxy = (tl.x + bx) | ((tl.y + by) << 16);
+                b.geo = tl.h | (std::min<uint32_t>(kBlk, tl.w - bx) << 16) | (std::min<uint32_t>(kBlk, tl.h - by) << 24);
                 b.pad = 0;
             }
         off += (uint64_t)tl.w * tl.h;
     }
-    HIP_TRY(hipMemcpyAsync(sl->d_blocks, sl->h_blocks, sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(sl->d_blocks, sl->h_blocks, sizeof(BlockDesc) * entries, hipMemcpyHostToDevice, s));
     sl->blocks_key.assign(tiles, tiles + n);
     sl->blocks_W = W;
     sl->blocks_H = H;
     sl->nblocks = (uint32_t)nb;
+    sl->per_shard = (uint32_t)per_shard;
+    return MIRT_OK;
+}
+
+// tracer.go:16-20 per column and per row: sx = phw * (float64(halfW - i) - 0.5) /
+// float64(halfW) (and sy likewise), the same fp64 operations the reference does per pixel.
+int sij_prepare(Slot* sl, const FrameArgs& fa, hipStream_t s) {
+    const uint32_t W = (uint32_t)fa.W, H = (uint32_t)fa.H;
+    if (sl->sij_W == W && sl->sij_H == H && sl->sij_phw == fa.phw && sl->sij_phh == fa.phh) return MIRT_OK;
+    const size_t n = (size_t)W + H;
+    int r = dev_grow(sl->d_sij, sl->sij_cap, n);
+    if (r != MIRT_OK) return r;
+    if (sl->h_sij_cap < n) {
+        if (sl->h_sij) (void)hipHostFree(sl->h_sij);
+        sl->h_sij = nullptr;
+        sl->h_sij_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&sl->h_sij, sizeof(double) * n));
+        sl->h_sij_cap = n;
+    }
+    for (uint32_t i = 0; i < W; ++i) sl->h_sij[i] = fa.phw * ((double)(fa.halfW - (int32_t)i) - 0.5) / (double)fa.halfW;
+    for (uint32_t j = 0; j < H; ++j)
+        sl->h_sij[W + j] = fa.phh * ((double)(fa.halfH - (int32_t)j) - 0.5) / (double)fa.halfH;
+    HIP_TRY(hipMemcpyAsync(sl->d_sij, sl->h_sij, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    sl->sij_W = W;
+    sl->sij_H = H;
+    sl->sij_phw = fa.phw;
+    sl->sij_phh = fa.phh;
     return MIRT_OK;
 }
 
@@ -336,19 +373,33 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         pixels += (uint64_t)tl.w * tl.h;
     }
     if (pixels > 0xffffffffull) return fail(MIRT_E_LIMIT, "more than 2^32 pixels in one call");
+    if (W > 65535 || H > 65535) return fail(MIRT_E_LIMIT, "screen width/height above 65535");
     FrameArgs fa;
     uint64_t tris = 0;
     fill_args(c, f, W, H, fa, tris);
     if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
+    if ((r = sij_prepare(sl, fa, s)) != MIRT_OK) return r;
     const uint32_t nl = f->n_lights;
     WorkArgs wa{};
     wa.blocks = sl->d_blocks;
+    wa.sij = sl->d_sij;
     wa.nblocks = sl->nblocks;
+    wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
     const uint64_t hit_slots = (uint64_t)kQShards * wa.hit_cap;
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
+    if (sl->rdy_cap < hit_slots / 64) {  // new ready tags must not match any frame tag
+        if ((r = dev_grow(sl->rdy, sl->rdy_cap, hit_slots / 64)) != MIRT_OK) return r;
+        HIP_TRY(hipMemsetAsync(sl->rdy, 0, sl->rdy_cap * sizeof(uint32_t), s));
+    }
+    if (++sl->frame_tag == 0) {  // tags wrap after 2^32 frames: clear the ready tags
+        sl->frame_tag = 1;
+        HIP_TRY(hipMemsetAsync(sl->rdy, 0, sl->rdy_cap * sizeof(uint32_t), s));
+    }
+    wa.rdy = sl->rdy;
+    wa.frame_tag = sl->frame_tag;
     wa.hits = sl->hits;
     wa.litw = sl->litw;
     wa.blkdone = sl->blkdone;
@@ -385,9 +436,9 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    if (c->flags & MIRT_OPT_FUSED_FRAME) {
-        // one fused launch per frame (k_frame); profile times land in the primary slot
-        HIP_TRY(launch_frame(fa, wa, out, pgrid, c->flags, s));
+    if (c->flags & MIRT_OPT_ONE_KERNEL) {
+        // one launch per frame (k_trace); its time lands in the primary slot of the profile
+        HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
         if (prof) {
             HIP_TRY(hipEventRecord(pr.ev[1], s));
             HIP_TRY(hipEventRecord(pr.ev[2], s));
@@ -462,9 +513,12 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->hits) (void)hipFree(s->hits);
         if (s->litw) (void)hipFree(s->litw);
         if (s->blkdone) (void)hipFree(s->blkdone);
+        if (s->rdy) (void)hipFree(s->rdy);
         if (s->counters) (void)hipFree(s->counters);
         if (s->d_tiles) (void)hipFree(s->d_tiles);
         if (s->d_blocks) (void)hipFree(s->d_blocks);
+        if (s->d_sij) (void)hipFree(s->d_sij);
+        if (s->h_sij) (void)hipHostFree(s->h_sij);
         if (s->h_blocks) (void)hipHostFree(s->h_blocks);
         if (s->h_tiles) (void)hipHostFree(s->h_tiles);
         if (s->summary) (void)hipFree(s->summary);

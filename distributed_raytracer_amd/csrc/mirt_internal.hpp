@@ -91,13 +91,13 @@ struct TileDesc {
 };
 
 // One 8x8 pixel block of one tile: the primary kernel's work item.  Built on the host
-// per tile list (cached while the list does not change), so a wave finds its pixels with
-// one scalar load instead of a search over the tile list.
-struct alignas(32) BlockDesc {
-    uint64_t out;          // packed index of the block's (0, 0) pixel
-    uint32_t px, py;       // screen pixel of (0, 0)
-    uint32_t th;           // height of the tile (column stride of the packed tile)
-    uint32_t vw, vh;       // valid columns / rows (<= 8)
+// per tile list (cached while the list does not change) and stored shard-major (entry
+// q * per_shard + k describes block k * kQShards + q), so the consecutive tickets of a
+// shard read consecutive 16-byte entries with one scalar load each.
+struct alignas(16) BlockDesc {
+    uint32_t out;          // packed index of the block's (0, 0) pixel
+    uint32_t pxy;          // screen pixel of (0, 0): px | py << 16
+    uint32_t geo;          // tile height (packed column stride) | vw << 16 | vh << 24
     uint32_t pad;
 };
 
@@ -143,20 +143,29 @@ enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kS
 __host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_hits(int s) { return (2 * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_stat(int k, int s) { return (3 * kQShards + k * kStatShards + s) * kLine; }
-// done(s), s < kStatShards: workgroups of k_frame finished per shard; done(kStatShards):
-// shards finished (two levels keep every same-address atomic count <= 64).
+// done(s), s < kStatShards: workgroups of the frame's last kernel finished per shard;
+// done(kStatShards): shards finished (two levels keep every same-address count <= 64).
+// pdone(q): primary blocks of shard q finished (k_trace).
 __host__ __device__ constexpr int cnt_done(int s) { return (3 * kQShards + kStatN * kStatShards + s) * kLine; }
-constexpr int kCntN = (3 * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
+__host__ __device__ constexpr int cnt_pdone(int q) {
+    return (3 * kQShards + kStatN * kStatShards + kStatShards + 1 + q) * kLine;
+}
+constexpr int kCntN = (4 * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
 typedef unsigned long long cnt_t;
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
 struct WorkArgs {
     const BlockDesc* blocks;
+    const double* sij;     // tracer.go:19-20 per column (W values) then per row (H values)
     uint32_t nblocks;
+    uint32_t per_shard;    // BlockDesc entries per shard (ceil(nblocks / kQShards))
     uint32_t hit_cap;      // records per hit region (multiple of 64)
     HitRec* hits;          // kQShards regions of hit_cap records
     uint32_t* litw;        // per hit slot: bit l = light l reaches the hit (atomicOr by k_shadow)
     uint32_t* blkdone;     // per 64-slot hit block: lights finished (the last one shades the block)
+    uint32_t* rdy;         // per 64-slot hit block: frame_tag once its slots are written (k_trace)
+    uint32_t frame_tag;    // non-zero, different from the previous frame's on this slot
+    uint32_t pad2;
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
@@ -183,7 +192,7 @@ hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                          hipStream_t s);
-hipError_t launch_frame(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                         hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);

@@ -121,9 +121,9 @@ typedef struct {
     uint64_t shadow_rays;
     uint64_t hits;
     uint64_t tri_tests;     /* ray-triangle tests performed (brute force: rays * tris) */
-    double ms_primary;      /* raygen + nearest-hit kernel (MIRT_OPT_FUSED_FRAME: the whole frame) */
-    double ms_shadow;       /* shadow-ray + Phong kernel */
-    double ms_shade;        /* separate shading kernel if any (0 when shading is folded in) */
+    double ms_primary;      /* the primary kernel (MIRT_OPT_ONE_KERNEL: the whole frame) */
+    double ms_shadow;       /* the shadow + Phong kernel (MIRT_OPT_ONE_KERNEL: 0) */
+    double ms_shade;        /* reserved (0) */
     double ms_total;        /* first kernel start -> last kernel end */
 } mirt_stats;
 
@@ -209,7 +209,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split instead of the dynamic work queues */
 #define MIRT_OPT_TIMELINE 8u        /* record per-wave start/end stamps (mirt_debug_timeline) */
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
-#define MIRT_OPT_FUSED_FRAME 32u    /* one fused kernel per frame (primary + shadow + shade per 8x8 block) */
+#define MIRT_OPT_ONE_KERNEL 32u     /* one k_trace launch per frame (default: primary, then shadow+shade) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*
@@ -227,7 +227,7 @@ int mirt_debug_fp64(mirt_ctx *ctx, int op, uint32_t n, const double *a, const do
  *   [0] kernel (0 primary, 1 shadow)  [1] global wave id
  *   [2] s_memrealtime at wave start   [3] at wave end (100 MHz constant clock)
  *   [4] s_memtime at wave start       [5] at wave end (shader clock)
- *   [6] HW_ID register                [7] XCC id | work items taken << 32
+ *   [6] s_memrealtime after the LDS mesh staging   [7] XCC id | work items taken << 32
  */
 int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 

@@ -22,5 +22,9 @@ echo "write pass ok"
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
   --output-format csv -d "$OUT/pmc_sq" -o run -- python3 $BENCH > "$OUT/pmc_sq.log" 2>&1 || { echo "sq pass failed rc=$?"; exit 1; }
 echo "sq pass ok"
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 \
+  SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_SALU \
+  --output-format csv -d "$OUT/pmc_f64" -o run -- python3 $BENCH > "$OUT/pmc_f64.log" 2>&1 || { echo "f64 pass failed rc=$?"; exit 1; }
+echo "f64 pass ok"
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 echo done

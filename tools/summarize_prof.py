@@ -50,7 +50,7 @@ def main():
                                   "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
-    for p in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_f64"):
         f = os.path.join(src, p, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -70,7 +70,9 @@ def main():
             e["fetch_kib"] = c["FETCH_SIZE"]
             e["write_kib"] = c["WRITE_SIZE"]
             e["hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
-        for n in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
+        for n in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                  "SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                  "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_INT32", "SQ_INSTS_SALU"):
             if n in c:
                 e[n] = c[n]
         if "GRBM_GUI_ACTIVE" in c and dur.get(k):
@@ -82,6 +84,8 @@ def main():
         json.dump({"tag": a.tag, "width": a.width, "height": a.height, "gpus": a.gpus,
                    "k_primary_hbm_bytes_per_launch": kp["hbm_bytes_per_launch"],
                    "k_primary_avg_ns": kp["avg_ns"],
+                   "k_primary_fp64_flops_per_launch": kp.get("SQ_INSTS_VALU_FLOPS_FP64"),
+                   "k_primary_valu_insts_per_launch": kp.get("SQ_INSTS_VALU"),
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; (2*FETCH+WRITE)*1024"},
                   open(os.path.join(dst, f"{a.tag}_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
