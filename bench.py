@@ -218,11 +218,11 @@ def main():
                                  "VALU, see DESIGN.md"},
             "roofline_fp64_valu": None if fp64_flops is None else {
                 "bound": "fp64-valu", "kernel": "k_primary", "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFLOPS,
-                "achieved": round(fp64_flops / (prim_ms / 1e3) / 1e12, 3),
-                "frac": round(fp64_flops / (prim_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
-                "flops_per_launch": fp64_flops,
-                "note": "SQ_INSTS_VALU_FLOPS_FP64 per launch from the committed rocprofv3 pass (profiles/), over "
-                        "this run's k_primary HIP-event time"},
+                "achieved": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12, 3),
+                "frac": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
+                "flops_per_launch": int(64 * fp64_flops),
+                "note": "SQ_INSTS_VALU_FLOPS_FP64 (counts per wave instruction, FMA = 2) x 64 lanes per launch, "
+                        "from the committed rocprofv3 pass (profiles/), over this run's k_primary HIP-event time"},
         }
         if not a.no_parity:
             fr = sh.frame
