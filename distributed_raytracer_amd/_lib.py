@@ -51,7 +51,8 @@ class Camera(C.Structure):
 
 class Frame(C.Structure):
     _fields_ = [("objects", C.POINTER(Object)), ("n_objects", C.c_uint32),
-                ("lights", C.POINTER(Light)), ("n_lights", C.c_uint32), ("camera", Camera)]
+                ("lights", C.POINTER(Light)), ("n_lights", C.c_uint32), ("camera", Camera),
+                ("max_bounces", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class Tile(C.Structure):
@@ -66,7 +67,7 @@ class Outputs(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("ms_primary", C.c_double), ("ms_shadow", C.c_double),
-                ("ms_shade", C.c_double), ("ms_total", C.c_double)]
+                ("ms_shade", C.c_double), ("ms_total", C.c_double), ("reflection_rays", C.c_uint64)]
 
 
 class Profile(C.Structure):
@@ -76,7 +77,7 @@ class Profile(C.Structure):
                 ("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
                 ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64),
-                ("stack_overflows", C.c_uint64)]
+                ("stack_overflows", C.c_uint64), ("reflection_rays", C.c_uint64), ("reflect_ms_sum", C.c_double)]
 
 
 class MeshView(C.Structure):

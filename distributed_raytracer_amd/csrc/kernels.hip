@@ -251,7 +251,7 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], in
         cnt_t sum = 0;
         for (int k = 0; k < kWG / 64; ++k) sum += red[k][threadIdx.x];
         const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes
-                       : threadIdx.x == 2 ? stat_leaves : stat_hits;
+                       : threadIdx.x == 2 ? stat_leaves : stat_hits;  // < 0: not recorded
         if (sum && stat >= 0) {
             const cnt_t old = atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
             asm volatile("" ::"v"(old));
@@ -763,7 +763,11 @@ __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& 
     cnt_t sum = 0;
     for (int sh = 0; sh < kStatShards; ++sh)
         sum += atomicAdd(&wa.counters[cnt_stat(st == kStatShadowRays ? kStatHits : st, sh)], (cnt_t)0);
-    if (st == kStatShadowRays) sum *= fa.n_lights;
+    if (st == kStatShadowRays) {  // one per light per primary hit, plus those of reflection hits
+        sum *= fa.n_lights;
+        for (int sh = 0; sh < kStatShards; ++sh)
+            sum += atomicAdd(&wa.counters[cnt_stat(kStatReflShadowRays, sh)], (cnt_t)0);
+    }
     wa.summary[st] = sum;
     if (wa.prof_acc && sum) atomicAdd(&wa.prof_acc[st], sum);
 }
@@ -935,6 +939,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         st64<COH>(w + 5, dbits(nh.normal.z));
         st64<COH>(w + 6, oidx);
         st64<COH>(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
+        if (wa.bounces) vstore(wa.dir0 + 3 * slot, d);  // the reflect kernel's incoming D
     } else {
         st64<COH>(w + 7, (uint64_t)kNoHit);
     }
@@ -1003,6 +1008,12 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     const uint64_t oidx = ld64<COH>(w + 6);
     const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
     const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+    if (wa.bounces) {  // the reflect kernel combines the levels and writes the pixel
+        wa.ph0[3 * slot] = col.r;
+        wa.ph0[3 * slot + 1] = col.g;
+        wa.ph0[3 * slot + 2] = col.b;
+        return;
+    }
     if (out.rgb) {
         out.rgb[3 * oidx] = col.r;
         out.rgb[3 * oidx + 1] = col.g;
@@ -1121,7 +1132,7 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
-    frame_fold(fa, wa);
+    if (!wa.bounces) frame_fold(fa, wa);  // otherwise k_reflect is the frame's last kernel
 }
 
 // ---------------------------------------------------------------- one-launch frame
@@ -1220,6 +1231,125 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     __syncthreads();
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
     if (wa.timeline) clock.record(wa, 0, taken);
+    frame_fold(fa, wa);
+}
+
+// ---------------------------------------------------------------- reflections (configs[4])
+// EXTENSION, not in the reference (oracle: rt_oracle.c shade_reflect).
+// Work item: the 64 slots of one hit block.  Each lane follows its own bounce chain:
+// R = D - 2 (D.N) N, nearest hit of trace(hit + R 1e-4, R), phong there with shadow
+// rays; then the levels are combined innermost first, c_k = c_add(ph_k, c_mul(Ks_k,
+// c_(k+1))), a miss contributing black, the deepest level (k = bounces) plain phong.
+// Level 0's phong comes from the shadow kernel (WorkArgs::ph0).
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    __shared__ cnt_t red[kWG / 64][4];
+    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    if (RESIDENT) {
+        stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const ShardCursor sc;
+    WaveStats ws{0, 0, 0, 0, 0};
+    cnt_t refl_rays = 0, refl_shadow = 0;
+    const uint32_t B = min(wa.bounces, (uint32_t)MIRT_MAX_BOUNCES);
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+        const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
+        cnt_t* qc = &wa.counters[cnt_queue(2, q)];
+        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        while (k < nch) {
+            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
+            const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
+            const HitRec rec = wa.hits[slot];
+            const bool active = rec.obj != kNoHit;
+            RGB ph[MIRT_MAX_BOUNCES + 1], ks[MIRT_MAX_BOUNCES + 1];
+            V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
+            uint32_t levels = 0;   // levels with a phong value
+            bool missed = false;   // the chain ended on a miss (else on the depth limit)
+            if (active) {
+                D = vload(wa.dir0 + 3 * slot);
+                hit = vload(rec.h);
+                N = vload(rec.n);
+                ph[0] = RGB{wa.ph0[3 * slot], wa.ph0[3 * slot + 1], wa.ph0[3 * slot + 2]};
+                const double* mt = fa.obj[rec.obj].m.mats + (size_t)rec.mat * 10;
+                ks[0] = RGB{mt[6], mt[7], mt[8]};
+                levels = 1;
+            }
+            bool on = active;
+            for (uint32_t lv = 1; lv <= B; ++lv) {
+                if (__ballot(on) == 0) break;
+                const V3 R = sub(D, scale(N, 2 * dot(D, N)));
+                const V3 o = add(hit, scale(R, 0.0001));
+                Visits vis{0, 0, 0, 0};
+                const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, on, true, vis);
+                refl_rays += __popcll(__ballot(on));
+                ws.tests += (cnt_t)vis.tests * __popcll(__ballot(on));
+                ws.nodes += vis.nodes;
+                ws.leaves += vis.leaves;
+                ws.overflow += vis.overflow;
+                if (on && !r.ok) {
+                    missed = true;
+                    on = false;
+                }
+                uint32_t lit = 0;
+                refl_shadow += (cnt_t)__popcll(__ballot(on)) * fa.n_lights;
+                for (uint32_t l = 0; l < fa.n_lights; ++l) {  // tracer.go:60-64 at the reflected hit
+                    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+                    V3 so{0, 0, 0}, sd{1, 0, 0};
+                    if (on) {
+                        sd = norm(sub(lpos, r.hit));
+                        so = add(r.hit, scale(sd, 0.0001));
+                    }
+                    Visits sv{0, 0, 0, 0};
+                    bool is_lit;
+                    if (segment) {
+                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, on, sv);
+                    } else {
+                        const Nearest sr = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, on, false, sv);
+                        is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
+                    }
+                    lit |= (uint32_t)is_lit << l;
+                    ws.tests += (cnt_t)sv.tests * __popcll(__ballot(on));
+                    ws.nodes += sv.nodes;
+                    ws.leaves += sv.leaves;
+                    ws.overflow += sv.overflow;
+                }
+                if (on) {
+                    const double* mt = fa.obj[r.obj].m.mats + (size_t)r.mat * 10;
+                    ph[lv] = phong(fa, mt, r.hit, r.normal, lit);
+                    ks[lv] = RGB{mt[6], mt[7], mt[8]};
+                    levels = lv + 1;
+                    D = R;
+                    hit = r.hit;
+                    N = r.normal;
+                }
+            }
+            if (active) {
+                const uint32_t L = levels - 1;
+                RGB c = ph[L];
+                if (missed) c = c_add(ph[L], c_mul(ks[L], RGB{0, 0, 0}));  // c_reflected = black
+                for (int lv = (int)L - 1; lv >= 0; --lv) c = c_add(ph[lv], c_mul(ks[lv], c));
+                if (out.rgb) {
+                    out.rgb[3 * rec.out] = c.r;
+                    out.rgb[3 * rec.out + 1] = c.g;
+                    out.rgb[3 * rec.out + 2] = c.b;
+                }
+                if (out.rgb8) {
+                    out.rgb8[3 * rec.out] = c_u8(c.r);
+                    out.rgb8[3 * rec.out + 1] = c_u8(c.g);
+                    out.rgb8[3 * rec.out + 2] = c_u8(c.b);
+                }
+            }
+            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+        }
+    }
+    // reflection rays and their shadow rays as two extra statistics (per workgroup)
+    WaveStats extra{refl_rays, refl_shadow, 0, 0, 0};
+    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
+    __syncthreads();
+    stats_flush(wa.counters, red, kStatReflRays, kStatReflShadowRays, -1, -1, extra);
     frame_fold(fa, wa);
 }
 
@@ -1346,6 +1476,15 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 #define K_RAYS(P, B, R) hipLaunchKernelGGL((k_rays<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, io)
     MIRT_DISPATCH(K_RAYS);
 #undef K_RAYS
+    return hipGetLastError();
+}
+
+hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                          hipStream_t s) {
+    const bool resident = is_resident(fa);
+#define K_REFLECT(P, B, R) hipLaunchKernelGGL((k_reflect<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    MIRT_DISPATCH(K_REFLECT);
+#undef K_REFLECT
     return hipGetLastError();
 }
 

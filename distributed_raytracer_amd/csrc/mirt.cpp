@@ -66,6 +66,10 @@ struct Slot {
     size_t blkdone_cap = 0;
     uint32_t* rdy = nullptr;
     size_t rdy_cap = 0;
+    double* dir0 = nullptr;   // configs[4] reflections: primary direction per hit slot
+    size_t dir0_cap = 0;
+    double* ph0 = nullptr;    // configs[4] reflections: phong of the primary hit per slot
+    size_t ph0_cap = 0;
     uint32_t frame_tag = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
@@ -218,6 +222,8 @@ int check_frame(const mirt_ctx* c, const mirt_frame* f) {
         return fail(MIRT_E_LIMIT, "n_lights > MIRT_MAX_LIGHTS (" + std::to_string(MIRT_MAX_LIGHTS) + ")");
     if (f->n_objects && !f->objects) return fail(MIRT_E_INVALID, "objects is NULL");
     if (f->n_lights && !f->lights) return fail(MIRT_E_INVALID, "lights is NULL");
+    if (f->max_bounces > MIRT_MAX_BOUNCES)
+        return fail(MIRT_E_LIMIT, "max_bounces > MIRT_MAX_BOUNCES (" + std::to_string(MIRT_MAX_BOUNCES) + ")");
     for (uint32_t i = 0; i < f->n_objects; ++i) {
         uint32_t id = f->objects[i].mesh_id;
         if (id >= c->meshes.size() || !c->meshes[id].live)
@@ -400,6 +406,13 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     }
     wa.rdy = sl->rdy;
     wa.frame_tag = sl->frame_tag;
+    wa.bounces = f->max_bounces;
+    if (wa.bounces) {
+        if ((r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
+        if ((r = dev_grow(sl->ph0, sl->ph0_cap, 3 * hit_slots)) != MIRT_OK) return r;
+        wa.dir0 = sl->dir0;
+        wa.ph0 = sl->ph0;
+    }
     wa.hits = sl->hits;
     wa.litw = sl->litw;
     wa.blkdone = sl->blkdone;
@@ -436,7 +449,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    if (c->flags & MIRT_OPT_ONE_KERNEL) {
+    if ((c->flags & MIRT_OPT_ONE_KERNEL) && !wa.bounces) {
         // one launch per frame (k_trace); its time lands in the primary slot of the profile
         HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
         if (prof) {
@@ -451,6 +464,10 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         // launched with no lights, to shade every hit with the ambient term
         HIP_TRY(launch_shadow(fa, wa, out, sgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
+        if (wa.bounces) {  // configs[4] extension: the frame's last kernel
+            if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+            HIP_TRY(launch_reflect(fa, wa, out, sgrid, c->flags, s));
+        }
     }
     sl->dirty = false;
     if (prof) {
@@ -475,6 +492,7 @@ int fill_stats(Slot* sl, hipStream_t s, uint64_t pixels, uint64_t tris, uint32_t
     st->hits = sl->h_summary[kStatHits];
     st->shadow_rays = sl->h_summary[kStatShadowRays];
     st->tri_tests = sl->h_summary[kStatPrimTests] + sl->h_summary[kStatShadowTests];
+    st->reflection_rays = sl->h_summary[kStatReflRays];
     return MIRT_OK;
 }
 
@@ -514,6 +532,8 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->litw) (void)hipFree(s->litw);
         if (s->blkdone) (void)hipFree(s->blkdone);
         if (s->rdy) (void)hipFree(s->rdy);
+        if (s->dir0) (void)hipFree(s->dir0);
+        if (s->ph0) (void)hipFree(s->ph0);
         if (s->counters) (void)hipFree(s->counters);
         if (s->d_tiles) (void)hipFree(s->d_tiles);
         if (s->d_blocks) (void)hipFree(s->d_blocks);
@@ -873,7 +893,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->launches++;
         out->primary_ms_sum += a;
         out->shadow_ms_sum += b;
-        out->shade_ms_sum += d;
+        out->reflect_ms_sum += d;
         out->frame_ms_sum += t;
         out->primary_rays += r.pixels;
     }
@@ -890,6 +910,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->shadow_node_visits = acc[kStatShadowNodes];
         out->shadow_leaf_visits = acc[kStatShadowLeaves];
         out->stack_overflows = acc[kStatOverflow];
+        out->reflection_rays = acc[kStatReflRays];
     }
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);

@@ -122,7 +122,7 @@ struct HitRec {
 // Counters kept in device memory per call slot, zeroed before every frame.  Each counter
 // owns a 128-byte line: same-line atomics serialise (~90 per microsecond on MI355X), so
 // every contended counter is split kQShards ways.
-//   queue(q, s): work-queue tickets of kernel q (0 primary, 1 shadow) for shard s.
+//   queue(q, s): work-queue tickets of kernel q (0 primary, 1 shadow, 2 reflect) for shard s.
 //     Primary block b belongs to shard b % kQShards; a wave serves the shard
 //     (global wave id % kQShards) and takes one block per ticket.
 //   hits(s):     hit slots of shard s.  A block with at least one hit takes 64 slots of
@@ -139,18 +139,23 @@ struct HitRec {
 // accumulator) once the producing kernels are done.
 constexpr int kQShards = 64, kStatShards = 8, kLine = 16;
 enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kStatShadowNodes,
-       kStatShadowLeaves, kStatHits, kStatOverflow, kStatShadowRays, kStatN };
+       kStatShadowLeaves, kStatHits, kStatOverflow, kStatShadowRays, kStatReflRays, kStatReflShadowRays, kStatN };
+constexpr int kQueues = 3;
 __host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
-__host__ __device__ constexpr int cnt_hits(int s) { return (2 * kQShards + s) * kLine; }
-__host__ __device__ constexpr int cnt_stat(int k, int s) { return (3 * kQShards + k * kStatShards + s) * kLine; }
+__host__ __device__ constexpr int cnt_hits(int s) { return (kQueues * kQShards + s) * kLine; }
+__host__ __device__ constexpr int cnt_stat(int k, int s) {
+    return ((kQueues + 1) * kQShards + k * kStatShards + s) * kLine;
+}
 // done(s), s < kStatShards: workgroups of the frame's last kernel finished per shard;
 // done(kStatShards): shards finished (two levels keep every same-address count <= 64).
 // pdone(q): primary blocks of shard q finished (k_trace).
-__host__ __device__ constexpr int cnt_done(int s) { return (3 * kQShards + kStatN * kStatShards + s) * kLine; }
-__host__ __device__ constexpr int cnt_pdone(int q) {
-    return (3 * kQShards + kStatN * kStatShards + kStatShards + 1 + q) * kLine;
+__host__ __device__ constexpr int cnt_done(int s) {
+    return ((kQueues + 1) * kQShards + kStatN * kStatShards + s) * kLine;
 }
-constexpr int kCntN = (4 * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
+__host__ __device__ constexpr int cnt_pdone(int q) {
+    return ((kQueues + 1) * kQShards + kStatN * kStatShards + kStatShards + 1 + q) * kLine;
+}
+constexpr int kCntN = ((kQueues + 2) * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
 typedef unsigned long long cnt_t;
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
@@ -165,7 +170,9 @@ struct WorkArgs {
     uint32_t* blkdone;     // per 64-slot hit block: lights finished (the last one shades the block)
     uint32_t* rdy;         // per 64-slot hit block: frame_tag once its slots are written (k_trace)
     uint32_t frame_tag;    // non-zero, different from the previous frame's on this slot
-    uint32_t pad2;
+    uint32_t bounces;      // configs[4] reflection extension (mirt_frame.max_bounces), 0 = off
+    double* dir0;          // bounces: per hit slot, the primary ray direction (3 doubles)
+    double* ph0;           // bounces: per hit slot, phong of the primary hit (3 doubles)
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
@@ -195,6 +202,8 @@ hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlane
 hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                         hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
+hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+                          hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);

@@ -172,6 +172,7 @@ class EnvMutables:
     objects: List[SceneObject] = field(default_factory=list)
     lights: List[Light] = field(default_factory=list)
     cam: Optional[Camera] = None
+    max_bounces: int = 0  # configs[4] reflection EXTENSION (mirt.h); 0 = the reference
 
     def to_frame(self) -> Tuple[L.Frame, list]:
         """C mirt_frame; the second value keeps the arrays alive for the call."""
@@ -183,7 +184,7 @@ class EnvMutables:
         lts = (L.Light * max(1, len(self.lights)))()
         for i, lt in enumerate(self.lights):
             lts[i] = L.Light(_d3(lt.pos), _d3(lt.col))
-        fr = L.Frame(objs, len(self.objects), lts, len(self.lights), self.cam.to_c())
+        fr = L.Frame(objs, len(self.objects), lts, len(self.lights), self.cam.to_c(), int(self.max_bounces), 0)
         return fr, [objs, lts]
 
 

@@ -46,6 +46,7 @@ extern "C" {
 
 #define MIRT_MAX_OBJECTS 16
 #define MIRT_MAX_LIGHTS 16
+#define MIRT_MAX_BOUNCES 8
 
 typedef struct mirt_ctx mirt_ctx;
 
@@ -90,6 +91,11 @@ typedef struct {
     const mirt_light *lights;
     uint32_t n_lights;
     mirt_camera camera;
+    /* configs[4] EXTENSION (not in the reference): reflection bounces per primary hit,
+     * 0..MIRT_MAX_BOUNCES.  0 = the reference's Trace.  Semantics in DESIGN.md §4.6:
+     * c = c_add(phong, c_mul(Ks, c_reflected)), R = D - 2(D.N)N, origin hit + R*1e-4. */
+    uint32_t max_bounces;
+    uint32_t reserved;
 } mirt_frame;
 
 /* shared/comms/comms.proto:25-31 WorkOrder geometry */
@@ -125,6 +131,7 @@ typedef struct {
     double ms_shadow;       /* the shadow + Phong kernel (MIRT_OPT_ONE_KERNEL: 0) */
     double ms_shade;        /* reserved (0) */
     double ms_total;        /* first kernel start -> last kernel end */
+    uint64_t reflection_rays; /* configs[4] extension (mirt_frame.max_bounces) */
 } mirt_stats;
 
 /* Accumulated per-kernel device times while profiling is enabled (HIP events). */
@@ -137,6 +144,9 @@ typedef struct {
     uint64_t primary_node_visits, primary_leaf_visits, shadow_node_visits, shadow_leaf_visits;
     /* traversal stack overflows (provably impossible; a non-zero value is a library bug) */
     uint64_t stack_overflows;
+    /* configs[4] extension: reflection rays traced and the reflect kernel's device time */
+    uint64_t reflection_rays;
+    double reflect_ms_sum;
 } mirt_profile;
 
 int mirt_abi_version(void);

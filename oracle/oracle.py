@@ -46,7 +46,7 @@ class OrTile(C.Structure):
 
 class OrStats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("box_tests", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("box_tests", C.c_uint64), ("reflection_rays", C.c_uint64)]
 
 
 def build() -> str:
@@ -65,6 +65,7 @@ def lib():
         L.or_build.restype = C.c_void_p
         L.or_build.argtypes = [C.POINTER(OrScene), C.c_int]
         L.or_free.argtypes = [C.c_void_p]
+        L.or_set_bounces.argtypes = [C.c_void_p, C.c_int]
         L.or_camera_ok.argtypes = [C.c_void_p]
         L.or_trace_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(OrTile), C.c_uint32, C.c_int,
                                      C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -122,6 +123,10 @@ class Oracle:
             self.close()
         except Exception:
             pass
+
+    def set_bounces(self, bounces: int) -> None:
+        """configs[4] reflection extension (rt_oracle.c shade_reflect); 0 = the reference."""
+        lib().or_set_bounces(self._ctx, int(bounces))
 
     def trace_tiles(self, W: int, H: int, tiles, nthreads: int = 1, shade: bool = True):
         """Returns dict(valid, rgb, rgb8, face, obj, stats) with outputs packed per tile,

@@ -222,6 +222,7 @@ typedef struct {
 typedef struct { uint32_t x, y, w, h; } or_tile;
 typedef struct {
     uint64_t primary_rays, shadow_rays, hits, tri_tests, box_tests;
+    uint64_t reflection_rays;  /* configs[4] extension (or_set_bounces) */
 } or_stats;
 
 /* ------------------------------------------------------------- R-tree (rtreego) */
@@ -404,6 +405,7 @@ typedef struct {
     vec3 cam_pos, cam_fwd, cam_left, cam_up;
     double fov;
     int cam_ok;
+    int bounces;          /* configs[4] reflection extension: 0 = the reference */
 } or_ctx;
 
 /* camera.go:35-44 NewCamera (GlobalUp = (0,1,0), environment.go:22) */
@@ -672,20 +674,47 @@ static vec3 pixel_to_point(const or_ctx *c, int i, int j, int width, int height)
     return v_add(v_add(v_add(c->cam_pos, c->cam_fwd), ioff), joff);
 }
 
+/*
+ * configs[4] reflection extension (NOT in the reference; BASELINE.json / SURVEY.md §8(d)
+ * define it by the build):  at a hit reached along direction D,
+ *   c = c_add(phong(hit), c_mul(Ks, c_reflected)),
+ *   c_reflected = the same rule at the nearest hit of trace(hit + R 1e-4, R) (black on a
+ *   miss), R = D - 2 (D.N) N computed as sub(D, scale(N, 2 dot(D, N))), not normalised;
+ * recursion stops after `bounces` reflections (the deepest level is plain phong).  trace
+ * and phong are the reference's (tracer.go:27-77), camera-distance object choice included.
+ */
+static rgb shade_reflect(const or_ctx *c, const hitrec *h, vec3 d_in, int depth, scratch *sc, uint64_t *shadow_rays,
+                         uint64_t *refl_rays) {
+    rgb ph = phong(c, h, sc, shadow_rays);
+    if (depth >= c->bounces) return ph;
+    vec3 R = v_sub(d_in, v_scale(h->normal, 2 * v_dot(d_in, h->normal)));
+    (*refl_rays)++;
+    hitrec h2 = trace(c, v_add(h->hit, v_scale(R, 0.0001)), R, sc);
+    rgb cr = {0, 0, 0};
+    if (h2.ok) cr = shade_reflect(c, &h2, R, depth + 1, sc, shadow_rays, refl_rays);
+    const double *mt = &c->meshes[c->s.objects[h->obj].mesh].m->materials[10 * h->mat];
+    rgb ks = {mt[6], mt[7], mt[8]};
+    return c_add(ph, c_mul(ks, cr));
+}
+
 /* tracer.go:81-91 Trace */
 typedef struct { int valid; rgb c; uint32_t face, obj; } pixel_out;
-static pixel_out trace_pixel(const or_ctx *c, int i, int j, int W, int H, scratch *sc, uint64_t *shadow_rays) {
+static pixel_out trace_pixel(const or_ctx *c, int i, int j, int W, int H, scratch *sc, uint64_t *shadow_rays,
+                             uint64_t *refl_rays) {
     pixel_out p; memset(&p, 0, sizeof(p));
     vec3 sp = pixel_to_point(c, i, j, W, H);
-    hitrec h = trace(c, c->cam_pos, v_norm(v_sub(sp, c->cam_pos)), sc);
+    vec3 d = v_norm(v_sub(sp, c->cam_pos));
+    hitrec h = trace(c, c->cam_pos, d, sc);
     if (h.ok) {
         p.valid = 1;
-        p.c = phong(c, &h, sc, shadow_rays);
+        p.c = c->bounces > 0 ? shade_reflect(c, &h, d, 0, sc, shadow_rays, refl_rays) : phong(c, &h, sc, shadow_rays);
         p.face = h.face;
         p.obj = h.obj;
     }
     return p;
 }
+
+void or_set_bounces(or_ctx *c, int bounces) { c->bounces = bounces < 0 ? 0 : bounces; }
 
 /* --------------------------------------------------------- tile driver */
 typedef struct {
@@ -695,7 +724,7 @@ typedef struct {
     uint32_t W, H;
     int tid, nthreads, shade;
     uint8_t *valid; double *rgb; uint8_t *rgb8; int32_t *face; int32_t *obj;
-    uint64_t primary, shadow, hits, tri, box;
+    uint64_t primary, shadow, hits, tri, box, refl;
     uint32_t max_faces;
 } job;
 
@@ -703,7 +732,7 @@ static void *run_job(void *arg) {
     job *jb = (job *)arg;
     scratch sc; sc.tri_tests = 0; sc.box_tests = 0;
     sc.stack_face = (uint32_t *)malloc(sizeof(uint32_t) * (jb->max_faces + 1));
-    uint64_t shadow = 0;
+    uint64_t shadow = 0, refl = 0;
     for (uint32_t t = 0; t < jb->ntiles; t++) {
         const or_tile *tl = &jb->tiles[t];
         /* worker/distributed/main.go:67-89: i over width (outer), j over height (inner) */
@@ -713,7 +742,8 @@ static void *run_job(void *arg) {
                 pixel_out p;
                 jb->primary++;
                 if (jb->shade) {
-                    p = trace_pixel(jb->c, (int)(tl->x + i), (int)(tl->y + j), (int)jb->W, (int)jb->H, &sc, &shadow);
+                    p = trace_pixel(jb->c, (int)(tl->x + i), (int)(tl->y + j), (int)jb->W, (int)jb->H, &sc, &shadow,
+                                    &refl);
                 } else {
                     memset(&p, 0, sizeof(p));
                     vec3 sp = pixel_to_point(jb->c, (int)(tl->x + i), (int)(tl->y + j), (int)jb->W, (int)jb->H);
@@ -737,6 +767,7 @@ static void *run_job(void *arg) {
         }
     }
     jb->shadow = shadow;
+    jb->refl = refl;
     jb->tri = sc.tri_tests;
     jb->box = sc.box_tests;
     free(sc.stack_face);
@@ -777,6 +808,7 @@ int or_trace_tiles(const or_ctx *c, uint32_t W, uint32_t H, const or_tile *tiles
         memset(st, 0, sizeof(*st));
         for (int t = 0; t < nthreads; t++) {
             st->primary_rays += jobs[t].primary; st->shadow_rays += jobs[t].shadow; st->hits += jobs[t].hits;
+            st->reflection_rays += jobs[t].refl;
             st->tri_tests += jobs[t].tri; st->box_tests += jobs[t].box;
         }
     }
