@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--scene", default=SCENE)
+    ap.add_argument("--bounces", type=int, default=0,
+                    help="configs[4] reflection EXTENSION: bounces per primary hit (0 = the reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
@@ -53,6 +55,18 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes of k_primary from a rocprofv3 --pmc pass (see profiles/)")
     return ap.parse_args()
+
+
+def workload_name(a, W: int, H: int, tris: int, nl: int) -> str:
+    """The BASELINE.json config this run measures (configs[1] by default)."""
+    model = "suzanne.obj" if os.path.abspath(a.scene) == os.path.abspath(SCENE) else os.path.basename(
+        os.path.dirname(os.path.abspath(a.scene))) + f" ({tris} tris)"
+    name = f"{model} {W}x{H}, primary + one shadow ray per light ({nl}) + Phong"
+    if a.bounces:
+        name += f" + {a.bounces}-bounce reflections (configs[4] extension)"
+    if model == "suzanne.obj" and W == 1920 and H == 1080 and not a.bounces:
+        name += " (BASELINE configs[1])"
+    return name
 
 
 def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
@@ -81,13 +95,16 @@ def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
     return out
 
 
-def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int) -> dict:
+def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int,
+                 bounces: int = 0) -> dict:
     """Parity gate of the timed frame: a 1/16 subsample — every 16th
     column — against the oracle, valid mask and rgb8 bit-exact."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
     cols = list(range(5, W, 16))
-    ref = Oracle(load_scene(scene_path)).trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=HOST_CORES)
+    orc = Oracle(load_scene(scene_path), use_rtree=True)
+    orc.set_bounces(bounces)
+    ref = orc.trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=HOST_CORES)
     sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
     ok = bool(np.array_equal(fb_valid[sub], ref["valid"]) and np.array_equal(fb_rgb8[sub], ref["rgb8"]))
     return {"columns_checked": len(cols), "bit_exact": ok, "hits": int(fb_valid.sum())}
@@ -118,7 +135,8 @@ def main():
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_ONE_KERNEL if a.one_kernel else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
-    frame = env.mutable().to_frame()
+    import dataclasses
+    frame = dataclasses.replace(env.mutable(), max_bounces=a.bounces).to_frame()
     tris = sum(len(m.face_v) for m in env.meshes)
     nl = len(env.mutable().lights)
     sh = FrameSharder(ctx, W, H, rank, world, a.tile)
@@ -152,22 +170,22 @@ def main():
 
     elapsed = t1 - t0
     pl = max(prof["launches"], 1)
-    counts = torch.tensor([elapsed, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl],
-                          dtype=torch.float64, device=dev)
+    counts = torch.tensor([elapsed, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
+                           prof["reflection_rays"] / pl], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = counts[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         sums = counts[1:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         elapsed = float(tmax.item())
-        primary, shadow, hits = (float(x) for x in sums.tolist())
+        primary, shadow, hits, refl = (float(x) for x in sums.tolist())
     else:
-        primary, shadow, hits = (float(x) for x in counts[1:].tolist())
+        primary, shadow, hits, refl = (float(x) for x in counts[1:].tolist())
 
     if rank == 0:
         steps = a.steps
         ms = elapsed / steps * 1e3
-        rays_per_frame = primary + shadow  # per frame, all ranks (device counters of the profiled pass)
+        rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
         launches = max(prof["launches"], 1)
         prim_ms = prof["primary_ms_sum"] / launches
         prim_tests = prof["primary_tri_tests"] / launches
@@ -194,8 +212,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), static frame-0 camera",
-            "config": {"workload": f"suzanne.obj {W}x{H}, primary + one shadow ray per light (3) + Phong "
-                                   f"(BASELINE configs[1])", "width": W, "height": H, "triangles": tris,
+            "config": {"workload": workload_name(a, W, H, tris, nl), "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
@@ -207,7 +224,7 @@ def main():
                 "primary_node_visits", "primary_leaf_visits", "shadow_node_visits", "shadow_leaf_visits")},
             "ms_kernels": {"primary": round(prim_ms, 4),
                            "shadow": round(prof["shadow_ms_sum"] / launches, 4),
-                           "shade": round(prof["shade_ms_sum"] / launches, 4),
+                           "reflect": round(prof["reflect_ms_sum"] / launches, 4),
                            "frame_device": round(prof["frame_ms_sum"] / launches, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -226,7 +243,7 @@ def main():
         }
         if not a.no_parity:
             fr = sh.frame
-            line["parity"] = parity_check(fr.valid.cpu().numpy(), fr.rgb8.cpu().numpy(), a.scene, W, H)
+            line["parity"] = parity_check(fr.valid.cpu().numpy(), fr.rgb8.cpu().numpy(), a.scene, W, H, a.bounces)
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.scene, W, H)
         print(json.dumps(line), flush=True)
