@@ -121,9 +121,16 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    # One process per GPU.  MIRT_DIST_BACKEND=gloo (rehearsal of the N>1 path on a box
+    # with fewer GPUs than ranks): ranks share GPUs and the gather stages through host.
+    backend = os.environ.get("MIRT_DIST_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd.framebuffer import FrameSharder
@@ -144,7 +151,7 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            dist.barrier(device_ids=[local]) if backend == "nccl" else dist.barrier()
 
     # One stream for every frame: frames are serialised on the GPU (no two frames in
     # flight writing the same framebuffer); the host still enqueues ahead of the GPU.
@@ -154,6 +161,7 @@ def main():
     with torch.cuda.stream(stream):
         for _ in range(a.warmup):
             sh.render(frame)
+        sh.flush()
         torch.cuda.synchronize(dev)
 
         ctx.profile_enable(True)
@@ -161,7 +169,8 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            sh.render(frame)
+            sh.render(frame)  # N > 1: frame k's gather overlaps frame k+1's tracing
+        sh.flush()            # the last frame's gather + unpack are inside the timed region
         torch.cuda.synchronize(dev)
         barrier()
         t1 = time.perf_counter()
@@ -171,7 +180,8 @@ def main():
     elapsed = t1 - t0
     pl = max(prof["launches"], 1)
     counts = torch.tensor([elapsed, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
-                           prof["reflection_rays"] / pl], dtype=torch.float64, device=dev)
+                           prof["reflection_rays"] / pl], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
     if world > 1:
         tmax = counts[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -248,7 +258,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(a.scene, W, H)
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
 
 

@@ -1398,6 +1398,7 @@ __global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ til
         }
         const TileDesc td = tiles[lo];
         const uint64_t local = p - td.out_off;
+        if (local >= (uint64_t)td.w * td.h) continue;  // padding between ranks' packed buffers
         const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
         const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
         if (src.valid && dst.valid) dst.valid[q] = src.valid[p];

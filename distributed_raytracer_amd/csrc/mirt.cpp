@@ -81,6 +81,8 @@ struct Slot {
     BlockDesc* h_blocks = nullptr;  // pinned staging
     size_t blocks_cap = 0, h_blocks_cap = 0;
     std::vector<mirt_tile> blocks_key;
+    std::vector<TileDesc> unpack_key;  // tile list of the last unpack (device copy in d_tiles)
+    uint32_t unpack_key_H = 0;
     uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0, per_shard = 0;
     // pixelToPoint per column / per row (tracer.go:19-20), cached per (fov, W, H)
     double* d_sij = nullptr;
@@ -786,8 +788,11 @@ int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, ui
     return MIRT_OK;
 }
 
-int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                            const mirt_outputs* packed, const mirt_outputs* fb, void* stream) {
+namespace {
+// Unpack with per-tile packed offsets (NULL: back to back).  The slot keeps its last
+// tile list on the device and skips the upload while the caller repeats it.
+int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, const uint64_t* offsets, uint32_t n,
+                const mirt_outputs* packed, const mirt_outputs* fb, void* stream) {
     if (!c || !tiles || !packed || !fb || n == 0) return fail(MIRT_E_INVALID, "NULL argument or empty tile list");
     HIP_TRY(hipSetDevice(c->device));
     Slot* sl = nullptr;
@@ -795,23 +800,46 @@ int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile
     if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     hipStream_t s = (hipStream_t)stream;  // NULL is the HIP null stream, as in the HIP API
+    const size_t cap_before = sl->tiles_cap;
     if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
-    uint64_t pixels = 0;
+    if (sl->tiles_cap != cap_before) sl->unpack_key.clear();  // reallocated: the device copy is gone
+    uint64_t pixels = 0, span = 0;
+    std::vector<TileDesc> td(n);
     for (uint32_t t = 0; t < n; ++t) {
         if ((uint64_t)tiles[t].x + tiles[t].w > W || (uint64_t)tiles[t].y + tiles[t].h > H || !tiles[t].w ||
             !tiles[t].h)
             return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty or exceeds the screen");
-        TileDesc& d = sl->h_tiles[t];
-        d = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, pixels, {0, 0}};
+        const uint64_t off = offsets ? offsets[t] : pixels;
+        if (off < span) return fail(MIRT_E_INVALID, "tile offsets must ascend without overlap");
+        td[t] = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, off, {0, 0}};
         pixels += (uint64_t)tiles[t].w * tiles[t].h;
+        span = off + (uint64_t)tiles[t].w * tiles[t].h;
     }
-    HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
+    if (sl->unpack_key_H != H || sl->unpack_key.size() != n ||
+        memcmp(sl->unpack_key.data(), td.data(), sizeof(TileDesc) * n) != 0) {
+        memcpy(sl->h_tiles, td.data(), sizeof(TileDesc) * n);
+        HIP_TRY(hipMemcpyAsync(sl->d_tiles, sl->h_tiles, sizeof(TileDesc) * n, hipMemcpyHostToDevice, s));
+        sl->unpack_key = td;
+        sl->unpack_key_H = H;
+    }
     OutPlanes src{packed->rgb, packed->rgb8, packed->valid, packed->face, packed->object};
     OutPlanes dst{fb->rgb, fb->rgb8, fb->valid, fb->face, fb->object};
-    HIP_TRY(launch_unpack(sl->d_tiles, n, pixels, H, src, dst, s));
+    HIP_TRY(launch_unpack(sl->d_tiles, n, span, H, src, dst, s));
     HIP_TRY(hipEventRecord(sl->done, s));
     sl->pending = true;
     return MIRT_OK;
+}
+}  // namespace
+
+int mirt_unpack_tiles_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
+                            const mirt_outputs* packed, const mirt_outputs* fb, void* stream) {
+    return unpack_impl(c, W, H, tiles, nullptr, n, packed, fb, stream);
+}
+
+int mirt_unpack_tiles_at_async(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, const uint64_t* offsets,
+                               uint32_t n, const mirt_outputs* packed, const mirt_outputs* fb, void* stream) {
+    if (!offsets) return fail(MIRT_E_INVALID, "offsets is NULL");
+    return unpack_impl(c, W, H, tiles, offsets, n, packed, fb, stream);
 }
 
 int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* orig, const double* dir, uint8_t* ok,

@@ -93,6 +93,12 @@ def gather_packed(buf, world: int, rank: int, root: int = 0, group=None):
     backend), gloo for CPU tensors (tests).  Returns the list on root, None elsewhere."""
     import torch
     import torch.distributed as dist
+    if buf.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device gather: stage through host memory (tests / 1-GPU rehearsals)
+        cpu = buf.cpu()
+        out = [torch.empty_like(cpu) for _ in range(world)] if rank == root else None
+        dist.gather(cpu, out, dst=root, group=group)
+        return [t.to(buf.device) for t in out] if out is not None else None
     out = [torch.empty_like(buf) for _ in range(world)] if rank == root else None
     dist.gather(buf, out, dst=root, group=group)
     return out
@@ -156,6 +162,12 @@ class FrameSharder:
 
     With world == 1 the frame is traced as ONE tile straight into the framebuffer
     (the worker/sequential draw), with no gather and no unpack.
+
+    With world > 1 frames are pipelined: frame k's gather (async on the collective's own
+    stream) overlaps frame k+1's tracing, so each rank keeps two packed buffers; frame k
+    is unpacked on the root once its gather is done, during render(k+1) or flush().
+    All ranks' tiles are unpacked by ONE launch (mirt_unpack_tiles_at_async with the
+    per-rank packed offsets).
     """
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: int = 64, root: int = 0,
@@ -171,12 +183,65 @@ class FrameSharder:
             self.tiles_all = plan_tiles(W, H, tile)
         self.mine = assign(self.tiles_all, world, rank)
         self.cap = packed_capacity(self.tiles_all, world)
+        self._pending = None  # (works, gathered buffers) of the frame whose gather is in flight
+        self._k = 0
         if world == 1:
             self.packed = None
             self.frame = alloc_planes(W * H, self.device, with_rgb)
         else:
-            self.packed = alloc_planes(self.cap, self.device, with_rgb)
+            self.bufs = [alloc_planes(self.cap, self.device, with_rgb) for _ in range(2)]
+            self.packed = self.bufs[0]
             self.frame = alloc_planes(W * H, self.device, with_rgb) if rank == root else None
+            if rank == root:
+                # every rank's tiles at its packed offset r * cap in the gathered buffer
+                tl, off = [], []
+                for r in range(world):
+                    o = r * self.cap
+                    for t in assign(self.tiles_all, world, r):
+                        tl.append(t)
+                        off.append(o)
+                        o += t[2] * t[3]
+                self._unpack_tiles = _tiles_c(tl)
+                self._unpack_offsets = (C.c_uint64 * len(off))(*off)
+                self._unpack_n = len(tl)
+                self.gathered = [torch.empty(world * self.cap * 4, dtype=torch.uint8, device=self.device)
+                                 for _ in range(2)]
+                self.gathered_rgb = ([torch.empty((world * self.cap, 3), dtype=torch.float64, device=self.device)
+                                      for _ in range(2)] if with_rgb else None)
+
+    def _gather(self, k: int):
+        """Issue the gather of packed buffer k % 2 to the root (async with RCCL)."""
+        import torch.distributed as dist
+        buf = self.bufs[k % 2]
+        works = []
+        pairs = [(buf.raw, self.gathered[k % 2] if self.rank == self.root else None)]
+        if self.with_rgb:
+            pairs.append((buf.rgb, self.gathered_rgb[k % 2] if self.rank == self.root else None))
+        for src, dst in pairs:
+            if src.is_cuda and dist.get_backend(self.group) == "gloo":
+                got = gather_packed(src, self.world, self.rank, self.root, self.group)  # synchronous staging
+                if dst is not None:
+                    for r, g in enumerate(got):
+                        dst.view(self.world, -1)[r].copy_(g.reshape(-1))
+                continue
+            outs = None
+            if dst is not None:
+                outs = [o.view(src.shape) for o in dst.view(self.world, -1).unbind(0)]
+            works.append(dist.gather(src, outs, dst=self.root, group=self.group, async_op=True))
+        return works
+
+    def _unpack(self, k: int, stream_ptr: int) -> None:
+        # rank r's gathered region is its packed raw buffer [rgb8 (3 cap) | valid (cap)]:
+        # make each plane contiguous over the ranks (two strided copies), then one launch
+        raw = self.gathered[k % 2].view(self.world, self.cap * 4)
+        self._rgb8_all = raw[:, : self.cap * 3].reshape(self.world * self.cap, 3)
+        self._valid_all = raw[:, self.cap * 3:].reshape(self.world * self.cap)
+        src = DevicePlanes(rgb8=self._rgb8_all, valid=self._valid_all,
+                           rgb=self.gathered_rgb[k % 2] if self.with_rgb else None)
+        s_out, d_out = src.outputs(), self.frame.outputs()
+        L.check(L.lib().mirt_unpack_tiles_at_async(self.ctx.handle, self.W, self.H, self._unpack_tiles,
+                                                   self._unpack_offsets, self._unpack_n, C.byref(s_out),
+                                                   C.byref(d_out), C.c_void_p(stream_ptr) if stream_ptr else None))
 
     def render(self, frame_and_keep) -> None:
         """Enqueue one frame on torch's current stream (no host sync)."""
@@ -185,15 +250,29 @@ class FrameSharder:
         if self.world == 1:
             trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.tiles_all, self.frame, s)
             return
-        trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.mine, self.packed, s)
-        got = gather_packed(self.packed.raw, self.world, self.rank, self.root, self.group)
-        got_rgb = (gather_packed(self.packed.rgb, self.world, self.rank, self.root, self.group)
-                   if self.with_rgb else None)
+        k = self._k
+        self._k += 1
+        trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.mine, self.bufs[k % 2], s)
+        works = self._gather(k)
+        self._finish_pending(s)
+        self._pending = (k, works)
+
+    def _finish_pending(self, s) -> None:
+        if self._pending is None:
+            return
+        k, works = self._pending
+        self._pending = None
+        for w in works:
+            w.wait()  # the current stream waits for the collective (no host block with RCCL)
         if self.rank == self.root:
-            n = self.cap
-            for r in range(self.world):
-                tiles_r = assign(self.tiles_all, self.world, r)
-                buf = got[r]
-                src = DevicePlanes(rgb8=buf[: n * 3].view(n, 3), valid=buf[n * 3:],
-                                   rgb=got_rgb[r] if got_rgb is not None else None)
-                unpack_device(self.ctx, self.W, self.H, tiles_r, src, self.frame, s)
+            self._unpack(k, s)
+
+    def flush(self) -> None:
+        """Complete the frame whose gather is still in flight (unpack on the root)."""
+        import torch
+        if self.world > 1:
+            self._finish_pending(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def last_packed(self):
+        return self.bufs[(self._k - 1) % 2] if self.world > 1 else None

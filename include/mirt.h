@@ -202,6 +202,14 @@ int mirt_trace_tiles_async(mirt_ctx *ctx, const mirt_frame *frame, uint32_t W, u
  */
 int mirt_unpack_tiles_async(mirt_ctx *ctx, uint32_t W, uint32_t H, const mirt_tile *tiles, uint32_t n_tiles,
                             const mirt_outputs *packed, const mirt_outputs *frame_out, void *stream);
+/*
+ * Same, with an explicit packed offset (in pixels, ascending) per tile, so the packed
+ * buffers of several ranks (each padded to a common size for the gather) are scattered
+ * in ONE launch.  The device copy of the tile list is reused while the list repeats.
+ */
+int mirt_unpack_tiles_at_async(mirt_ctx *ctx, uint32_t W, uint32_t H, const mirt_tile *tiles,
+                               const uint64_t *offsets, uint32_t n_tiles, const mirt_outputs *packed,
+                               const mirt_outputs *frame_out, void *stream);
 
 /* tracer.go:27-50 trace() on n arbitrary rays (host buffers), brute force. */
 int mirt_trace_rays(mirt_ctx *ctx, const mirt_frame *frame, uint32_t n, const double *origins,
