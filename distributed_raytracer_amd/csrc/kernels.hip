@@ -395,6 +395,12 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
 #ifndef MIRT_LDS_MESH
 #define MIRT_LDS_MESH 1
 #endif
+#ifndef MIRT_BLOCK_FRUSTUM
+#define MIRT_BLOCK_FRUSTUM 1
+#endif
+#ifndef MIRT_SKIP_MISS_STORES  // measurement builds only (outputs left unwritten)
+#define MIRT_SKIP_MISS_STORES 0
+#endif
 // Traversal per kernel: 1 = wide cone traversal (shared-origin packets), 0 = per-lane
 // 8-child sweep with scalar node loads.  Measured on MI355X (suzanne 1080p): the sweep is
 // faster for both (profiles/r01_*); the wide walk stays for meshes where it wins.
@@ -866,6 +872,90 @@ __device__ __forceinline__ BlockDesc block_desc(const WorkArgs& wa, uint32_t q, 
     return k < wa.per_shard ? BlockDesc{v[0], v[1], v[2], v[3]} : BlockDesc{0, 0, 0, 0};
 }
 
+// ---------------------------------------------------------------- block frustum
+// Exact pre-test of a whole 8x8 block against the root's child boxes (one-object frames).
+// The block's rays start at O (camera, object space) with directions proportional to
+// U(s, t) = fwd + left * s + up * t, affine in the per-column / per-row offsets s, t, so
+// every ray lies in the cone spanned by the four corner directions (the lanes' fp64 rays
+// deviate by ~2^-52 relative, far inside the margin).  A child box entirely outside one
+// of the cone's four side planes cannot meet any ray of the block; MT candidates lie in
+// their (inflated) leaf boxes, so the block's result cannot depend on that child.  The
+// test runs in fp32 with a margin of 2^-12 of the magnitudes involved.  Five planes: the
+// four sides (each through O and two adjacent corner directions) and the plane through O
+// normal to the cone's axis (without it a box behind the camera that straddles the axis
+// passes every side test).  Lane L < 40 tests child L / 5 against plane L % 5.
+struct RootBoxes {
+    float lx, ly, lz, hx, hy, hz;
+    bool valid;
+};
+__device__ __forceinline__ RootBoxes load_root_boxes(const DevMesh& m) {
+    const uint32_t c = min((threadIdx.x & 63) / 5, 7u);
+    const float* nb = (const float*)m.nodes;  // node 0 = the root
+    RootBoxes r;
+    r.lx = nb[c];
+    r.ly = nb[8 + c];
+    r.lz = nb[16 + c];
+    r.hx = nb[24 + c];
+    r.hy = nb[32 + c];
+    r.hz = nb[40 + c];
+    r.valid = ((const uint32_t*)nb)[48 + c] != kBvhEmpty;
+    return r;
+}
+// Bit c set: root child c may meet a ray of the block.
+__device__ __forceinline__ uint32_t block_frustum(const FrameArgs& fa, const WorkArgs& wa, const RootBoxes& rb, V3 o,
+                                                  double scale, uint32_t px, uint32_t py, uint32_t vw, uint32_t vh) {
+    const uint32_t lane = threadIdx.x & 63;
+    const float s0 = (float)wa.sij[px], s1 = (float)wa.sij[px + vw - 1];
+    const float t0 = (float)wa.sij[fa.W + py], t1 = (float)wa.sij[fa.W + py + vh - 1];
+    const float fx = (float)fa.fwd[0], fy = (float)fa.fwd[1], fz = (float)fa.fwd[2];
+    const float lx = (float)fa.left[0], ly = (float)fa.left[1], lz = (float)fa.left[2];
+    const float ux = (float)fa.up[0], uy = (float)fa.up[1], uz = (float)fa.up[2];
+    auto U = [&](float s, float t, float& x, float& y, float& z) {
+        x = fx + lx * s + ux * t;
+        y = fy + ly * s + uy * t;
+        z = fz + lz * s + uz * t;
+    };
+    float ax, ay, az, bx, by, bz, cx, cy, cz, dx, dy, dz;
+    U(s0, t0, ax, ay, az);
+    U(s1, t0, bx, by, bz);
+    U(s1, t1, cx, cy, cz);
+    U(s0, t1, dx, dy, dz);
+    // this lane's plane: edge (P, Q) of the corner cycle A B C D, or (p == 4) the axis
+    const uint32_t p = lane % 5;
+    const float px_ = p == 0 ? ax : p == 1 ? bx : p == 2 ? cx : dx;
+    const float py_ = p == 0 ? ay : p == 1 ? by : p == 2 ? cy : dy;
+    const float pz_ = p == 0 ? az : p == 1 ? bz : p == 2 ? cz : dz;
+    const float qx = p == 0 ? bx : p == 1 ? cx : p == 2 ? dx : ax;
+    const float qy = p == 0 ? by : p == 1 ? cy : p == 2 ? dy : ay;
+    const float qz = p == 0 ? bz : p == 1 ? cz : p == 2 ? dz : az;
+    float nx = py_ * qz - pz_ * qy, ny = pz_ * qx - px_ * qz, nz = px_ * qy - py_ * qx;
+    const float mx = ax + cx, my = ay + cy, mz = az + cz;  // inside the cone
+    if (p == 4) {  // every corner direction has a positive component along M (narrow cone)
+        nx = mx;
+        ny = my;
+        nz = mz;
+    }
+    if (nx * mx + ny * my + nz * mz < 0.0f) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+    const float vx = (nx >= 0.0f ? rb.hx : rb.lx) - ox;  // the box corner farthest along n
+    const float vy = (ny >= 0.0f ? rb.hy : rb.ly) - oy;
+    const float vz = (nz >= 0.0f ? rb.hz : rb.lz) - oz;
+    const float mag = fmaxf(fmaxf(fabsf(ox), fabsf(oy)), fabsf(oz)) + 4.0f * (float)scale + 1.0f;
+    const float margin = 0x1p-12f * (fabsf(nx) + fabsf(ny) + fabsf(nz)) * mag;
+    const bool outside = nx * vx + ny * vy + nz * vz < -margin;
+    const uint64_t rej = __ballot(lane < 40 && rb.valid && outside);
+    const uint64_t val = __ballot(lane < 40 && p == 0 && rb.valid);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (((val >> (5 * c)) & 1ull) && !((rej >> (5 * c)) & 0x1full)) mask |= 1u << c;
+    return mask;
+}
+
 // ---------------------------------------------------------------- primary block
 // One 8x8 pixel block: raygen (tracer.go:15-22, :86), nearest hit, outputs of misses,
 // and, if any lane hit, 64 hit slots of region q (slot = lane) with their lit word and
@@ -873,7 +963,8 @@ __device__ __forceinline__ BlockDesc block_desc(const WorkArgs& wa, uint32_t q, 
 template <bool REL, bool PREFILTER, bool BRUTE, bool COH>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
-                                              const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc) {
+                                              const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
+                                              bool frustum = false) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -881,6 +972,34 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
     const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
     const bool active = lx < vw && ly < vh;
+    if (frustum) {  // one object, culling on: whole-block frustum pre-test against the root
+        const DevObject& ob = fa.obj[0];
+        const RootBoxes rb = load_root_boxes(ob.m);
+        const V3 o = sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]});
+        const double far = fmax(fmax(__builtin_fabs(o.x), __builtin_fabs(o.y)), __builtin_fabs(o.z));
+        if (far <= ob.m.cull_limit &&
+            block_frustum(fa, wa, rb, o, ob.m.cull_limit * (1.0 / 256.0), px, py, vw, vh) == 0) {
+            ++ws.nodes;
+            if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
+                const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
+                if (out.valid) out.valid[oidx] = 0;
+                if (out.face) out.face[oidx] = -1;
+                if (out.object) out.object[oidx] = -1;
+                if (out.rgb) {
+                    out.rgb[3 * oidx] = 0.0;
+                    out.rgb[3 * oidx + 1] = 0.0;
+                    out.rgb[3 * oidx + 2] = 0.0;
+                }
+                if (out.rgb8) {
+                    out.rgb8[3 * oidx] = 0;
+                    out.rgb8[3 * oidx + 1] = 0;
+                    out.rgb8[3 * oidx + 2] = 0;
+                }
+            }
+            pc.lap(2);
+            return;
+        }
+    }
     const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
 
     // tracer.go:15-22 pixelToPoint (its two divisions, per column and per row, come from
@@ -1041,7 +1160,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     // the first two tickets are in flight while the mesh is staged
     uint32_t q = sc.first_shard();
     uint32_t t0 = 0, t1 = 0;
-    if (wa.dynamic && q < (uint32_t)kQShards) {
+    if ((wa.dynamic & kDynPrimary) && q < (uint32_t)kQShards) {
         t0 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
         t1 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
     }
@@ -1055,12 +1174,13 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     clock.mark_staged();
     WaveStats ws{0, 0, 0, 0, 0};
     PhaseClock pc;
+    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_FRUSTUM);
     for (; q < (uint32_t)kQShards; q += sc.shard_step()) {
         cnt_t* qc = &wa.counters[cnt_queue(0, q)];
         // Ticket pipeline two deep: when block k starts, ticket k+1 is already known, so
         // its descriptor is fetched (scalar loads, no wait) while block k is traced.
         uint32_t k, kn;
-        if (wa.dynamic) {
+        if ((wa.dynamic & kDynPrimary)) {
             if (q != sc.first_shard()) {
                 t0 = ticket_issue(qc);
                 t1 = ticket_issue(qc);
@@ -1074,15 +1194,15 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
         uint32_t blk = k * kQShards + q;
         BlockDesc bd = block_desc(wa, q, k);
         while (blk < wa.nblocks) {
-            const uint32_t t2 = wa.dynamic ? ticket_issue(qc) : 0;
+            const uint32_t t2 = (wa.dynamic & kDynPrimary) ? ticket_issue(qc) : 0;
             const uint32_t nblk = kn * kQShards + q;
             const BlockDesc nbd = block_desc(wa, q, kn);  // scalar loads, used next iteration
             ++taken;
             primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd, q,
-                                                             ws, pc);
+                                                             ws, pc, use_frustum);
             blk = nblk;
             bd = nbd;
-            kn = wa.dynamic ? ticket_resolve(t2) : kn + sc.peers();
+            kn = (wa.dynamic & kDynPrimary) ? ticket_resolve(t2) : kn + sc.peers();
             pc.lap(3);
         }
     }
@@ -1121,13 +1241,13 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
         const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
         const uint32_t items = nch * nl;
         cnt_t* qc = &wa.counters[cnt_queue(1, q)];
-        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        uint32_t k = (wa.dynamic & kDynShadow) ? ticket_resolve(ticket_issue(qc)) : sc.rank();
         while (k < items) {
-            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
+            const uint32_t nxt = (wa.dynamic & kDynShadow) ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
             shadow_item<PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment, q, c, l, ws);
-            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+            k = (wa.dynamic & kDynShadow) ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
@@ -1258,9 +1378,9 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
         cnt_t* qc = &wa.counters[cnt_queue(2, q)];
-        uint32_t k = wa.dynamic ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        uint32_t k = (wa.dynamic & kDynReflect) ? ticket_resolve(ticket_issue(qc)) : sc.rank();
         while (k < nch) {
-            const uint32_t nxt = wa.dynamic ? ticket_issue(qc) : 0;
+            const uint32_t nxt = (wa.dynamic & kDynReflect) ? ticket_issue(qc) : 0;
             const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
             const HitRec rec = wa.hits[slot];
             const bool active = rec.obj != kNoHit;
@@ -1342,7 +1462,7 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
                     out.rgb8[3 * rec.out + 2] = c_u8(c.b);
                 }
             }
-            k = wa.dynamic ? ticket_resolve(nxt) : k + sc.peers();
+            k = (wa.dynamic & kDynReflect) ? ticket_resolve(nxt) : k + sc.peers();
         }
     }
     // reflection rays and their shadow rays as two extra statistics (per workgroup)

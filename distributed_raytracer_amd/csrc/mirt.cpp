@@ -421,7 +421,9 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.counters = sl->counters + (size_t)sl->parity * kCntN;
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
-    wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE) ? 0u : 1u;
+    wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
+                     ? 0u
+                     : (uint32_t)(kDynShadow | kDynReflect | ((c->flags & MIRT_OPT_DYNAMIC_PRIMARY) ? kDynPrimary : 0));
     if (c->flags & MIRT_OPT_TIMELINE) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->timeline) {

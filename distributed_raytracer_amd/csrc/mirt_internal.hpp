@@ -175,13 +175,17 @@ struct WorkArgs {
     double* ph0;           // bounces: per hit slot, phong of the primary hit (3 doubles)
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
-    uint32_t dynamic;      // 1: sharded work queues, 0: static round-robin (ablation)
+    uint32_t dynamic;      // kDyn* bits: kernels that take work from the sharded queues (else static)
     uint32_t timeline_cap; // records the timeline buffer holds per kernel
     uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
     cnt_t* summary;        // kStatN totals of this frame (written by k_shade's last workgroup)
     cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
 };
 constexpr int kTimelineRec = 8;
+// WorkArgs::dynamic.  Measured on MI355X: the primary kernel's blocks are even enough for
+// a static round-robin split (the ticket atomics cost more than they balance), the shadow
+// and reflect kernels' items are not.
+enum { kDynPrimary = 1, kDynShadow = 2, kDynReflect = 4 };
 
 // Arbitrary-ray inputs/outputs for mirt_trace_rays.
 struct RayIO {

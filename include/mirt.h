@@ -224,10 +224,12 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 /* Ask for kernel variants (benchmark ablations).  0 = defaults. */
 #define MIRT_OPT_NO_PREFILTER 1u  /* always take the true fp64 divide for r2 */
 #define MIRT_OPT_BRUTE_FORCE 2u   /* test every triangle (no BVH culling), mesh streamed via LDS */
-#define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split instead of the dynamic work queues */
+#define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split in every kernel (no work queues) */
 #define MIRT_OPT_TIMELINE 8u        /* record per-wave start/end stamps (mirt_debug_timeline) */
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
 #define MIRT_OPT_ONE_KERNEL 32u     /* one k_trace launch per frame (default: primary, then shadow+shade) */
+#define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
+#define MIRT_OPT_DYNAMIC_PRIMARY 128u /* primary blocks from the work queues (default: static split) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*

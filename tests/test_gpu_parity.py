@@ -77,7 +77,8 @@ def _variants(ctx, fn):
         for opts in (0, rt._lib.MIRT_OPT_NO_PREFILTER, rt._lib.MIRT_OPT_BRUTE_FORCE,
                      rt._lib.MIRT_OPT_BRUTE_FORCE | rt._lib.MIRT_OPT_NO_PREFILTER,
                      rt._lib.MIRT_OPT_STATIC_SCHEDULE, rt._lib.MIRT_OPT_NO_SEGMENT,
-                     rt._lib.MIRT_OPT_ONE_KERNEL, rt._lib.MIRT_OPT_ONE_KERNEL | rt._lib.MIRT_OPT_BRUTE_FORCE):
+                     rt._lib.MIRT_OPT_ONE_KERNEL, rt._lib.MIRT_OPT_ONE_KERNEL | rt._lib.MIRT_OPT_BRUTE_FORCE,
+                     rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_DYNAMIC_PRIMARY):
             ctx.set_options(opts)
             out[opts] = fn()
     finally:

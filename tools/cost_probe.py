@@ -28,7 +28,9 @@ def main():
         "closeup": rt.Camera.new(tuple(np.asarray(cam.pos) + 0.6 * (np.array([1.0, 1.0, -1.0]) - np.asarray(cam.pos))),
                                  tuple(np.array([1.0, 1.0, -1.0]) - np.asarray(cam.pos)), cam.fov),
     }
-    opts = {"two_kernels": 0, "no_segment": rt._lib.MIRT_OPT_NO_SEGMENT, "one_kernel": rt._lib.MIRT_OPT_ONE_KERNEL}
+    opts = {"default": 0, "static": rt._lib.MIRT_OPT_STATIC_SCHEDULE, "no_frustum": rt._lib.MIRT_OPT_NO_FRUSTUM,
+            "dyn_primary": rt._lib.MIRT_OPT_DYNAMIC_PRIMARY,
+            "one_kernel": rt._lib.MIRT_OPT_ONE_KERNEL}
     sh = FrameSharder(ctx, 1920, 1080, 0, 1, 64)
     out = {}
     stream = torch.cuda.Stream()

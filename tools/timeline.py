@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--static", action="store_true")
+    ap.add_argument("--opts", type=int, default=0, help="extra MIRT_OPT_* bits")
     ap.add_argument("--save", default="")
     ap.add_argument("--view", default="default", choices=("default", "away"))
     ap.add_argument("--phase", action="store_true",
@@ -68,7 +69,7 @@ def main():
         mut = rt.EnvMutables(mut.objects, mut.lights, rt.Camera.new(c.pos, tuple(-np.asarray(c.forward)), c.fov))
     frame = mut.to_frame()
     sh = FrameSharder(ctx, a.width, a.height, 0, 1, 64)
-    opts = rt._lib.MIRT_OPT_TIMELINE | (rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static else 0)
+    opts = rt._lib.MIRT_OPT_TIMELINE | (rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static else 0) | a.opts
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         ctx.set_options(0)
