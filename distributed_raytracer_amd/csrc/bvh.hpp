@@ -160,7 +160,7 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
         Bvh8Node root;
         for (int c = 0; c < 8; ++c) root.child[c] = kBvhEmpty;
         for (int k = 0; k < 3; ++k)
-            for (int c = 0; c < 8; ++c) root.lo[k][c] = root.hi[k][c] = 0.0f;
+            for (int c = 0; c < 8; ++c) root.lo(k, c) = root.hi(k, c) = 0.0f;
         out.nodes.push_back(root);
         return out;
     }
@@ -198,13 +198,13 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
         for (int c = 0; c < 8; ++c) {
             if (c >= (int)kids.size()) {
                 nd.child[c] = kBvhEmpty;
-                for (int k = 0; k < 3; ++k) { nd.lo[k][c] = 1.0f; nd.hi[k][c] = -1.0f; }
+                for (int k = 0; k < 3; ++k) { nd.lo(k, c) = 1.0f; nd.hi(k, c) = -1.0f; }
                 continue;
             }
             const BNode& k = b.nodes[kids[c]];
             for (int a = 0; a < 3; ++a) {
-                nd.lo[a][c] = round_down(k.box.lo[a] - inflate);
-                nd.hi[a][c] = round_up(k.box.hi[a] + inflate);
+                nd.lo(a, c) = round_down(k.box.lo[a] - inflate);
+                nd.hi(a, c) = round_up(k.box.hi[a] + inflate);
             }
             if (k.left < 0) {
                 nd.child[c] = kBvhLeafBit | (k.count << kBvhCountShift) | k.first;

@@ -34,6 +34,8 @@ typedef const __attribute__((address_space(4))) double* cdptr;
 typedef const __attribute__((address_space(4))) Bvh8Node* cnptr;
 typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
 typedef const __attribute__((address_space(4))) u32x16* cv16ptr;
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) u32x8* cv8ptr;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(4))) u32x4* cv4ptr;
 
@@ -305,20 +307,21 @@ __device__ __forceinline__ Ray32 ray32(V3 ro, V3 d) {
     r.oiz = r.oz * r.iz;
     return r;
 }
-// A node in SGPRs: four s_load_dwordx16.  Words 0..23 lo[axis][child], 24..47
-// hi[axis][child], 48..55 child refs.
+// A node in SGPRs: three s_load_dwordx16 + one s_load_dwordx8.  Words 16 a + 2 c (+1): lo (hi) of child c on
+// axis a, 48..55 child refs.
 struct NodeRegs {
-    u32x16 w0, w1, w2, w3;
+    u32x16 w0, w1, w2;
+    u32x8 w3;  // the child refs (the node's last 8 words are padding, never loaded)
     __device__ __forceinline__ uint32_t word(int i) const {
         return i < 16 ? w0[i] : i < 32 ? w1[i - 16] : i < 48 ? w2[i - 32] : w3[i - 48];
     }
-    __device__ __forceinline__ float lo(int a, int c) const { return __uint_as_float(word(a * 8 + c)); }
-    __device__ __forceinline__ float hi(int a, int c) const { return __uint_as_float(word(24 + a * 8 + c)); }
+    __device__ __forceinline__ float lo(int a, int c) const { return __uint_as_float(word(a * 16 + 2 * c)); }
+    __device__ __forceinline__ float hi(int a, int c) const { return __uint_as_float(word(a * 16 + 2 * c + 1)); }
     __device__ __forceinline__ uint32_t child(int c) const { return word(48 + c); }
 };
 __device__ __forceinline__ NodeRegs load_node(cnptr nd) {
     const cv16ptr p = (cv16ptr)nd;
-    return NodeRegs{p[0], p[1], p[2], p[3]};
+    return NodeRegs{p[0], p[1], p[2], ((cv8ptr)nd)[6]};
 }
 
 // Ray vs child c's box, t >= 0 half-line.  Boxes are inflated by 2^-12 of the mesh
@@ -332,6 +335,59 @@ __device__ __forceinline__ bool slab32(const NodeRegs& nd, int c, const Ray32& r
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     return tn <= (SEG ? fminf(tf, tmax) : tf);
+}
+
+// The same test as a lane mask (v_cmp straight into SGPRs: no per-lane bool to pack).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// {lo, hi} * a[SA] - b[SB] in one v_pk_fma_f32: the box pair is an SGPR operand and
+// op_sel broadcasts one dword of each ray pair to both halves (no per-child moves).
+#define MIRT_PK_SLAB(SA, SB)                                                                         \
+    template <>                                                                                      \
+    __device__ __forceinline__ f32x2 pk_slab<SA, SB>(f32x2 box, f32x2 a, f32x2 b) {                  \
+        f32x2 t;                                                                                     \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0," #SA "," #SB "] op_sel_hi:[1," #SA "," #SB      \
+            "] neg_lo:[0,0,1] neg_hi:[0,0,1]"                                                        \
+            : "=v"(t) : "s"(box), "v"(a), "v"(b));                                                   \
+        return t;                                                                                    \
+    }
+template <int SA, int SB>
+__device__ __forceinline__ f32x2 pk_slab(f32x2 box, f32x2 a, f32x2 b);
+__device__ __forceinline__ float a_min(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float a_max(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float a_min3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float a_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+MIRT_PK_SLAB(0, 1)
+MIRT_PK_SLAB(1, 0)
+#undef MIRT_PK_SLAB
+template <bool SEG>
+__device__ __forceinline__ uint64_t slab_mask(const NodeRegs& nd, int c, const Ray32& r, float tmax) {
+    // both planes of an axis in one packed FMA; ray pairs (ix, iy), (iz, oix), (oiy, oiz)
+    const f32x2 p0 = {r.ix, r.iy}, p1 = {r.iz, r.oix}, p2 = {r.oiy, r.oiz};
+    const f32x2 tx = pk_slab<0, 1>((f32x2){nd.lo(0, c), nd.hi(0, c)}, p0, p1);
+    const f32x2 ty = pk_slab<1, 0>((f32x2){nd.lo(1, c), nd.hi(1, c)}, p0, p2);
+    const f32x2 tz = pk_slab<0, 1>((f32x2){nd.lo(2, c), nd.hi(2, c)}, p1, p2);
+    // min/max as asm too: the compiler would otherwise canonicalize each asm result first
+    // (no NaN reaches here: 1/D is clamped to +-2^60, bounds and origins are finite)
+    const float tn = a_max3(a_min(tx.x, tx.y), a_min(ty.x, ty.y), a_max(a_min(tz.x, tz.y), 0.0f));
+    float tf = a_min3(a_max(tx.x, tx.y), a_max(ty.x, ty.y), a_max(tz.x, tz.y));
+    if (SEG) tf = a_min(tf, tmax);
+    return __builtin_amdgcn_fcmpf(tn, tf, 5 /* FCMP_OLE: tn <= tf */);
 }
 
 // Wave-uniform walk of one object's 8-wide BVH (packet traversal).  A child is entered
@@ -348,24 +404,28 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
     const bool force = !(far <= m.cull_limit);
     bool live = lane_on;
+    const uint64_t fmask = __ballot(force);
     WaveStack stk;
     uint32_t cur = 0;
     for (;;) {
         cur = __builtin_amdgcn_readfirstlane(cur);
         const NodeRegs nd = load_node((cnptr)m.nodes + cur);
         ++vis.nodes;
-        uint32_t hits = 0;  // per lane: bit c = ray hits child c
+        // wave-uniform: bit c = some live lane's ray hits child c (each test's compare
+        // result is the lane mask itself: no per-lane bit packing)
+        uint32_t entered = 0;
+        const uint64_t lmask = __ballot(live);
 #pragma unroll
         for (int c = 0; c < 8; ++c)
-            if (nd.child(c) != kBvhEmpty)  // branch-free: every lane evaluates, masks after
-                hits |= (uint32_t)(live & (force | slab32<SEG>(nd, c, r, tmax))) << c;
+            if (nd.child(c) != kBvhEmpty && ((slab_mask<SEG>(nd, c, r, tmax) | fmask) & lmask) != 0)
+                entered |= 1u << c;
         // classify the entered children (unrolled: SALU only), then test the leaves in ONE
         // loop so the triangle test is instantiated once (code size: instruction cache)
         uint32_t leafmask = 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const uint32_t ref = nd.child(c);
-            if (ref == kBvhEmpty || __ballot((hits >> c) & 1u) == 0) continue;
+            if (!((entered >> c) & 1u)) continue;
             if (ref & kBvhLeafBit)
                 leafmask |= 1u << c;
             else
@@ -542,12 +602,12 @@ __device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t*
         if (on) {
             const float* nb = (const float*)(m.nodes + node);
             ref = ((const uint32_t*)nb)[48 + c];
-            lx = nb[c];
-            ly = nb[8 + c];
-            lz = nb[16 + c];
-            hx = nb[24 + c];
-            hy = nb[32 + c];
-            hz = nb[40 + c];
+            lx = nb[2 * c];
+            ly = nb[16 + 2 * c];
+            lz = nb[32 + 2 * c];
+            hx = nb[2 * c + 1];
+            hy = nb[16 + 2 * c + 1];
+            hz = nb[32 + 2 * c + 1];
         }
         const bool acc = ref != kBvhEmpty && (cone.all || cone_box(cone, lx, ly, lz, hx, hy, hz));
         const bool is_leaf = (ref & kBvhLeafBit) != 0;
@@ -836,6 +896,10 @@ __device__ __forceinline__ uint32_t ticket_issue(cnt_t* c) {
     return t;
 }
 __device__ __forceinline__ uint32_t ticket_resolve(uint32_t t) { return __builtin_amdgcn_readfirstlane(t); }
+// Work items of shard q when item k of the shard is global item k * kQShards + q.
+__device__ __forceinline__ uint32_t shard_items(uint32_t n, uint32_t q) {
+    return n > q ? (n - q + kQShards - 1) / kQShards : 0u;
+}
 
 // ---------------------------------------------------------------- hit slots
 // A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.  COH: device-scope
@@ -884,36 +948,31 @@ __device__ __forceinline__ BlockDesc block_desc(const WorkArgs& wa, uint32_t q, 
 // four sides (each through O and two adjacent corner directions) and the plane through O
 // normal to the cone's axis (without it a box behind the camera that straddles the axis
 // passes every side test).  Lane L < 40 tests child L / 5 against plane L % 5.
-struct RootBoxes {
-    float lx, ly, lz, hx, hy, hz;
-    bool valid;
-};
-__device__ __forceinline__ RootBoxes load_root_boxes(const DevMesh& m) {
-    const uint32_t c = min((threadIdx.x & 63) / 5, 7u);
-    const float* nb = (const float*)m.nodes;  // node 0 = the root
-    RootBoxes r;
-    r.lx = nb[c];
-    r.ly = nb[8 + c];
-    r.lz = nb[16 + c];
-    r.hx = nb[24 + c];
-    r.hy = nb[32 + c];
-    r.hz = nb[40 + c];
-    r.valid = ((const uint32_t*)nb)[48 + c] != kBvhEmpty;
-    return r;
+// Root child boxes in LDS (staged once per workgroup): entry 2c = lo.xyz | valid,
+// 2c + 1 = hi.xyz.
+__device__ __forceinline__ void stage_root_boxes(float4* __restrict__ rootb, const DevMesh& m) {
+    if (threadIdx.x < 8) {
+        const uint32_t c = threadIdx.x;
+        const float* nb = (const float*)m.nodes;  // node 0 = the root
+        const bool valid = ((const uint32_t*)nb)[48 + c] != kBvhEmpty;
+        rootb[2 * c] = make_float4(nb[2 * c], nb[16 + 2 * c], nb[32 + 2 * c], valid ? 1.0f : 0.0f);
+        rootb[2 * c + 1] = make_float4(nb[2 * c + 1], nb[17 + 2 * c], nb[33 + 2 * c], 0.0f);
+    }
 }
-// Bit c set: root child c may meet a ray of the block.
-__device__ __forceinline__ uint32_t block_frustum(const FrameArgs& fa, const WorkArgs& wa, const RootBoxes& rb, V3 o,
-                                                  double scale, uint32_t px, uint32_t py, uint32_t vw, uint32_t vh) {
+// Bit c set: root child c may meet a ray of the block.  Loads: LDS only (the per-frame
+// constants are kernel arguments, wa.fr).
+__device__ __forceinline__ uint32_t block_frustum(const FrustumArgs& fr, const float4* __restrict__ rootb,
+                                                  uint32_t px, uint32_t py, uint32_t vw, uint32_t vh) {
     const uint32_t lane = threadIdx.x & 63;
-    const float s0 = (float)wa.sij[px], s1 = (float)wa.sij[px + vw - 1];
-    const float t0 = (float)wa.sij[fa.W + py], t1 = (float)wa.sij[fa.W + py + vh - 1];
-    const float fx = (float)fa.fwd[0], fy = (float)fa.fwd[1], fz = (float)fa.fwd[2];
-    const float lx = (float)fa.left[0], ly = (float)fa.left[1], lz = (float)fa.left[2];
-    const float ux = (float)fa.up[0], uy = (float)fa.up[1], uz = (float)fa.up[2];
+    const uint32_t c = min(lane / 5, 7u);
+    const float4 lo = rootb[2 * c], hi = rootb[2 * c + 1];
+    // corner offsets: the affine form of tracer.go:19-20 in fp64, rounded to fp32
+    const float s0 = (float)(fr.sB - fr.sA * (double)px), s1 = (float)(fr.sB - fr.sA * (double)(px + vw - 1));
+    const float t0 = (float)(fr.tB - fr.tA * (double)py), t1 = (float)(fr.tB - fr.tA * (double)(py + vh - 1));
     auto U = [&](float s, float t, float& x, float& y, float& z) {
-        x = fx + lx * s + ux * t;
-        y = fy + ly * s + uy * t;
-        z = fz + lz * s + uz * t;
+        x = fr.f[0] + fr.l[0] * s + fr.u[0] * t;
+        y = fr.f[1] + fr.l[1] * s + fr.u[1] * t;
+        z = fr.f[2] + fr.l[2] * s + fr.u[2] * t;
     };
     float ax, ay, az, bx, by, bz, cx, cy, cz, dx, dy, dz;
     U(s0, t0, ax, ay, az);
@@ -940,19 +999,17 @@ __device__ __forceinline__ uint32_t block_frustum(const FrameArgs& fa, const Wor
         ny = -ny;
         nz = -nz;
     }
-    const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-    const float vx = (nx >= 0.0f ? rb.hx : rb.lx) - ox;  // the box corner farthest along n
-    const float vy = (ny >= 0.0f ? rb.hy : rb.ly) - oy;
-    const float vz = (nz >= 0.0f ? rb.hz : rb.lz) - oz;
-    const float mag = fmaxf(fmaxf(fabsf(ox), fabsf(oy)), fabsf(oz)) + 4.0f * (float)scale + 1.0f;
-    const float margin = 0x1p-12f * (fabsf(nx) + fabsf(ny) + fabsf(nz)) * mag;
-    const bool outside = nx * vx + ny * vy + nz * vz < -margin;
-    const uint64_t rej = __ballot(lane < 40 && rb.valid && outside);
-    const uint64_t val = __ballot(lane < 40 && p == 0 && rb.valid);
+    const float vx = (nx >= 0.0f ? hi.x : lo.x) - fr.o[0];  // the box corner farthest along n
+    const float vy = (ny >= 0.0f ? hi.y : lo.y) - fr.o[1];
+    const float vz = (nz >= 0.0f ? hi.z : lo.z) - fr.o[2];
+    const float margin = 0x1p-12f * (fabsf(nx) + fabsf(ny) + fabsf(nz)) * fr.mag;
+    // an empty child slot counts as outside every plane
+    const bool outside = lo.w == 0.0f || nx * vx + ny * vy + nz * vz < -margin;
+    const uint64_t rej = __ballot(lane < 40 && outside);
     uint32_t mask = 0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-        if (((val >> (5 * c)) & 1ull) && !((rej >> (5 * c)) & 0x1full)) mask |= 1u << c;
+    for (int k = 0; k < 8; ++k)
+        if (!((rej >> (5 * k)) & 0x1full)) mask |= 1u << k;
     return mask;
 }
 
@@ -964,7 +1021,7 @@ template <bool REL, bool PREFILTER, bool BRUTE, bool COH>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
-                                              bool frustum = false) {
+                                              bool frustum = false, const float4* __restrict__ rootb = nullptr) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -972,33 +1029,26 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
     const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
     const bool active = lx < vw && ly < vh;
-    if (frustum) {  // one object, culling on: whole-block frustum pre-test against the root
-        const DevObject& ob = fa.obj[0];
-        const RootBoxes rb = load_root_boxes(ob.m);
-        const V3 o = sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]});
-        const double far = fmax(fmax(__builtin_fabs(o.x), __builtin_fabs(o.y)), __builtin_fabs(o.z));
-        if (far <= ob.m.cull_limit &&
-            block_frustum(fa, wa, rb, o, ob.m.cull_limit * (1.0 / 256.0), px, py, vw, vh) == 0) {
-            ++ws.nodes;
-            if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
-                const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
-                if (out.valid) out.valid[oidx] = 0;
-                if (out.face) out.face[oidx] = -1;
-                if (out.object) out.object[oidx] = -1;
-                if (out.rgb) {
-                    out.rgb[3 * oidx] = 0.0;
-                    out.rgb[3 * oidx + 1] = 0.0;
-                    out.rgb[3 * oidx + 2] = 0.0;
-                }
-                if (out.rgb8) {
-                    out.rgb8[3 * oidx] = 0;
-                    out.rgb8[3 * oidx + 1] = 0;
-                    out.rgb8[3 * oidx + 2] = 0;
-                }
+    if (frustum && block_frustum(wa.fr, rootb, px, py, vw, vh) == 0) {  // whole-block pre-test
+        ++ws.nodes;
+        if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
+            const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
+            if (out.valid) out.valid[oidx] = 0;
+            if (out.face) out.face[oidx] = -1;
+            if (out.object) out.object[oidx] = -1;
+            if (out.rgb) {
+                out.rgb[3 * oidx] = 0.0;
+                out.rgb[3 * oidx + 1] = 0.0;
+                out.rgb[3 * oidx + 2] = 0.0;
             }
-            pc.lap(2);
-            return;
+            if (out.rgb8) {
+                out.rgb8[3 * oidx] = 0;
+                out.rgb8[3 * oidx + 1] = 0;
+                out.rgb8[3 * oidx + 2] = 0;
+            }
         }
+        pc.lap(2);
+        return;
     }
     const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
 
@@ -1153,56 +1203,42 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
+    __shared__ float4 rootb[16];
     WaveClock clock;
     uint32_t taken = 0;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     const ShardCursor sc;
-    // the first two tickets are in flight while the mesh is staged
-    uint32_t q = sc.first_shard();
-    uint32_t t0 = 0, t1 = 0;
-    if ((wa.dynamic & kDynPrimary) && q < (uint32_t)kQShards) {
-        t0 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
-        t1 = ticket_issue(&wa.counters[cnt_queue(0, q)]);
-    }
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
+    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;
+    if (use_frustum) stage_root_boxes(rootb, fa.obj[0].m);
     if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
-        __syncthreads();
     }
+    if (RESIDENT || use_frustum) __syncthreads();
     clock.mark_staged();
     WaveStats ws{0, 0, 0, 0, 0};
     PhaseClock pc;
-    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_FRUSTUM);
-    for (; q < (uint32_t)kQShards; q += sc.shard_step()) {
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         cnt_t* qc = &wa.counters[cnt_queue(0, q)];
-        // Ticket pipeline two deep: when block k starts, ticket k+1 is already known, so
-        // its descriptor is fetched (scalar loads, no wait) while block k is traced.
-        uint32_t k, kn;
-        if ((wa.dynamic & kDynPrimary)) {
-            if (q != sc.first_shard()) {
-                t0 = ticket_issue(qc);
-                t1 = ticket_issue(qc);
-            }
-            k = ticket_resolve(t0);
-            kn = ticket_resolve(t1);
-        } else {
-            k = sc.rank();
-            kn = k + sc.peers();
-        }
-        uint32_t blk = k * kQShards + q;
+        const uint32_t count = shard_items(wa.nblocks, q), peers = sc.peers();
+        // Blocks rank and rank + peers of the shard are this wave's (static split, no
+        // atomics on the way in); with the queue on, blocks 2 peers + ticket follow.  The
+        // pipeline is two deep: when block k starts, the next one is already known and its
+        // descriptor is fetched (scalar loads, no wait) while block k is traced.
+        const bool dyn = (wa.dynamic & kDynPrimary) && count > 2 * peers;
+        uint32_t k = sc.rank(), kn = k + peers;
         BlockDesc bd = block_desc(wa, q, k);
-        while (blk < wa.nblocks) {
-            const uint32_t t2 = (wa.dynamic & kDynPrimary) ? ticket_issue(qc) : 0;
-            const uint32_t nblk = kn * kQShards + q;
+        while (k < count) {
+            const uint32_t t2 = dyn ? ticket_issue(qc) : 0;
             const BlockDesc nbd = block_desc(wa, q, kn);  // scalar loads, used next iteration
             ++taken;
             primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd, q,
-                                                             ws, pc, use_frustum);
-            blk = nblk;
+                                                             ws, pc, use_frustum, rootb);
+            k = kn;
             bd = nbd;
-            kn = (wa.dynamic & kDynPrimary) ? ticket_resolve(t2) : kn + sc.peers();
+            kn = dyn ? 2 * peers + ticket_resolve(t2) : kn + peers;
             pc.lap(3);
         }
     }
@@ -1239,15 +1275,18 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
     const uint32_t nl = max(fa.n_lights, 1u);
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
-        const uint32_t items = nch * nl;
+        const uint32_t items = nch * nl, peers = sc.peers();
         cnt_t* qc = &wa.counters[cnt_queue(1, q)];
-        uint32_t k = (wa.dynamic & kDynShadow) ? ticket_resolve(ticket_issue(qc)) : sc.rank();
+        // item rank is this wave's (static); with the queue on, items peers + ticket follow,
+        // each ticket taken while the previous item is traced
+        const bool dyn = (wa.dynamic & kDynShadow) && items > peers;
+        uint32_t k = sc.rank();
         while (k < items) {
-            const uint32_t nxt = (wa.dynamic & kDynShadow) ? ticket_issue(qc) : 0;
+            const uint32_t nxt = dyn ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
             shadow_item<PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment, q, c, l, ws);
-            k = (wa.dynamic & kDynShadow) ? ticket_resolve(nxt) : k + sc.peers();
+            k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);

@@ -281,6 +281,34 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         }
 }
 
+// Constants of the primary kernel's whole-block frustum pre-test (kernels.hip
+// block_frustum), from the same fp64 values the kernel's rays are built from.
+void frustum_args(const mirt_ctx* c, const FrameArgs& fa, FrustumArgs& fr) {
+    memset(&fr, 0, sizeof(fr));
+    if (fa.n_objects != 1 || (c->flags & (MIRT_OPT_NO_FRUSTUM | MIRT_OPT_BRUTE_FORCE)) || fa.halfW < 1 ||
+        fa.halfH < 1)
+        return;
+    const DevObject& ob = fa.obj[0];
+    double o[3], far = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        o[k] = fa.cam[k] - ob.pos[k];
+        far = std::max(far, std::fabs(o[k]));
+    }
+    if (!(far <= ob.m.cull_limit)) return;  // also: cull_limit < 0 (culling off)
+    for (int k = 0; k < 3; ++k) {
+        fr.o[k] = (float)o[k];
+        fr.f[k] = (float)fa.fwd[k];
+        fr.l[k] = (float)fa.left[k];
+        fr.u[k] = (float)fa.up[k];
+    }
+    fr.mag = (float)(far + 4.0 * (ob.m.cull_limit * (1.0 / 256.0)) + 1.0);
+    fr.sA = fa.phw / (double)fa.halfW;
+    fr.sB = fa.phw * ((double)fa.halfW - 0.5) / (double)fa.halfW;
+    fr.tA = fa.phh / (double)fa.halfH;
+    fr.tB = fa.phh * ((double)fa.halfH - 0.5) / (double)fa.halfH;
+    fr.on = std::isfinite(fr.sA) && std::isfinite(fr.sB) && std::isfinite(fr.tA) && std::isfinite(fr.tB) ? 1u : 0u;
+}
+
 int prof_get(mirt_ctx* c, ProfRec& r) {
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->prof_free.empty()) {
@@ -421,6 +449,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.counters = sl->counters + (size_t)sl->parity * kCntN;
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
+    frustum_args(c, fa, wa.fr);
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
                      ? 0u
                      : (uint32_t)(kDynShadow | kDynReflect | ((c->flags & MIRT_OPT_DYNAMIC_PRIMARY) ? kDynPrimary : 0));

@@ -11,7 +11,10 @@ namespace mirt {
 // Launch geometry.  Persistent workgroups of 8 waves (two per CU: the LDS mesh copy is
 // 72 KiB).  A wave's unit of primary work is one 8x8 pixel block; waves take blocks
 // from a sharded work queue independently of each other (see the counter layout below).
-constexpr int kWG = 512;
+#ifndef MIRT_WG
+#define MIRT_WG 512
+#endif
+constexpr int kWG = MIRT_WG;  // threads per workgroup of the trace kernels
 constexpr int kBlk = 8;
 // Doubles per triangle record in HBM and LDS: P1, E1 = P2-P1, E2 = P3-P1 (72 B).
 constexpr int kTriD = 9;
@@ -25,12 +28,14 @@ constexpr int kLdsTris = 1024;
 // slab test (DESIGN.md §4 "Exact culling").  child[c]: kBvhEmpty, an inner node index,
 // or kBvhLeafBit | count << kBvhCountShift | first (a contiguous triangle range).
 // Non-empty children come first.  256 B, 64-byte aligned: fetched as four
-// s_load_dwordx16 per visit.
+// s_load_dwordx16 per visit.  A child's lo/hi bounds on one axis are adjacent words (an
+// aligned SGPR pair: one packed-fp32 operand of the slab test).
 struct alignas(64) Bvh8Node {
-    float lo[3][8];
-    float hi[3][8];
+    float box[3][8][2];  // [axis][child][lo, hi]
     uint32_t child[8];
     uint32_t pad[8];
+    float& lo(int a, int c) { return box[a][c][0]; }
+    float& hi(int a, int c) { return box[a][c][1]; }
 };
 constexpr uint32_t kBvhEmpty = 0xffffffffu;
 constexpr uint32_t kBvhLeafBit = 0x80000000u;
@@ -158,6 +163,15 @@ __host__ __device__ constexpr int cnt_pdone(int q) {
 constexpr int kCntN = ((kQueues + 2) * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
 typedef unsigned long long cnt_t;
 
+// Block frustum pre-test of one-object frames (kernels.hip block_frustum): per-frame
+// constants computed on the host with the kernel's fp64 operations, then rounded to fp32.
+struct FrustumArgs {
+    float o[3], mag;       // camera in object space (cam - pos); max|o| + 4 scale + 1
+    float f[3], l[3], u[3];
+    uint32_t on;           // one object, culling on, origin within cull_limit, W, H >= 2
+    double sA, sB, tA, tB; // tracer.go:19-20 as affine maps: sij[i] ~ sB - sA i, sij[W + j] ~ tB - tA j
+};
+
 // Per-frame work description shared by the primary, shadow and shade kernels.
 struct WorkArgs {
     const BlockDesc* blocks;
@@ -175,6 +189,7 @@ struct WorkArgs {
     double* ph0;           // bounces: per hit slot, phong of the primary hit (3 doubles)
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
+    FrustumArgs fr;
     uint32_t dynamic;      // kDyn* bits: kernels that take work from the sharded queues (else static)
     uint32_t timeline_cap; // records the timeline buffer holds per kernel
     uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
