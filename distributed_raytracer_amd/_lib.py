@@ -29,7 +29,6 @@ MIRT_OPT_TIMELINE = 8
 MIRT_OPT_NO_SEGMENT = 16
 MIRT_OPT_ONE_KERNEL = 32
 MIRT_OPT_NO_FRUSTUM = 64
-MIRT_OPT_DYNAMIC_PRIMARY = 128
 
 D3 = C.c_double * 3
 

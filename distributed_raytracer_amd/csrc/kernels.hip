@@ -937,80 +937,25 @@ __device__ __forceinline__ BlockDesc block_desc(const WorkArgs& wa, uint32_t q, 
 }
 
 // ---------------------------------------------------------------- block frustum
-// Exact pre-test of a whole 8x8 block against the root's child boxes (one-object frames).
-// The block's rays start at O (camera, object space) with directions proportional to
-// U(s, t) = fwd + left * s + up * t, affine in the per-column / per-row offsets s, t, so
-// every ray lies in the cone spanned by the four corner directions (the lanes' fp64 rays
-// deviate by ~2^-52 relative, far inside the margin).  A child box entirely outside one
-// of the cone's four side planes cannot meet any ray of the block; MT candidates lie in
-// their (inflated) leaf boxes, so the block's result cannot depend on that child.  The
-// test runs in fp32 with a margin of 2^-12 of the magnitudes involved.  Five planes: the
-// four sides (each through O and two adjacent corner directions) and the plane through O
-// normal to the cone's axis (without it a box behind the camera that straddles the axis
-// passes every side test).  Lane L < 40 tests child L / 5 against plane L % 5.
-// Root child boxes in LDS (staged once per workgroup): entry 2c = lo.xyz | valid,
-// 2c + 1 = hi.xyz.
-__device__ __forceinline__ void stage_root_boxes(float4* __restrict__ rootb, const DevMesh& m) {
-    if (threadIdx.x < 8) {
-        const uint32_t c = threadIdx.x;
-        const float* nb = (const float*)m.nodes;  // node 0 = the root
-        const bool valid = ((const uint32_t*)nb)[48 + c] != kBvhEmpty;
-        rootb[2 * c] = make_float4(nb[2 * c], nb[16 + 2 * c], nb[32 + 2 * c], valid ? 1.0f : 0.0f);
-        rootb[2 * c + 1] = make_float4(nb[2 * c + 1], nb[17 + 2 * c], nb[33 + 2 * c], 0.0f);
-    }
+// Whole-block pre-test (one-object frames, mirt_internal.hpp FrustumArgs): the block's
+// rays span s in [s(px + vw - 1), s(px)] and t in [t(py + vh - 1), t(py)]; lane c < 8
+// checks that range against root child c's projected rectangle (staged in LDS).  A block
+// none of whose rectangles it overlaps cannot hit the object.  Bit c set: child c may be
+// met by a ray of the block.
+__device__ __forceinline__ void stage_frustum(float4* __restrict__ rects, const FrustumArgs& fr) {
+    if (threadIdx.x < 8)
+        rects[threadIdx.x] = make_float4(fr.rect[threadIdx.x][0], fr.rect[threadIdx.x][1], fr.rect[threadIdx.x][2],
+                                         fr.rect[threadIdx.x][3]);
 }
-// Bit c set: root child c may meet a ray of the block.  Loads: LDS only (the per-frame
-// constants are kernel arguments, wa.fr).
-__device__ __forceinline__ uint32_t block_frustum(const FrustumArgs& fr, const float4* __restrict__ rootb,
+__device__ __forceinline__ uint32_t block_frustum(const FrustumArgs& fr, const float4* __restrict__ rects,
                                                   uint32_t px, uint32_t py, uint32_t vw, uint32_t vh) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = min(lane / 5, 7u);
-    const float4 lo = rootb[2 * c], hi = rootb[2 * c + 1];
-    // corner offsets: the affine form of tracer.go:19-20 in fp64, rounded to fp32
+    const float4 r = rects[lane & 7];
     const float s0 = (float)(fr.sB - fr.sA * (double)px), s1 = (float)(fr.sB - fr.sA * (double)(px + vw - 1));
     const float t0 = (float)(fr.tB - fr.tA * (double)py), t1 = (float)(fr.tB - fr.tA * (double)(py + vh - 1));
-    auto U = [&](float s, float t, float& x, float& y, float& z) {
-        x = fr.f[0] + fr.l[0] * s + fr.u[0] * t;
-        y = fr.f[1] + fr.l[1] * s + fr.u[1] * t;
-        z = fr.f[2] + fr.l[2] * s + fr.u[2] * t;
-    };
-    float ax, ay, az, bx, by, bz, cx, cy, cz, dx, dy, dz;
-    U(s0, t0, ax, ay, az);
-    U(s1, t0, bx, by, bz);
-    U(s1, t1, cx, cy, cz);
-    U(s0, t1, dx, dy, dz);
-    // this lane's plane: edge (P, Q) of the corner cycle A B C D, or (p == 4) the axis
-    const uint32_t p = lane % 5;
-    const float px_ = p == 0 ? ax : p == 1 ? bx : p == 2 ? cx : dx;
-    const float py_ = p == 0 ? ay : p == 1 ? by : p == 2 ? cy : dy;
-    const float pz_ = p == 0 ? az : p == 1 ? bz : p == 2 ? cz : dz;
-    const float qx = p == 0 ? bx : p == 1 ? cx : p == 2 ? dx : ax;
-    const float qy = p == 0 ? by : p == 1 ? cy : p == 2 ? dy : ay;
-    const float qz = p == 0 ? bz : p == 1 ? cz : p == 2 ? dz : az;
-    float nx = py_ * qz - pz_ * qy, ny = pz_ * qx - px_ * qz, nz = px_ * qy - py_ * qx;
-    const float mx = ax + cx, my = ay + cy, mz = az + cz;  // inside the cone
-    if (p == 4) {  // every corner direction has a positive component along M (narrow cone)
-        nx = mx;
-        ny = my;
-        nz = mz;
-    }
-    if (nx * mx + ny * my + nz * mz < 0.0f) {
-        nx = -nx;
-        ny = -ny;
-        nz = -nz;
-    }
-    const float vx = (nx >= 0.0f ? hi.x : lo.x) - fr.o[0];  // the box corner farthest along n
-    const float vy = (ny >= 0.0f ? hi.y : lo.y) - fr.o[1];
-    const float vz = (nz >= 0.0f ? hi.z : lo.z) - fr.o[2];
-    const float margin = 0x1p-12f * (fabsf(nx) + fabsf(ny) + fabsf(nz)) * fr.mag;
-    // an empty child slot counts as outside every plane
-    const bool outside = lo.w == 0.0f || nx * vx + ny * vy + nz * vz < -margin;
-    const uint64_t rej = __ballot(lane < 40 && outside);
-    uint32_t mask = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (!((rej >> (5 * k)) & 0x1full)) mask |= 1u << k;
-    return mask;
+    const bool meet = lane < 8 && fminf(s0, s1) <= r.y && fmaxf(s0, s1) >= r.x && fminf(t0, t1) <= r.w &&
+                      fmaxf(t0, t1) >= r.z;
+    return (uint32_t)__ballot(meet);
 }
 
 // ---------------------------------------------------------------- primary block
@@ -1021,7 +966,7 @@ template <bool REL, bool PREFILTER, bool BRUTE, bool COH>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
-                                              bool frustum = false, const float4* __restrict__ rootb = nullptr) {
+                                              bool frustum = false, const float4* __restrict__ frect = nullptr) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1029,7 +974,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
     const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
     const bool active = lx < vw && ly < vh;
-    if (frustum && block_frustum(wa.fr, rootb, px, py, vw, vh) == 0) {  // whole-block pre-test
+    if (frustum && block_frustum(wa.fr, frect, px, py, vw, vh) == 0) {  // whole-block pre-test
         ++ws.nodes;
         if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
             const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
@@ -1052,10 +997,11 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     }
     const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
 
-    // tracer.go:15-22 pixelToPoint (its two divisions, per column and per row, come from
-    // the host-built table: same fp64 operations), then tracer.go:86 (p - Cam.Pos).Norm()
-    const double si = wa.sij[i];
-    const double sj = wa.sij[fa.W + j];
+    // tracer.go:15-22 pixelToPoint with the reference's fp64 operations (computed, not
+    // loaded: a vector load here would wait for the previous block's stores, which share
+    // its in-order memory counter), then tracer.go:86 (p - Cam.Pos).Norm()
+    const double si = fa.phw * ((double)(fa.halfW - (int32_t)i) - 0.5) / (double)fa.halfW;
+    const double sj = fa.phh * ((double)(fa.halfH - (int32_t)j) - 0.5) / (double)fa.halfH;
     V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}), scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
                scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
     V3 d = norm(sub(p, cam));
@@ -1071,6 +1017,38 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
 
     const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
     const bool is_hit = active && nh.ok;
+    // hit slots first: the slot allocation's returning atomic is waited for before this
+    // block's output stores are issued (the wait would otherwise cover them too)
+    const uint64_t mask = __ballot(is_hit);
+    if (mask) {
+        ws.hits += __popcll(mask);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        const size_t slot = (size_t)q * wa.hit_cap + base + lane;
+        uint64_t* w = (uint64_t*)&wa.hits[slot];
+        if (is_hit) {
+            st64<COH>(w + 0, dbits(nh.hit.x));
+            st64<COH>(w + 1, dbits(nh.hit.y));
+            st64<COH>(w + 2, dbits(nh.hit.z));
+            st64<COH>(w + 3, dbits(nh.normal.x));
+            st64<COH>(w + 4, dbits(nh.normal.y));
+            st64<COH>(w + 5, dbits(nh.normal.z));
+            st64<COH>(w + 6, oidx);
+            st64<COH>(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
+            if (wa.bounces) vstore(wa.dir0 + 3 * slot, d);  // the reflect kernel's incoming D
+        } else {
+            st64<COH>(w + 7, (uint64_t)kNoHit);
+        }
+        st32<COH>(&wa.litw[slot], 0u);
+        if (lane == 0) st32<COH>(&wa.blkdone[slot / 64], 0u);
+        if (COH) {
+            // publish: every lane's stores are performed before the chunk is marked ready
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) st32<true>(&wa.rdy[slot / 64], wa.frame_tag);
+        }
+    }
     if (active) {
         if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
         if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
@@ -1087,38 +1065,6 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                 out.rgb8[3 * oidx + 2] = 0;
             }
         }
-    }
-    const uint64_t mask = __ballot(is_hit);
-    if (!mask) {
-        pc.lap(2);
-        return;
-    }
-    ws.hits += __popcll(mask);
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    const size_t slot = (size_t)q * wa.hit_cap + base + lane;
-    uint64_t* w = (uint64_t*)&wa.hits[slot];
-    if (is_hit) {
-        st64<COH>(w + 0, dbits(nh.hit.x));
-        st64<COH>(w + 1, dbits(nh.hit.y));
-        st64<COH>(w + 2, dbits(nh.hit.z));
-        st64<COH>(w + 3, dbits(nh.normal.x));
-        st64<COH>(w + 4, dbits(nh.normal.y));
-        st64<COH>(w + 5, dbits(nh.normal.z));
-        st64<COH>(w + 6, oidx);
-        st64<COH>(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
-        if (wa.bounces) vstore(wa.dir0 + 3 * slot, d);  // the reflect kernel's incoming D
-    } else {
-        st64<COH>(w + 7, (uint64_t)kNoHit);
-    }
-    st32<COH>(&wa.litw[slot], 0u);
-    if (lane == 0) st32<COH>(&wa.blkdone[slot / 64], 0u);
-    if (COH) {
-        // publish: every lane's stores are performed before the chunk is marked ready
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) st32<true>(&wa.rdy[slot / 64], wa.frame_tag);
     }
     pc.lap(2);
 }
@@ -1203,7 +1149,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
-    __shared__ float4 rootb[16];
+    __shared__ float4 frect[8];  // frustum rectangles
     WaveClock clock;
     uint32_t taken = 0;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1211,7 +1157,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
     const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;
-    if (use_frustum) stage_root_boxes(rootb, fa.obj[0].m);
+    if (use_frustum) stage_frustum(frect, wa.fr);
     if (RESIDENT) {
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
@@ -1221,25 +1167,30 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     WaveStats ws{0, 0, 0, 0, 0};
     PhaseClock pc;
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        cnt_t* qc = &wa.counters[cnt_queue(0, q)];
-        const uint32_t count = shard_items(wa.nblocks, q), peers = sc.peers();
-        // Blocks rank and rank + peers of the shard are this wave's (static split, no
-        // atomics on the way in); with the queue on, blocks 2 peers + ticket follow.  The
-        // pipeline is two deep: when block k starts, the next one is already known and its
-        // descriptor is fetched (scalar loads, no wait) while block k is traced.
-        const bool dyn = (wa.dynamic & kDynPrimary) && count > 2 * peers;
-        uint32_t k = sc.rank(), kn = k + peers;
-        BlockDesc bd = block_desc(wa, q, k);
-        while (k < count) {
-            const uint32_t t2 = dyn ? ticket_issue(qc) : 0;
-            const BlockDesc nbd = block_desc(wa, q, kn);  // scalar loads, used next iteration
-            ++taken;
-            primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd, q,
-                                                             ws, pc, use_frustum, rootb);
-            k = kn;
-            bd = nbd;
-            kn = dyn ? 2 * peers + ticket_resolve(t2) : kn + peers;
-            pc.lap(3);
+        // Static split: blocks rank, rank + peers, ... of the shard (blocks are even enough
+        // that queue tickets cost more than they balance).  The wave's descriptors arrive
+        // with ONE vector load, lane L holding its (base + L)-th block, and are read out
+        // with v_readlane: no per-block memory round trip (a scalar load would be waited
+        // for at the block's first LDS access, which shares its counter).
+        const uint32_t count = shard_items(wa.nblocks, q);
+        const uint32_t peers = __builtin_amdgcn_readfirstlane(sc.peers());
+        const uint32_t rank = __builtin_amdgcn_readfirstlane(sc.rank());
+        const uint32_t mine = rank < count ? (count - rank + peers - 1) / peers : 0u;  // this wave's blocks
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint32_t b0 = 0; b0 < mine; b0 += 64) {
+            const uint32_t kl = rank + (b0 + lane) * peers;
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (b0 + lane < mine) v = ((const u32x4*)wa.blocks)[(size_t)q * wa.per_shard + kl];
+            const uint32_t nb = min(mine - b0, 64u);
+            for (uint32_t j = 0; j < nb; ++j) {
+                const BlockDesc bd{(uint32_t)__builtin_amdgcn_readlane((int)v[0], (int)j),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)v[1], (int)j),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)v[2], (int)j), 0u};
+                ++taken;
+                primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd,
+                                                                 q, ws, pc, use_frustum, frect);
+                pc.lap(3);
+            }
         }
     }
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);

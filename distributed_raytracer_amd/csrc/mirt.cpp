@@ -49,6 +49,7 @@ struct MeshDev {
     double* mats = nullptr;
     uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
+    Bvh8Node root{};     // host copy of the BVH root (frustum pre-test rectangles)
     bool has_normals = false;
     bool live = false;
 };
@@ -85,11 +86,6 @@ struct Slot {
     uint32_t unpack_key_H = 0;
     uint32_t blocks_W = 0, blocks_H = 0, nblocks = 0, per_shard = 0;
     // pixelToPoint per column / per row (tracer.go:19-20), cached per (fov, W, H)
-    double* d_sij = nullptr;
-    double* h_sij = nullptr;  // pinned staging
-    size_t sij_cap = 0, h_sij_cap = 0;
-    double sij_phw = 0, sij_phh = 0;
-    uint32_t sij_W = 0, sij_H = 0;
     cnt_t* summary = nullptr;     // kStatN totals of the last frame (device)
     cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
     bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
@@ -281,27 +277,83 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         }
 }
 
-// Constants of the primary kernel's whole-block frustum pre-test (kernels.hip
-// block_frustum), from the same fp64 values the kernel's rays are built from.
-void frustum_args(const mirt_ctx* c, const FrameArgs& fa, FrustumArgs& fr) {
+// Rectangles of the primary kernel's whole-block frustum pre-test (mirt_internal.hpp
+// FrustumArgs).  With R the inverse of the basis matrix [fwd left up], a point X (object
+// space, relative to the camera) lies on the ray of (s, t) at parameter z = R0.X > 0 iff
+// s = R1.X / z and t = R2.X / z.  A box entirely in front of the camera (every corner at
+// z > 2^-20 |X|) projects into the bounding rectangle of its corners' (s, t); a box
+// entirely behind it (z < 0 everywhere: rays start at z = 0) is never met; anything else
+// is always tested.  Hits lie inside the inflated boxes, and the margin
+// covers the fp64 rounding of this projection and of the kernels' rays.
+void frustum_args(const mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa, FrustumArgs& fr) {
     memset(&fr, 0, sizeof(fr));
     if (fa.n_objects != 1 || (c->flags & (MIRT_OPT_NO_FRUSTUM | MIRT_OPT_BRUTE_FORCE)) || fa.halfW < 1 ||
         fa.halfH < 1)
         return;
     const DevObject& ob = fa.obj[0];
-    double o[3], far = 0.0;
+    const MeshDev& md = c->meshes[f->objects[0].mesh_id];
+    double o[3], far = 0.0, big = 0.0;
     for (int k = 0; k < 3; ++k) {
         o[k] = fa.cam[k] - ob.pos[k];
         far = std::max(far, std::fabs(o[k]));
+        big = std::max({big, std::fabs(fa.cam[k]), std::fabs(ob.pos[k])});
     }
-    if (!(far <= ob.m.cull_limit)) return;  // also: cull_limit < 0 (culling off)
-    for (int k = 0; k < 3; ++k) {
-        fr.o[k] = (float)o[k];
-        fr.f[k] = (float)fa.fwd[k];
-        fr.l[k] = (float)fa.left[k];
-        fr.u[k] = (float)fa.up[k];
+    // culling off, or a camera so far out that the rays' own rounding could approach the margin
+    if (!(far <= ob.m.cull_limit) || !(big <= 0x1p30)) return;
+    const double F[3] = {fa.fwd[0], fa.fwd[1], fa.fwd[2]}, L[3] = {fa.left[0], fa.left[1], fa.left[2]},
+                 U[3] = {fa.up[0], fa.up[1], fa.up[2]};
+    // R = [F L U]^-1 by cofactors: row k of R is (column k+1 x column k+2) / det
+    auto cross3 = [](const double* a, const double* b, double* r) {
+        r[0] = a[1] * b[2] - a[2] * b[1];
+        r[1] = a[2] * b[0] - a[0] * b[2];
+        r[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    double R[3][3];
+    cross3(L, U, R[0]);
+    cross3(U, F, R[1]);
+    cross3(F, L, R[2]);
+    const double det = F[0] * R[0][0] + F[1] * R[0][1] + F[2] * R[0][2];
+    if (!(std::fabs(det) > 0.5) || !std::isfinite(det)) return;  // not a (near-)orthonormal camera basis
+    for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a) R[k][a] /= det;
+    const Bvh8Node& root = md.root;
+    for (int ch = 0; ch < 8; ++ch) {
+        float* r = fr.rect[ch];
+        r[0] = r[2] = INFINITY;  // empty: no (s, t) satisfies lo <= x <= hi
+        r[1] = r[3] = -INFINITY;
+        if (root.child[ch] == kBvhEmpty) continue;
+        double slo = INFINITY, shi = -INFINITY, tlo = INFINITY, thi = -INFINITY;
+        int front = 0, behind = 0;
+        for (int k = 0; k < 8; ++k) {
+            const double X[3] = {(double)((k & 1) ? root.hi(0, ch) : root.lo(0, ch)) - o[0],
+                                 (double)((k & 2) ? root.hi(1, ch) : root.lo(1, ch)) - o[1],
+                                 (double)((k & 4) ? root.hi(2, ch) : root.lo(2, ch)) - o[2]};
+            const double mag = std::max({std::fabs(X[0]), std::fabs(X[1]), std::fabs(X[2])});
+            const double z = R[0][0] * X[0] + R[0][1] * X[1] + R[0][2] * X[2];
+            if (z > 0x1p-20 * mag) {
+                ++front;
+                const double s = (R[1][0] * X[0] + R[1][1] * X[1] + R[1][2] * X[2]) / z;
+                const double t = (R[2][0] * X[0] + R[2][1] * X[1] + R[2][2] * X[2]) / z;
+                slo = std::min(slo, s);
+                shi = std::max(shi, s);
+                tlo = std::min(tlo, t);
+                thi = std::max(thi, t);
+            } else if (z < 0.0) {
+                ++behind;
+            }
+        }
+        if (behind == 8) continue;  // never met
+        if (front < 8 || !(std::fabs(slo) + std::fabs(shi) + std::fabs(tlo) + std::fabs(thi) < 0x1p60)) {
+            r[0] = r[2] = -INFINITY;  // always tested
+            r[1] = r[3] = INFINITY;
+            continue;
+        }
+        auto widen = [](double x) { return 0x1p-18 * (1.0 + std::fabs(x)); };
+        r[0] = detail::round_down(slo - widen(slo));
+        r[1] = detail::round_up(shi + widen(shi));
+        r[2] = detail::round_down(tlo - widen(tlo));
+        r[3] = detail::round_up(thi + widen(thi));
     }
-    fr.mag = (float)(far + 4.0 * (ob.m.cull_limit * (1.0 / 256.0)) + 1.0);
     fr.sA = fa.phw / (double)fa.halfW;
     fr.sB = fa.phw * ((double)fa.halfW - 0.5) / (double)fa.halfW;
     fr.tA = fa.phh / (double)fa.halfH;
@@ -367,32 +419,6 @@ int blocks_prepare(Slot* sl, uint32_t W, uint32_t H, const mirt_tile* tiles, uin
     return MIRT_OK;
 }
 
-// tracer.go:16-20 per column and per row: sx = phw * (float64(halfW - i) - 0.5) /
-// float64(halfW) (and sy likewise), the same fp64 operations the reference does per pixel.
-int sij_prepare(Slot* sl, const FrameArgs& fa, hipStream_t s) {
-    const uint32_t W = (uint32_t)fa.W, H = (uint32_t)fa.H;
-    if (sl->sij_W == W && sl->sij_H == H && sl->sij_phw == fa.phw && sl->sij_phh == fa.phh) return MIRT_OK;
-    const size_t n = (size_t)W + H;
-    int r = dev_grow(sl->d_sij, sl->sij_cap, n);
-    if (r != MIRT_OK) return r;
-    if (sl->h_sij_cap < n) {
-        if (sl->h_sij) (void)hipHostFree(sl->h_sij);
-        sl->h_sij = nullptr;
-        sl->h_sij_cap = 0;
-        HIP_TRY(hipHostMalloc((void**)&sl->h_sij, sizeof(double) * n));
-        sl->h_sij_cap = n;
-    }
-    for (uint32_t i = 0; i < W; ++i) sl->h_sij[i] = fa.phw * ((double)(fa.halfW - (int32_t)i) - 0.5) / (double)fa.halfW;
-    for (uint32_t j = 0; j < H; ++j)
-        sl->h_sij[W + j] = fa.phh * ((double)(fa.halfH - (int32_t)j) - 0.5) / (double)fa.halfH;
-    HIP_TRY(hipMemcpyAsync(sl->d_sij, sl->h_sij, sizeof(double) * n, hipMemcpyHostToDevice, s));
-    sl->sij_W = W;
-    sl->sij_H = H;
-    sl->sij_phw = fa.phw;
-    sl->sij_phh = fa.phh;
-    return MIRT_OK;
-}
-
 // Enqueue primary -> shadow -> shade for a tile list on stream s.
 int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
                   uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel, uint64_t* pixels_out,
@@ -414,11 +440,9 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     uint64_t tris = 0;
     fill_args(c, f, W, H, fa, tris);
     if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
-    if ((r = sij_prepare(sl, fa, s)) != MIRT_OK) return r;
     const uint32_t nl = f->n_lights;
     WorkArgs wa{};
     wa.blocks = sl->d_blocks;
-    wa.sij = sl->d_sij;
     wa.nblocks = sl->nblocks;
     wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
@@ -449,10 +473,10 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.counters = sl->counters + (size_t)sl->parity * kCntN;
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
-    frustum_args(c, fa, wa.fr);
+    frustum_args(c, f, fa, wa.fr);
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
                      ? 0u
-                     : (uint32_t)(kDynShadow | kDynReflect | ((c->flags & MIRT_OPT_DYNAMIC_PRIMARY) ? kDynPrimary : 0));
+                     : (uint32_t)(kDynShadow | kDynReflect);
     if (c->flags & MIRT_OPT_TIMELINE) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->timeline) {
@@ -570,8 +594,6 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->counters) (void)hipFree(s->counters);
         if (s->d_tiles) (void)hipFree(s->d_tiles);
         if (s->d_blocks) (void)hipFree(s->d_blocks);
-        if (s->d_sij) (void)hipFree(s->d_sij);
-        if (s->h_sij) (void)hipHostFree(s->h_sij);
         if (s->h_blocks) (void)hipHostFree(s->h_blocks);
         if (s->h_tiles) (void)hipHostFree(s->h_tiles);
         if (s->summary) (void)hipFree(s->summary);
@@ -709,6 +731,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     md.nmat = nm;
     md.has_normals = has_n;
     md.nnodes = (uint32_t)bvh.nodes.size();
+    md.root = bvh.nodes[0];
     md.depth = bvh.depth;
     md.scale = scale;
     auto upload = [&](void** dst, const void* src, size_t bytes) -> int {

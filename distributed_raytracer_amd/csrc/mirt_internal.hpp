@@ -36,6 +36,8 @@ struct alignas(64) Bvh8Node {
     uint32_t pad[8];
     float& lo(int a, int c) { return box[a][c][0]; }
     float& hi(int a, int c) { return box[a][c][1]; }
+    float lo(int a, int c) const { return box[a][c][0]; }
+    float hi(int a, int c) const { return box[a][c][1]; }
 };
 constexpr uint32_t kBvhEmpty = 0xffffffffu;
 constexpr uint32_t kBvhLeafBit = 0x80000000u;
@@ -163,19 +165,22 @@ __host__ __device__ constexpr int cnt_pdone(int q) {
 constexpr int kCntN = ((kQueues + 2) * kQShards + kStatN * kStatShards + kStatShards + 1) * kLine;
 typedef unsigned long long cnt_t;
 
-// Block frustum pre-test of one-object frames (kernels.hip block_frustum): per-frame
-// constants computed on the host with the kernel's fp64 operations, then rounded to fp32.
+// Block frustum pre-test of one-object frames (kernels.hip block_frustum).  A primary
+// ray of pixel (i, j) has direction fwd + left s_i + up t_j (tracer.go:19-21), so a ray
+// can only meet a root child box if (s_i, t_j) lies in the box's projection onto that
+// (s, t) plane.  The host projects each root child box per frame in fp64 and rounds the
+// rectangle outward with a relative margin of 2^-18; the kernel tests a block's range of
+// s and t against the 8 rectangles.
 struct FrustumArgs {
-    float o[3], mag;       // camera in object space (cam - pos); max|o| + 4 scale + 1
-    float f[3], l[3], u[3];
-    uint32_t on;           // one object, culling on, origin within cull_limit, W, H >= 2
-    double sA, sB, tA, tB; // tracer.go:19-20 as affine maps: sij[i] ~ sB - sA i, sij[W + j] ~ tB - tA j
+    float rect[8][4];      // per root child: s_lo, s_hi, t_lo, t_hi (empty child: an empty rectangle)
+    double sA, sB, tA, tB; // tracer.go:19-20 offsets as affine maps: column i ~ sB - sA i, row j ~ tB - tA j
+    uint32_t on;           // one object, culling on, bounded camera, W, H >= 2
+    uint32_t pad;
 };
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
 struct WorkArgs {
     const BlockDesc* blocks;
-    const double* sij;     // tracer.go:19-20 per column (W values) then per row (H values)
     uint32_t nblocks;
     uint32_t per_shard;    // BlockDesc entries per shard (ceil(nblocks / kQShards))
     uint32_t hit_cap;      // records per hit region (multiple of 64)
@@ -197,10 +202,8 @@ struct WorkArgs {
     cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
 };
 constexpr int kTimelineRec = 8;
-// WorkArgs::dynamic.  Measured on MI355X: the primary kernel's blocks are even enough for
-// a static round-robin split (the ticket atomics cost more than they balance), the shadow
-// and reflect kernels' items are not.
-enum { kDynPrimary = 1, kDynShadow = 2, kDynReflect = 4 };
+// WorkArgs::dynamic (the primary kernel always splits its blocks statically).
+enum { kDynShadow = 2, kDynReflect = 4 };
 
 // Arbitrary-ray inputs/outputs for mirt_trace_rays.
 struct RayIO {

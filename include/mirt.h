@@ -229,7 +229,6 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
 #define MIRT_OPT_ONE_KERNEL 32u     /* one k_trace launch per frame (default: primary, then shadow+shade) */
 #define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
-#define MIRT_OPT_DYNAMIC_PRIMARY 128u /* primary blocks from the work queues (default: static split) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 
 /*

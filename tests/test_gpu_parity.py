@@ -78,7 +78,7 @@ def _variants(ctx, fn):
                      rt._lib.MIRT_OPT_BRUTE_FORCE | rt._lib.MIRT_OPT_NO_PREFILTER,
                      rt._lib.MIRT_OPT_STATIC_SCHEDULE, rt._lib.MIRT_OPT_NO_SEGMENT,
                      rt._lib.MIRT_OPT_ONE_KERNEL, rt._lib.MIRT_OPT_ONE_KERNEL | rt._lib.MIRT_OPT_BRUTE_FORCE,
-                     rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_DYNAMIC_PRIMARY):
+                     rt._lib.MIRT_OPT_NO_FRUSTUM):
             ctx.set_options(opts)
             out[opts] = fn()
     finally:
@@ -118,6 +118,35 @@ def test_bvh_equals_brute_force_many_cameras_1080p(ctx, env):
             res[opts] = rt.draw(env, 1920, 1080, mut)
         ctx.set_options(0)
         assert res[0].valid.sum() > 10000
+        _same_frames(res)
+
+
+def test_block_frustum_exact_at_awkward_cameras(ctx, env):
+    """The whole-block frustum pre-test (projected root-child rectangles) never changes a
+    pixel: cameras inside the mesh's bounds, grazing the surface, with the object half
+    behind the camera or cut by the screen edge, very narrow and very wide fields of view,
+    odd frame sizes.  Default kernels vs the pre-test off vs brute force, bit-for-bit."""
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    c0 = np.array([1.0, 1.0, -1.0])  # suzanne's position in example/scene.json
+    cases = [  # (pos, look direction, fov, W, H)
+        (c0 + [0.0, 0.0, 0.1], [0.0, 0.0, -1.0], 1.2, 200, 150),       # inside the bounding box
+        (c0 + [0.0, 0.2, 0.0], [0.3, -1.0, 0.2], 1.6, 161, 97),        # inside, looking down
+        (c0 + [0.0, 0.0, 1.05], [0.0, 0.0, -1.0], 1.0, 240, 136),      # grazing the face
+        (c0 + [0.0, 0.0, 0.9], [1.0, 0.0, 0.05], 1.3, 240, 136),       # object beside / behind
+        (c0 + [3.0, 0.5, 3.0], [-0.2, -0.1, -1.0], 0.9, 320, 180),     # cut by the screen edge
+        (c0 + [0.5, 0.3, 6.0], [-0.08, -0.05, -1.0], 0.06, 256, 256),  # very narrow field of view
+        (c0 + [0.0, 0.0, 1.6], [0.0, 0.0, -1.0], 2.9, 300, 120),       # very wide field of view
+        (c0 + [0.0, 6.0, 0.0], [0.0, -1.0, 0.001], 1.0, 2, 2),         # 2x2 frame
+    ]
+    for pos, look, fov, W, H in cases:
+        cam = rt.Camera.new(tuple(pos), tuple(look), fov)
+        mut = rt.EnvMutables(base.objects, base.lights, cam)
+        res = {}
+        for opts in (0, rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_BRUTE_FORCE):
+            ctx.set_options(opts)
+            res[opts] = rt.draw(env, W, H, mut)
+        ctx.set_options(0)
         _same_frames(res)
 
 

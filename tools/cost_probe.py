@@ -2,8 +2,10 @@
 suzanne scene (1 GPU): the camera turned away (every ray misses: raygen, root test and
 outputs only), the default view, and a close-up (mesh fills the screen).
 
-usage (GPU box): python tools/cost_probe.py
+usage (GPU box): python tools/cost_probe.py [--repeat N] [--views default,away] [--opts default,static]
+Each (view, options) pair is timed N times (interleaved); the minimum is reported.
 """
+import argparse
 import json
 import os
 import sys
@@ -15,6 +17,11 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--views", default="")
+    ap.add_argument("--opts", default="")
+    a = ap.parse_args()
     import torch
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd.framebuffer import FrameSharder
@@ -29,34 +36,40 @@ def main():
                                  tuple(np.array([1.0, 1.0, -1.0]) - np.asarray(cam.pos)), cam.fov),
     }
     opts = {"default": 0, "static": rt._lib.MIRT_OPT_STATIC_SCHEDULE, "no_frustum": rt._lib.MIRT_OPT_NO_FRUSTUM,
-            "dyn_primary": rt._lib.MIRT_OPT_DYNAMIC_PRIMARY,
             "one_kernel": rt._lib.MIRT_OPT_ONE_KERNEL}
+    if a.views:
+        views = {k: views[k] for k in a.views.split(",")}
+    if a.opts:
+        opts = {k: opts[k] for k in a.opts.split(",")}
     sh = FrameSharder(ctx, 1920, 1080, 0, 1, 64)
     out = {}
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
-        for vname, c in views.items():
-            mut = rt.EnvMutables(base.objects, base.lights, c)
-            frame = mut.to_frame()
-            for oname, o in opts.items():
-                ctx.set_options(o)
-                for _ in range(5):
-                    sh.render(frame)
-                torch.cuda.synchronize()
-                ctx.profile_enable(True)
-                for _ in range(30):
-                    sh.render(frame)
-                torch.cuda.synchronize()
-                ctx.profile_enable(False)
-                p = ctx.profile_read()
-                n = max(p["launches"], 1)
-                out[f"{vname}/{oname}"] = {
-                    "primary_us": round(p["primary_ms_sum"] / n * 1e3, 1),
-                    "shadow_us": round(p["shadow_ms_sum"] / n * 1e3, 1),
-                    "frame_us": round(p["frame_ms_sum"] / n * 1e3, 1),
-                    "hits": p["hits"] // n,
-                    "prim_nodes": p["primary_node_visits"] // n, "prim_leaves": p["primary_leaf_visits"] // n,
-                    "prim_tests": p["primary_tri_tests"] // n, "shadow_tests": p["shadow_tri_tests"] // n}
+        for _ in range(a.repeat):
+            for vname, c in views.items():
+                mut = rt.EnvMutables(base.objects, base.lights, c)
+                frame = mut.to_frame()
+                for oname, o in opts.items():
+                    ctx.set_options(o)
+                    for _ in range(5):
+                        sh.render(frame)
+                    torch.cuda.synchronize()
+                    ctx.profile_enable(True)
+                    for _ in range(30):
+                        sh.render(frame)
+                    torch.cuda.synchronize()
+                    ctx.profile_enable(False)
+                    p = ctx.profile_read()
+                    n = max(p["launches"], 1)
+                    prev = out.get(f"{vname}/{oname}", {})
+                    best = lambda key, v: round(min(v, prev.get(key, v)), 1)
+                    out[f"{vname}/{oname}"] = {
+                        "primary_us": best("primary_us", p["primary_ms_sum"] / n * 1e3),
+                        "shadow_us": best("shadow_us", p["shadow_ms_sum"] / n * 1e3),
+                        "frame_us": best("frame_us", p["frame_ms_sum"] / n * 1e3),
+                        "hits": p["hits"] // n,
+                        "prim_nodes": p["primary_node_visits"] // n, "prim_leaves": p["primary_leaf_visits"] // n,
+                        "prim_tests": p["primary_tri_tests"] // n, "shadow_tests": p["shadow_tri_tests"] // n}
             ctx.set_options(0)
     for k, v in out.items():
         print(k, json.dumps(v))
