@@ -458,6 +458,12 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
 #ifndef MIRT_BLOCK_FRUSTUM
 #define MIRT_BLOCK_FRUSTUM 1
 #endif
+#ifndef MIRT_EXP_NO_PHONG  // measurement builds only: ambient colour only
+#define MIRT_EXP_NO_PHONG 0
+#endif
+#ifndef MIRT_EXP_NO_SHADOW_TRACE  // measurement builds only: every light reaches every hit
+#define MIRT_EXP_NO_SHADOW_TRACE 0
+#endif
 #ifndef MIRT_SKIP_MISS_STORES  // measurement builds only (outputs left unwritten)
 #define MIRT_SKIP_MISS_STORES 0
 #endif
@@ -791,7 +797,7 @@ __device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restri
     const double ns = mt[9];
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     RGB col = ka;  // tracer.go:56
-    for (uint32_t l = 0; l < fa.n_lights; ++l) {
+    for (uint32_t l = 0; l < (MIRT_EXP_NO_PHONG ? 0u : fa.n_lights); ++l) {
         if (!((lit >> l) & 1u)) continue;
         const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
         const RGB lcol{fa.lcol[l][0], fa.lcol[l][1], fa.lcol[l][2]};
@@ -1095,6 +1101,8 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     bool is_lit = false;
     if (fa.n_lights == 0) {
         // no lights: nothing to trace, the pass only shades (ambient)
+    } else if (MIRT_EXP_NO_SHADOW_TRACE) {
+        is_lit = true;
     } else if (segment) {
         is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis);
     } else {
@@ -1150,10 +1158,11 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
     __shared__ float4 frect[8];  // frustum rectangles
+    __shared__ uint32_t bq[kBlkQ][3];  // this workgroup's block descriptors (out, pxy, geo)
+    __shared__ uint32_t bq_next;
     WaveClock clock;
     uint32_t taken = 0;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    const ShardCursor sc;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
     const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;
@@ -1162,36 +1171,52 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
         const DevObject& ob = fa.obj[0];
         stage_tris<true>(lds, ob.m.tri, 0, ob.m.ntri, sub(cam, V3{ob.pos[0], ob.pos[1], ob.pos[2]}));
     }
-    if (RESIDENT || use_frustum) __syncthreads();
-    clock.mark_staged();
     WaveStats ws{0, 0, 0, 0, 0};
     PhaseClock pc;
-    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        // Static split: blocks rank, rank + peers, ... of the shard (blocks are even enough
-        // that queue tickets cost more than they balance).  The wave's descriptors arrive
-        // with ONE vector load, lane L holding its (base + L)-th block, and are read out
-        // with v_readlane: no per-block memory round trip (a scalar load would be waited
-        // for at the block's first LDS access, which shares its counter).
-        const uint32_t count = shard_items(wa.nblocks, q);
-        const uint32_t peers = __builtin_amdgcn_readfirstlane(sc.peers());
-        const uint32_t rank = __builtin_amdgcn_readfirstlane(sc.rank());
-        const uint32_t mine = rank < count ? (count - rank + peers - 1) / peers : 0u;  // this wave's blocks
-        const uint32_t lane = threadIdx.x & 63;
-        for (uint32_t b0 = 0; b0 < mine; b0 += 64) {
-            const uint32_t kl = rank + (b0 + lane) * peers;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (b0 + lane < mine) v = ((const u32x4*)wa.blocks)[(size_t)q * wa.per_shard + kl];
-            const uint32_t nb = min(mine - b0, 64u);
-            for (uint32_t j = 0; j < nb; ++j) {
-                const BlockDesc bd{(uint32_t)__builtin_amdgcn_readlane((int)v[0], (int)j),
-                                   (uint32_t)__builtin_amdgcn_readlane((int)v[1], (int)j),
-                                   (uint32_t)__builtin_amdgcn_readlane((int)v[2], (int)j), 0u};
-                ++taken;
-                primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, bd,
-                                                                 q, ws, pc, use_frustum, frect);
-                pc.lap(3);
+    // Workgroup w owns blocks w, w + G, w + 2G, ... (G = grid size): a regular lattice over
+    // the frame, so every workgroup gets about the same share of the object's footprint.
+    // Its descriptors are staged in LDS (kBlkQ at a time) and its waves take them with an
+    // LDS ticket: block costs differ by orders of magnitude (culled or not, hit or not), and
+    // an LDS atomic balances them without touching the vector memory counter.
+    // MIRT_OPT_STATIC_SCHEDULE: wave v of the workgroup takes entries v, v + 8, ... instead.
+    const uint32_t G = gridDim.x, wave = threadIdx.x >> 6;
+    const uint32_t mine = wa.nblocks > blockIdx.x ? (wa.nblocks - blockIdx.x + G - 1) / G : 0u;
+    const bool dyn = (wa.dynamic & kDynPrimary) != 0;
+    for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
+        const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
+        for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
+            const uint32_t b = blockIdx.x + (c0 + t) * G;
+            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(b % kQShards) * wa.per_shard + b / kQShards];
+            bq[t][0] = v[0];
+            bq[t][1] = v[1];
+            bq[t][2] = v[2];
+        }
+        if (threadIdx.x == 0) bq_next = kWG / 64;  // entries 0..7 go to waves 0..7 without a ticket
+        if (c0 == 0) clock.mark_staged();
+        __syncthreads();
+        uint32_t t = wave;
+        while (t < nc) {
+            const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
+            const uint32_t b = blockIdx.x + (c0 + t) * G;
+            ++taken;
+            primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws,
+                                                             pc, use_frustum, frect);
+            pc.lap(3);
+            if (dyn) {
+                uint32_t nt = 0;
+                if ((threadIdx.x & 63) == 0) nt = atomicAdd(&bq_next, 1u);
+                t = __builtin_amdgcn_readfirstlane(nt);
+            } else {
+                t += kWG / 64;
             }
         }
+        __syncthreads();  // every wave is done with this batch before it is restaged
+    }
+    if (mine == 0) {
+        __syncthreads();
+        clock.mark_staged();
     }
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
     if (MIRT_PHASE_TIMING) {  // record [4], [5], [6] = cycles in setup+raygen, trace, outputs

@@ -476,7 +476,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     frustum_args(c, f, fa, wa.fr);
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
                      ? 0u
-                     : (uint32_t)(kDynShadow | kDynReflect);
+                     : (uint32_t)(kDynPrimary | kDynShadow | kDynReflect);
     if (c->flags & MIRT_OPT_TIMELINE) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->timeline) {

@@ -202,8 +202,10 @@ struct WorkArgs {
     cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
 };
 constexpr int kTimelineRec = 8;
-// WorkArgs::dynamic (the primary kernel always splits its blocks statically).
-enum { kDynShadow = 2, kDynReflect = 4 };
+// WorkArgs::dynamic: kernels whose waves take work items dynamically (primary: LDS tickets
+// within the workgroup; shadow / reflect: the sharded device queues).
+enum { kDynPrimary = 1, kDynShadow = 2, kDynReflect = 4 };
+constexpr int kBlkQ = 256;  // primary block descriptors staged in LDS per batch
 
 // Arbitrary-ray inputs/outputs for mirt_trace_rays.
 struct RayIO {
