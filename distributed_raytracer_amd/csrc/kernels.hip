@@ -908,28 +908,10 @@ __device__ __forceinline__ uint32_t shard_items(uint32_t n, uint32_t q) {
 }
 
 // ---------------------------------------------------------------- hit slots
-// A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.  COH: device-scope
-// atomic stores / loads (coherent across the XCDs' L2s without cache flushes), used when
-// the producer and the consumer of a slot run in the same kernel (k_trace).
-template <bool COH>
-__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
-    if (COH)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
-template <bool COH>
-__device__ __forceinline__ uint64_t ld64(const uint64_t* p) {
-    if (COH) return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return *p;
-}
-template <bool COH>
-__device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
-    if (COH)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
+// A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.
+__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) { *p = v; }
+__device__ __forceinline__ uint64_t ld64(const uint64_t* p) { return *p; }
+__device__ __forceinline__ void st32(uint32_t* p, uint32_t v) { *p = v; }
 __device__ __forceinline__ double bitsd(uint64_t x) { return __longlong_as_double((long long)x); }
 
 // Descriptor of block k of shard q (shard-major table; scalar load; zero if past the end).
@@ -968,11 +950,19 @@ __device__ __forceinline__ uint32_t block_frustum(const FrustumArgs& fr, const f
 // One 8x8 pixel block: raygen (tracer.go:15-22, :86), nearest hit, outputs of misses,
 // and, if any lane hit, 64 hit slots of region q (slot = lane) with their lit word and
 // the block's light counter zeroed.  REL: the LDS mesh is stored relative to the camera.
-template <bool REL, bool PREFILTER, bool BRUTE, bool COH>
+// Hit chunks of a workgroup-local region (k_trace): LDS allocation counter and ready
+// flags, slot index of the region's chunk 0.
+struct LocalChunks {
+    uint32_t* count;
+    uint32_t* ready;
+    size_t base;
+};
+template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
-                                              bool frustum = false, const float4* __restrict__ frect = nullptr) {
+                                              bool frustum = false, const float4* __restrict__ frect = nullptr,
+                                              const LocalChunks* lc = nullptr) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1029,30 +1019,31 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     if (mask) {
         ws.hits += __popcll(mask);
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
+        if (lane == 0) base = lc ? atomicAdd(lc->count, 1u) : atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
         base = __builtin_amdgcn_readfirstlane(base);
-        const size_t slot = (size_t)q * wa.hit_cap + base + lane;
+        const size_t slot = lc ? lc->base + (size_t)base * 64 + lane : (size_t)q * wa.hit_cap + base + lane;
         uint64_t* w = (uint64_t*)&wa.hits[slot];
         if (is_hit) {
-            st64<COH>(w + 0, dbits(nh.hit.x));
-            st64<COH>(w + 1, dbits(nh.hit.y));
-            st64<COH>(w + 2, dbits(nh.hit.z));
-            st64<COH>(w + 3, dbits(nh.normal.x));
-            st64<COH>(w + 4, dbits(nh.normal.y));
-            st64<COH>(w + 5, dbits(nh.normal.z));
-            st64<COH>(w + 6, oidx);
-            st64<COH>(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
+            st64(w + 0, dbits(nh.hit.x));
+            st64(w + 1, dbits(nh.hit.y));
+            st64(w + 2, dbits(nh.hit.z));
+            st64(w + 3, dbits(nh.normal.x));
+            st64(w + 4, dbits(nh.normal.y));
+            st64(w + 5, dbits(nh.normal.z));
+            st64(w + 6, oidx);
+            st64(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
             if (wa.bounces) vstore(wa.dir0 + 3 * slot, d);  // the reflect kernel's incoming D
         } else {
-            st64<COH>(w + 7, (uint64_t)kNoHit);
+            st64(w + 7, (uint64_t)kNoHit);
         }
-        st32<COH>(&wa.litw[slot], 0u);
-        if (lane == 0) st32<COH>(&wa.blkdone[slot / 64], 0u);
-        if (COH) {
-            // publish: every lane's stores are performed before the chunk is marked ready
+        st32(&wa.litw[slot], 0u);
+        if (lane == 0) st32(&wa.blkdone[slot / 64], 0u);
+        if (lc) {
+            // publish to the workgroup: the chunk's stores have reached L2 (shared by every
+            // wave of this CU) before its ready flag is raised in LDS
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) st32<true>(&wa.rdy[slot / 64], wa.frame_tag);
+            if (lane == 0) __hip_atomic_store(&lc->ready[base], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     if (active) {
@@ -1079,20 +1070,20 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
 // the wave that finishes the chunk's last light.  n_lights == 0: one pass that shades.
-template <bool PREFILTER, bool BRUTE, bool COH>
+template <bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
-                                            bool segment, uint32_t q, uint32_t c, uint32_t l, WaveStats& ws) {
+                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
-    const size_t slot = (size_t)q * wa.hit_cap + (size_t)c * 64 + lane;
+    const size_t slot = chunk + lane;
     const uint64_t* w = (const uint64_t*)&wa.hits[slot];
-    const uint64_t w7 = ld64<COH>(w + 7);
+    const uint64_t w7 = ld64(w + 7);
     const bool active = (uint32_t)w7 != kNoHit;
     V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
     const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
     if (active) {
-        hit = V3{bitsd(ld64<COH>(w)), bitsd(ld64<COH>(w + 1)), bitsd(ld64<COH>(w + 2))};
+        hit = V3{bitsd(ld64(w)), bitsd(ld64(w + 1)), bitsd(ld64(w + 2))};
         V3 ldir = norm(sub(lpos, hit));     // tracer.go:61
         o = add(hit, scale(ldir, 0.0001));  // tracer.go:64
         d = ldir;
@@ -1127,8 +1118,8 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     done = __builtin_amdgcn_readfirstlane(done);
     if (done != nl - 1 || !active) return;
     const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
-    const V3 n{bitsd(ld64<COH>(w + 3)), bitsd(ld64<COH>(w + 4)), bitsd(ld64<COH>(w + 5))};
-    const uint64_t oidx = ld64<COH>(w + 6);
+    const V3 n{bitsd(ld64(w + 3)), bitsd(ld64(w + 4)), bitsd(ld64(w + 5))};
+    const uint64_t oidx = ld64(w + 6);
     const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
     const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
     if (wa.bounces) {  // the reflect kernel combines the levels and writes the pixel
@@ -1201,8 +1192,8 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
             const uint32_t b = blockIdx.x + (c0 + t) * G;
             ++taken;
-            primary_block<RESIDENT, PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws,
-                                                             pc, use_frustum, frect);
+            primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
+                                                      use_frustum, frect);
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -1261,7 +1252,8 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             const uint32_t nxt = dyn ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            shadow_item<PREFILTER, BRUTE, false>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment, q, c, l, ws);
+            shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+                                          (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws);
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
@@ -1271,97 +1263,112 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
 }
 
 // ---------------------------------------------------------------- one-launch frame
-// k_trace: primary blocks and shadow items in ONE persistent kernel.  A wave serves shard
-// q; shadow items (chunk, light) of region q become available as primary blocks of shard
-// q publish their hit slots (allocation counter + per-chunk ready tag), so the shadow
-// work of early blocks overlaps the primary work of late ones and the frame has one tail.
-// Waves prefer available shadow items, then primary blocks, and otherwise sleep until
-// either appears; a wave leaves the shard when every primary block of the shard is done
-// and its shadow ticket is past the final item count.  Nothing waits on a wave that has
-// not started (tickets are only taken by running waves), so progress does not depend on
-// every workgroup being resident.
+// k_trace: the whole frame in ONE persistent launch, primary blocks and their shadow
+// items handled inside the workgroup that owns the blocks.  Workgroup w owns the same
+// lattice of blocks as in k_primary and a private hit region (WorkArgs::wg_cap slots);
+// its waves take primary blocks and shadow items (chunk, light) with LDS tickets,
+// preferring shadow items so the region stays hot in this XCD's L2.  A chunk is
+// published through an LDS ready flag once its stores have reached L2 (every wave of the
+// workgroup shares that L2, so no device-scope coherence is needed).  One mesh staging,
+// no second launch, and the shadow work of early blocks fills the primary tail.  The mesh
+// is staged in absolute coordinates (the shadow rays' origins differ per lane).
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][(MIRT_PRIMARY_WIDE || MIRT_SHADOW_WIDE) ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
+    __shared__ float4 frect[8];
+    __shared__ uint32_t bq[kBlkQ][3];
+    __shared__ uint32_t ready[kBlkQ];
+    __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item;
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     WaveClock clock;
     uint32_t taken = 0;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
-    if (RESIDENT) {
-        stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
-        __syncthreads();
-    }
-    clock.mark_staged();
+    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;
+    if (use_frustum) stage_frustum(frect, wa.fr);
+    if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
     uint32_t* stk = wstk[threadIdx.x >> 6];
-    const ShardCursor sc;
     WaveStats wp{0, 0, 0, 0, 0}, wsh{0, 0, 0, 0, 0};
+    PhaseClock pc;
     const uint32_t nl = max(fa.n_lights, 1u);
     constexpr uint32_t kNone = 0xffffffffu;
-    // Every wait is bounded (~1 s): should progress ever stall, the wave records it in the
-    // overflow statistic (tests assert 0) and leaves, so the kernel always drains.
+    // every wait is bounded (~1 s): should progress ever stall, the wave records it in the
+    // overflow statistic (tests assert 0) and leaves, so the kernel always drains
     constexpr uint32_t kSpinLimit = 1u << 24;
     uint32_t spins = 0;
-    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards && spins < kSpinLimit; q += sc.shard_step()) {
-        const uint32_t nprim = (wa.nblocks > q) ? (wa.nblocks - q + kQShards - 1) / kQShards : 0;
-        cnt_t* pq = &wa.counters[cnt_queue(0, q)];
-        cnt_t* sqc = &wa.counters[cnt_queue(1, q)];
-        uint32_t* sq = lo32(sqc);
-        uint32_t* alloc = lo32(&wa.counters[cnt_hits(q)]);
-        uint32_t* pdone = lo32(&wa.counters[cnt_pdone(q)]);
-        uint32_t pk = ticket_resolve(ticket_issue(pq));
-        uint32_t pend = kNone;
+    const uint32_t G = gridDim.x;
+    const uint32_t mine = wa.nblocks > blockIdx.x ? (wa.nblocks - blockIdx.x + G - 1) / G : 0u;
+    size_t chunk0 = (size_t)blockIdx.x * wa.wg_cap;  // slot of this batch's chunk 0
+    auto lds_ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto lds_inc = [](uint32_t* p) {
+        uint32_t t = 0;
+        if ((threadIdx.x & 63) == 0) t = atomicAdd(p, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane(t);
+    };
+    for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
+        const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
+        for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
+            const uint32_t b = blockIdx.x + (c0 + t) * G;
+            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(b % kQShards) * wa.per_shard + b / kQShards];
+            bq[t][0] = v[0];
+            bq[t][1] = v[1];
+            bq[t][2] = v[2];
+            ready[t] = 0;
+        }
+        if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
+        if (c0 == 0) clock.mark_staged();
+        __syncthreads();
+        const LocalChunks lc{&s_chunks, ready, chunk0};
+        uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
         for (;;) {
-            // 1. a shadow item whose chunk has been allocated
-            const uint32_t avail =
-                (uint32_t)(__hip_atomic_load(alloc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 64) * nl;
-            if (pend == kNone &&
-                (uint32_t)__hip_atomic_load(sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < avail)
-                pend = ticket_resolve(ticket_issue(sqc));
+            // 1. a shadow item of an allocated chunk
+            const uint32_t avail = lds_ld(&s_chunks) * nl;
+            if (pend == kNone && lds_ld(&s_item) < avail) pend = lds_inc(&s_item);
             if (pend != kNone && pend < avail) {
                 const uint32_t c = pend / nl, l = pend - c * nl;
-                // the allocating wave is still writing the chunk: wait for its ready tag
-                while (__hip_atomic_load(&wa.rdy[(size_t)q * (wa.hit_cap / 64) + c], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) != wa.frame_tag &&
-                       ++spins < kSpinLimit)
-                    __builtin_amdgcn_s_sleep(1);
+                while (lds_ld(&ready[c]) == 0 && ++spins < kSpinLimit) __builtin_amdgcn_s_sleep(1);
                 if (spins >= kSpinLimit) break;
                 ++taken;
-                shadow_item<PREFILTER, BRUTE, true>(fa, wa, out, lds, stk, RESIDENT, segment, q, c, l, wsh);
+                shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l, wsh);
                 pend = kNone;
                 continue;
             }
             // 2. a primary block
-            if (pk < nprim) {
-                const uint32_t nxt = ticket_issue(pq);
-                ++taken;
-                const BlockDesc bd = block_desc(wa, q, pk);
-                PhaseClock pc;
-                primary_block<false, PREFILTER, BRUTE, true>(fa, wa, out, lds, stk, RESIDENT, bd, q, wp, pc);
-                // count the block done after its slots are published (allocation first)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if ((threadIdx.x & 63) == 0) atomicAdd(pdone, 1u);
-                pk = ticket_resolve(nxt);
-                continue;
+            if (lds_ld(&s_prim) < nc) {
+                const uint32_t t = lds_inc(&s_prim);
+                if (t < nc) {
+                    const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
+                    ++taken;
+                    primary_block<false, PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, bd, 0, wp, pc, use_frustum,
+                                                           frect, &lc);
+                    lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated
+                    continue;
+                }
             }
-            // 3. nothing available now
-            if ((uint32_t)__hip_atomic_load(pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nprim) {
-                const uint32_t total =
-                    (uint32_t)(__hip_atomic_load(alloc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 64) * nl;
+            // 3. nothing available now: leave once every block is done and no item is left
+            if (lds_ld(&s_pdone) >= nc) {
+                const uint32_t total = lds_ld(&s_chunks) * nl;
                 if (pend == kNone) {
-                    if ((uint32_t)__hip_atomic_load(sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) break;
-                    pend = ticket_resolve(ticket_issue(sqc));
+                    if (lds_ld(&s_item) >= total) break;
+                    pend = lds_inc(&s_item);
                 }
                 if (pend >= total) break;
                 continue;
             }
             if (++spins >= kSpinLimit) break;
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
         }
+        __syncthreads();  // every wave is done with this batch before it is restaged
+        chunk0 += (size_t)s_chunks * 64;
+        __syncthreads();
     }
+    if (mine == 0) clock.mark_staged();
     if (spins >= kSpinLimit) wp.overflow += 1;
+    __syncthreads();
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, wp);
     __syncthreads();
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);

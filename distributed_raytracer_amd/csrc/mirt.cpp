@@ -65,13 +65,10 @@ struct Slot {
     size_t litw_cap = 0;
     uint32_t* blkdone = nullptr;
     size_t blkdone_cap = 0;
-    uint32_t* rdy = nullptr;
-    size_t rdy_cap = 0;
     double* dir0 = nullptr;   // configs[4] reflections: primary direction per hit slot
     size_t dir0_cap = 0;
     double* ph0 = nullptr;    // configs[4] reflections: phong of the primary hit per slot
     size_t ph0_cap = 0;
-    uint32_t frame_tag = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
@@ -446,20 +443,15 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.nblocks = sl->nblocks;
     wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
-    const uint64_t hit_slots = (uint64_t)kQShards * wa.hit_cap;
+    // persistent: two 512-thread workgroups per CU
+    const int pgrid = (int)std::max<uint64_t>(
+        1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
+    // k_trace: workgroup w's hit region holds one chunk per block it owns
+    wa.wg_cap = (uint32_t)(((uint64_t)sl->nblocks + pgrid - 1) / pgrid * 64);
+    const uint64_t hit_slots = std::max<uint64_t>((uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap);
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
-    if (sl->rdy_cap < hit_slots / 64) {  // new ready tags must not match any frame tag
-        if ((r = dev_grow(sl->rdy, sl->rdy_cap, hit_slots / 64)) != MIRT_OK) return r;
-        HIP_TRY(hipMemsetAsync(sl->rdy, 0, sl->rdy_cap * sizeof(uint32_t), s));
-    }
-    if (++sl->frame_tag == 0) {  // tags wrap after 2^32 frames: clear the ready tags
-        sl->frame_tag = 1;
-        HIP_TRY(hipMemsetAsync(sl->rdy, 0, sl->rdy_cap * sizeof(uint32_t), s));
-    }
-    wa.rdy = sl->rdy;
-    wa.frame_tag = sl->frame_tag;
     wa.bounces = f->max_bounces;
     if (wa.bounces) {
         if ((r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
@@ -499,9 +491,6 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if (sl->dirty) HIP_TRY(hipMemsetAsync(sl->counters, 0, 2 * kCntN * sizeof(cnt_t), s));
     sl->dirty = true;
     sl->parity ^= 1u;
-    // persistent: two 512-thread workgroups per CU; waves take work from the queues
-    const int pgrid = (int)std::max<uint64_t>(
-        1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
@@ -588,7 +577,6 @@ void mirt_destroy(mirt_ctx* c) {
         if (s->hits) (void)hipFree(s->hits);
         if (s->litw) (void)hipFree(s->litw);
         if (s->blkdone) (void)hipFree(s->blkdone);
-        if (s->rdy) (void)hipFree(s->rdy);
         if (s->dir0) (void)hipFree(s->dir0);
         if (s->ph0) (void)hipFree(s->ph0);
         if (s->counters) (void)hipFree(s->counters);

@@ -187,8 +187,7 @@ struct WorkArgs {
     HitRec* hits;          // kQShards regions of hit_cap records
     uint32_t* litw;        // per hit slot: bit l = light l reaches the hit (atomicOr by k_shadow)
     uint32_t* blkdone;     // per 64-slot hit block: lights finished (the last one shades the block)
-    uint32_t* rdy;         // per 64-slot hit block: frame_tag once its slots are written (k_trace)
-    uint32_t frame_tag;    // non-zero, different from the previous frame's on this slot
+    uint32_t wg_cap;       // k_trace: hit slots per workgroup region (chunks of 64)
     uint32_t bounces;      // configs[4] reflection extension (mirt_frame.max_bounces), 0 = off
     double* dir0;          // bounces: per hit slot, the primary ray direction (3 doubles)
     double* ph0;           // bounces: per hit slot, phong of the primary hit (3 doubles)
