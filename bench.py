@@ -47,13 +47,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
-    ap.add_argument("--one-kernel", action="store_true", help="variant: one k_trace launch per frame")
+    ap.add_argument("--split-kernels", action="store_true",
+                    help="variant: k_primary then k_shadow (default: one k_trace launch per frame)")
     ap.add_argument("--static-schedule", action="store_true",
                     help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
-                    help="per-launch HBM bytes of k_primary from a rocprofv3 --pmc pass (see profiles/)")
+                    help="per-launch HBM bytes / fp64 flops of the dominant kernel from rocprofv3 --pmc passes (profiles/)")
     return ap.parse_args()
 
 
@@ -139,7 +140,7 @@ def main():
     ctx = rt.Context(local)
     opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
-        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_ONE_KERNEL if a.one_kernel else 0)
+        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses
@@ -204,15 +205,19 @@ def main():
         rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
         launches = max(prof["launches"], 1)
         prim_ms = prof["primary_ms_sum"] / launches
-        prim_tests = prof["primary_tri_tests"] / launches
-        achieved = prim_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
+        # the dominant kernel: k_trace (the whole frame, one launch) or, split, k_primary;
+        # reflection frames always run split (k_primary, k_shadow, k_reflect)
+        one = not a.split_kernels and not a.bounces
+        kname = "k_trace" if one else "k_primary"
+        k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / launches
+        achieved = k_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
         traffic = fp64_flops = None
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
                 if tj.get("width") == W and tj.get("height") == H and tj.get("gpus", 1) == world:
-                    traffic = tj.get("k_primary_hbm_bytes_per_launch")
-                    fp64_flops = tj.get("k_primary_fp64_flops_per_launch")
+                    traffic = tj.get(f"{kname}_hbm_bytes_per_launch")
+                    fp64_flops = tj.get(f"{kname}_fp64_flops_per_launch")
             except (OSError, ValueError):
                 traffic = None
         line = {
@@ -238,25 +243,25 @@ def main():
             "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / launches),
             "bvh_visits_per_frame": {k: int(prof[k] / launches) for k in (
                 "primary_node_visits", "primary_leaf_visits", "shadow_node_visits", "shadow_leaf_visits")},
-            "ms_kernels": {"primary": round(prim_ms, 4),
+            "ms_kernels": {("frame_kernel" if one else "primary"): round(prim_ms, 4),
                            "shadow": round(prof["shadow_ms_sum"] / launches, 4),
                            "reflect": round(prof["reflect_ms_sum"] / launches, 4),
                            "frame_device": round(prof["frame_ms_sum"] / launches, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_primary", "bytes_per_unit": BYTES_PER_TRI_TEST,
-                         "units_per_launch": int(prim_tests),
+                         "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST,
+                         "units_per_launch": int(k_tests),
                          "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
                                  "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
                                  "VALU, see DESIGN.md; kernel time = HIP events on the trace stream over a second "
                                  "region of the same frames (the throughput region runs without events)"},
             "roofline_fp64_valu": None if fp64_flops is None else {
-                "bound": "fp64-valu", "kernel": "k_primary", "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFLOPS,
+                "bound": "fp64-valu", "kernel": kname, "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFLOPS,
                 "achieved": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12, 3),
                 "frac": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
                 "flops_per_launch": int(64 * fp64_flops),
                 "note": "SQ_INSTS_VALU_FLOPS_FP64 (counts per wave instruction, FMA = 2) x 64 lanes per launch, "
-                        "from the committed rocprofv3 pass (profiles/), over this run's k_primary HIP-event time"},
+                        "from the committed rocprofv3 pass (profiles/), over this run's HIP-event time of the kernel"},
         }
         if not a.no_parity:
             fr = sh.frame

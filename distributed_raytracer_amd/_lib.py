@@ -27,7 +27,7 @@ MIRT_OPT_BRUTE_FORCE = 2
 MIRT_OPT_STATIC_SCHEDULE = 4
 MIRT_OPT_TIMELINE = 8
 MIRT_OPT_NO_SEGMENT = 16
-MIRT_OPT_ONE_KERNEL = 32
+MIRT_OPT_SPLIT_KERNELS = 32
 MIRT_OPT_NO_FRUSTUM = 64
 
 D3 = C.c_double * 3

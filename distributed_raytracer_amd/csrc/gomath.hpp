@@ -117,6 +117,13 @@ MIRT_HD bool go_is_odd_int(double x) {
     return xi == x && (((int64_t)xi) & 1) == 1;
 }
 
+// exp(yf * log(x)) of go_pow's fractional exponent, out of line: inlined, its polynomial
+// constants are hoisted out of the kernels' work loops into registers and spilled to
+// scratch, although the suzanne materials (integer Ns) never take this path.
+__host__ __device__ __attribute__((noinline)) inline double go_pow_frac(double yf, double x) {
+    return exp(yf * log(x));
+}
+
 // Go math.Pow.  The integer part of y is applied by repeated squaring on the Frexp
 // mantissa (bit-exact with Go); a fractional part uses exp(yf*log(x)), which matches Go
 // only to a few ulp (Go's amd64 Exp/Log are assembly).  tracer.go:72 uses it with the
@@ -160,7 +167,7 @@ MIRT_HD double go_pow(double x, double y) {
             yf--;
             yi++;
         }
-        a1 = exp(yf * log(x));
+        a1 = go_pow_frac(yf, x);
     }
     int xe;
     double x1 = go_frexp(x, xe);

@@ -495,7 +495,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    if ((c->flags & MIRT_OPT_ONE_KERNEL) && !wa.bounces) {
+    if (!(c->flags & MIRT_OPT_SPLIT_KERNELS) && !wa.bounces) {
         // one launch per frame (k_trace); its time lands in the primary slot of the profile
         HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
         if (prof) {

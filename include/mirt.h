@@ -127,8 +127,8 @@ typedef struct {
     uint64_t shadow_rays;
     uint64_t hits;
     uint64_t tri_tests;     /* ray-triangle tests performed (brute force: rays * tris) */
-    double ms_primary;      /* the primary kernel (MIRT_OPT_ONE_KERNEL: the whole frame) */
-    double ms_shadow;       /* the shadow + Phong kernel (MIRT_OPT_ONE_KERNEL: 0) */
+    double ms_primary;      /* the frame kernel k_trace (MIRT_OPT_SPLIT_KERNELS: the primary kernel) */
+    double ms_shadow;       /* MIRT_OPT_SPLIT_KERNELS: the shadow + Phong kernel (default: 0) */
     double ms_shade;        /* reserved (0) */
     double ms_total;        /* first kernel start -> last kernel end */
     uint64_t reflection_rays; /* configs[4] extension (mirt_frame.max_bounces) */
@@ -227,7 +227,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_STATIC_SCHEDULE 4u /* round-robin work split in every kernel (no work queues) */
 #define MIRT_OPT_TIMELINE 8u        /* record per-wave start/end stamps (mirt_debug_timeline) */
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
-#define MIRT_OPT_ONE_KERNEL 32u     /* one k_trace launch per frame (default: primary, then shadow+shade) */
+#define MIRT_OPT_SPLIT_KERNELS 32u  /* k_primary then k_shadow (default: one k_trace launch per frame) */
 #define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 

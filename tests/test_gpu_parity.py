@@ -77,7 +77,7 @@ def _variants(ctx, fn):
         for opts in (0, rt._lib.MIRT_OPT_NO_PREFILTER, rt._lib.MIRT_OPT_BRUTE_FORCE,
                      rt._lib.MIRT_OPT_BRUTE_FORCE | rt._lib.MIRT_OPT_NO_PREFILTER,
                      rt._lib.MIRT_OPT_STATIC_SCHEDULE, rt._lib.MIRT_OPT_NO_SEGMENT,
-                     rt._lib.MIRT_OPT_ONE_KERNEL, rt._lib.MIRT_OPT_ONE_KERNEL | rt._lib.MIRT_OPT_BRUTE_FORCE,
+                     rt._lib.MIRT_OPT_SPLIT_KERNELS, rt._lib.MIRT_OPT_SPLIT_KERNELS | rt._lib.MIRT_OPT_BRUTE_FORCE,
                      rt._lib.MIRT_OPT_NO_FRUSTUM):
             ctx.set_options(opts)
             out[opts] = fn()
@@ -172,7 +172,7 @@ def test_shadow_segments_exact_with_lights_near_surfaces(ctx, env):
             lights.append(rt.Light(tuple(float(x) for x in p), (1.0, 200 / 255, 100 / 255)))
         mut = rt.EnvMutables(base.objects, lights, base.cam)
         res = {}
-        for opts in (0, rt._lib.MIRT_OPT_BRUTE_FORCE, rt._lib.MIRT_OPT_NO_SEGMENT, rt._lib.MIRT_OPT_ONE_KERNEL):
+        for opts in (0, rt._lib.MIRT_OPT_BRUTE_FORCE, rt._lib.MIRT_OPT_NO_SEGMENT, rt._lib.MIRT_OPT_SPLIT_KERNELS):
             ctx.set_options(opts)
             res[opts] = rt.draw(env, 320, 240, mut)
         ctx.set_options(0)

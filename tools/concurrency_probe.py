@@ -23,7 +23,7 @@ def main():
     W, H = 1920, 1080
     dev = torch.device("cuda", 0)
     res = {}
-    for oname, o in (("split", 0), ("one_kernel", rt._lib.MIRT_OPT_ONE_KERNEL)):
+    for oname, o in (("one_kernel", 0), ("split", rt._lib.MIRT_OPT_SPLIT_KERNELS)):
         ctx.set_options(o)
         for k in (1, 2, 4):
             tiles = [(0, 0, W, H)] if k == 1 else plan_tiles(W, H, 64)

@@ -6,6 +6,7 @@ usage (GPU box): python tools/cost_probe.py [--repeat N] [--views default,away] 
 Each (view, options) pair is timed N times (interleaved); the minimum is reported.
 """
 import argparse
+import time
 import json
 import os
 import sys
@@ -36,7 +37,7 @@ def main():
                                  tuple(np.array([1.0, 1.0, -1.0]) - np.asarray(cam.pos)), cam.fov),
     }
     opts = {"default": 0, "static": rt._lib.MIRT_OPT_STATIC_SCHEDULE, "no_frustum": rt._lib.MIRT_OPT_NO_FRUSTUM,
-            "one_kernel": rt._lib.MIRT_OPT_ONE_KERNEL}
+            "split": rt._lib.MIRT_OPT_SPLIT_KERNELS}
     if a.views:
         views = {k: views[k] for k in a.views.split(",")}
     if a.opts:
@@ -54,6 +55,12 @@ def main():
                     for _ in range(5):
                         sh.render(frame)
                     torch.cuda.synchronize()
+                    # steady-state frame time without profiling events
+                    t0 = time.perf_counter()
+                    for _ in range(50):
+                        sh.render(frame)
+                    torch.cuda.synchronize()
+                    wall = (time.perf_counter() - t0) / 50 * 1e6
                     ctx.profile_enable(True)
                     for _ in range(30):
                         sh.render(frame)
@@ -64,6 +71,7 @@ def main():
                     prev = out.get(f"{vname}/{oname}", {})
                     best = lambda key, v: round(min(v, prev.get(key, v)), 1)
                     out[f"{vname}/{oname}"] = {
+                        "wall_us": best("wall_us", wall),
                         "primary_us": best("primary_us", p["primary_ms_sum"] / n * 1e3),
                         "shadow_us": best("shadow_us", p["shadow_ms_sum"] / n * 1e3),
                         "frame_us": best("frame_us", p["frame_ms_sum"] / n * 1e3),

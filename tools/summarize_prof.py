@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    for k in ("k_primary", "k_shadow", "k_frame", "k_rays", "k_unpack", "k_debug_fp64"):
+    for k in ("k_primary", "k_shadow", "k_trace", "k_reflect", "k_rays", "k_unpack", "k_debug_fp64"):
         if k in name:
             return k + ("<nopre>" if "false>" in name and k != "k_shade" else "")
     return name.split("(")[0][:40]
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--traffic-out", default="", help="merge the traffic keys into this json (default: <tag>_pmc_traffic.json)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -79,15 +80,21 @@ def main():
             e["clock_ghz_est"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (sum(dur[k]) / len(dur[k])) / 1e9, 3)
         summary["kernels"][k] = e
     json.dump(summary, open(os.path.join(dst, f"{a.tag}_summary.json"), "w"), indent=1)
-    kp = summary["kernels"].get("k_primary", {})
-    if "hbm_bytes_per_launch" in kp:
-        json.dump({"tag": a.tag, "width": a.width, "height": a.height, "gpus": a.gpus,
-                   "k_primary_hbm_bytes_per_launch": kp["hbm_bytes_per_launch"],
-                   "k_primary_avg_ns": kp["avg_ns"],
-                   "k_primary_fp64_flops_per_launch": kp.get("SQ_INSTS_VALU_FLOPS_FP64"),
-                   "k_primary_valu_insts_per_launch": kp.get("SQ_INSTS_VALU"),
-                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; (2*FETCH+WRITE)*1024"},
-                  open(os.path.join(dst, f"{a.tag}_pmc_traffic.json"), "w"), indent=1)
+    tout = a.traffic_out or os.path.join(dst, f"{a.tag}_pmc_traffic.json")
+    tj = json.load(open(tout)) if a.traffic_out and os.path.exists(tout) else {}
+    tj.update({"width": a.width, "height": a.height, "gpus": a.gpus,
+               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; (2*FETCH+WRITE)*1024"})
+    tj.setdefault("tags", [])
+    if a.tag not in tj["tags"]:
+        tj["tags"].append(a.tag)
+    for name in ("k_trace", "k_primary", "k_shadow"):
+        kp = summary["kernels"].get(name, {})
+        if "hbm_bytes_per_launch" in kp:
+            tj[f"{name}_hbm_bytes_per_launch"] = kp["hbm_bytes_per_launch"]
+            tj[f"{name}_avg_ns"] = kp["avg_ns"]
+            tj[f"{name}_fp64_flops_per_launch"] = kp.get("SQ_INSTS_VALU_FLOPS_FP64")
+            tj[f"{name}_valu_insts_per_launch"] = kp.get("SQ_INSTS_VALU")
+    json.dump(tj, open(tout, "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
 
