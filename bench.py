@@ -5,12 +5,19 @@ A "step" is one full frame of tracer.Trace semantics over example/scene.json
 (3 lights), Phong, uint8 packing — everything worker/sequential's draw loop does per
 frame.  Inputs (mesh, frame params) are resident on the GPU before timing; outputs stay
 in HBM.  With N GPUs (torchrun, one process per GPU) the same frame is split into
-interleaved 64x64 tiles and the packed tiles are gathered to rank 0 over RCCL and
+interleaved 32x32 tiles and the packed tiles are gathered to rank 0 over RCCL and
 unpacked into the framebuffer inside the timed region (strong scaling: total work is
 one frame whatever N is).
 
+Frames are pipelined (--inflight F, default 4): frame k runs on stream k % F with its own
+buffers, so frame k+1's kernel starts while frame k's last workgroups finish, as the
+reference master keeps several frames in flight.  ms_per_step is therefore the frame
+INTERVAL at steady state (throughput); frame_latency_ms is one frame rendered alone
+(render, gather, unpack, host sync) with the same launch shape.
+
 Prints ONE JSON line on rank 0 (contract in the task statement).  Fields beyond the
-contract: primary_mrays_s, rays_per_frame, hits, ms_kernels, parity.
+contract: frames_in_flight, frame_latency_ms, primary_mrays_s, rays_per_frame, hits,
+ms_kernels, parity, roofline_fp64_valu, cpu_baseline.
 """
 from __future__ import annotations
 
@@ -40,13 +47,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--scene", default=SCENE)
     ap.add_argument("--bounces", type=int, default=0,
                     help="configs[4] reflection EXTENSION: bounces per primary hit (0 = the reference)")
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("MIRT_INFLIGHT", "4")),
+                    help="frames in flight (one stream and one set of buffers each; frame k+1's kernel "
+                         "starts while frame k's last workgroups finish)")
+    ap.add_argument("--grid", default="",
+                    help="frame-kernel launch shape 'MIN_BLOCKS_PER_WG,MAX_WORKGROUPS' (mirt_set_grid; "
+                         "default: FrameSharder's choice for the frames in flight)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
+    ap.add_argument("--no-octant", action="store_true", help="ablation: generic (sorted) child-box test only")
     ap.add_argument("--split-kernels", action="store_true",
                     help="variant: k_primary then k_shadow (default: one k_trace launch per frame)")
     ap.add_argument("--static-schedule", action="store_true",
@@ -138,7 +152,7 @@ def main():
 
     W, H = a.width, a.height
     ctx = rt.Context(local)
-    opts = (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
+    opts = (rt._lib.MIRT_OPT_NO_OCTANT if a.no_octant else 0) | (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0)
     ctx.set_options(opts)
@@ -147,7 +161,9 @@ def main():
     frame = dataclasses.replace(env.mutable(), max_bounces=a.bounces).to_frame()
     tris = sum(len(m.face_v) for m in env.meshes)
     nl = len(env.mutable().lights)
-    sh = FrameSharder(ctx, W, H, rank, world, a.tile)
+    sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight)
+    if a.grid:
+        ctx.set_grid(*(int(x) for x in a.grid.split(",")))
     dev = torch.device("cuda", local)
 
     def barrier():
@@ -182,22 +198,34 @@ def main():
         sh.flush()
         torch.cuda.synchronize(dev)
         ctx.profile_enable(False)
+
+        # single-frame latency: one frame alone (render, gather + unpack, host sync), median
+        lat = []
+        for _ in range(min(a.steps, 20)):
+            barrier()
+            torch.cuda.synchronize(dev)
+            l0 = time.perf_counter()
+            sh.render(frame)
+            sh.flush()
+            torch.cuda.synchronize(dev)
+            lat.append(time.perf_counter() - l0)
+        latency = float(np.median(lat)) if lat else 0.0
     prof = ctx.profile_read()
 
     elapsed = t1 - t0
     pl = max(prof["launches"], 1)
-    counts = torch.tensor([elapsed, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
+    counts = torch.tensor([elapsed, latency, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
                            prof["reflection_rays"] / pl], dtype=torch.float64,
                           device=dev if backend == "nccl" else "cpu")
     if world > 1:
-        tmax = counts[:1].clone()
+        tmax = counts[:2].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        sums = counts[1:].clone()
+        sums = counts[2:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax.item())
+        elapsed, latency = (float(x) for x in tmax.tolist())
         primary, shadow, hits, refl = (float(x) for x in sums.tolist())
     else:
-        primary, shadow, hits, refl = (float(x) for x in counts[1:].tolist())
+        primary, shadow, hits, refl = (float(x) for x in counts[2:].tolist())
 
     if rank == 0:
         steps = a.steps
@@ -237,6 +265,8 @@ def main():
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
+            "frames_in_flight": sh.F,
+            "frame_latency_ms": round(latency * 1e3, 4),
             "primary_mrays_s": round(primary / (ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
             "hits_per_frame": int(hits),
@@ -251,6 +281,10 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST,
                          "units_per_launch": int(k_tests),
+                         # with frames in flight a launch shares the chip with its neighbours,
+                         # so per-launch time overstates the cost: the same bytes per frame
+                         # over the steady-state frame interval
+                         "chip_rate_gbs": round(k_tests * BYTES_PER_TRI_TEST / (ms / 1e3) / 1e9, 1),
                          "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
                                  "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
                                  "VALU, see DESIGN.md; kernel time = HIP events on the trace stream over a second "

@@ -29,6 +29,7 @@ MIRT_OPT_TIMELINE = 8
 MIRT_OPT_NO_SEGMENT = 16
 MIRT_OPT_SPLIT_KERNELS = 32
 MIRT_OPT_NO_FRUSTUM = 64
+MIRT_OPT_NO_OCTANT = 128
 
 D3 = C.c_double * 3
 
@@ -62,7 +63,7 @@ class Tile(C.Structure):
 
 class Outputs(C.Structure):
     _fields_ = [("rgb", C.c_void_p), ("rgb8", C.c_void_p), ("valid", C.c_void_p), ("face", C.c_void_p),
-                ("object", C.c_void_p)]
+                ("object", C.c_void_p), ("rgbv", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -119,6 +120,9 @@ SIGNATURES = {
     "mirt_profile_enable": (C.c_int, [_P, C.c_int]),
     "mirt_profile_read": (C.c_int, [_P, C.POINTER(Profile)]),
     "mirt_set_options": (C.c_int, [_P, C.c_uint32]),
+    "mirt_set_grid": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "mirt_stream_create": (C.c_int, [_P, C.POINTER(_P)]),
+    "mirt_stream_destroy": (C.c_int, [_P, _P]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_unpack_tiles_at_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),

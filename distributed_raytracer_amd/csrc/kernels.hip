@@ -319,9 +319,11 @@ struct NodeRegs {
     __device__ __forceinline__ float hi(int a, int c) const { return __uint_as_float(word(a * 16 + 2 * c + 1)); }
     __device__ __forceinline__ uint32_t child(int c) const { return word(48 + c); }
 };
-__device__ __forceinline__ NodeRegs load_node(cnptr nd) {
+// oct (packet_octant): axis a with bit a set loads the (hi, lo) copy of its bounds.
+__device__ __forceinline__ NodeRegs load_node(cnptr nd, uint32_t oct = 0) {
     const cv16ptr p = (cv16ptr)nd;
-    return NodeRegs{p[0], p[1], p[2], ((cv8ptr)nd)[6]};
+    const uint32_t o = oct & 7u;  // mixed packets (kOctMixed = 8) load the (lo, hi) pairs
+    return NodeRegs{p[(o & 1u) ? 4 : 0], p[(o & 2u) ? 5 : 1], p[(o & 4u) ? 6 : 2], ((cv8ptr)nd)[6]};
 }
 
 // Ray vs child c's box, t >= 0 half-line.  Boxes are inflated by 2^-12 of the mesh
@@ -390,6 +392,47 @@ __device__ __forceinline__ uint64_t slab_mask(const NodeRegs& nd, int c, const R
     return __builtin_amdgcn_fcmpf(tn, tf, 5 /* FCMP_OLE: tn <= tf */);
 }
 
+// Sign octant of a packet: bit a set = every live lane's fp32 1/d is negative on axis a;
+// kOctMixed = live lanes disagree on some axis.  With a uniform octant each axis's near and
+// far plane are known without comparing them: for 1/d > 0, fma(lo, 1/d, -o/d) <=
+// fma(hi, 1/d, -o/d) because lo <= hi and rounding is monotonic (reversed for 1/d < 0).
+// Every node also stores each axis's bounds as (hi, lo) pairs (Bvh8Node::sbox); a packet
+// loads, per axis, the copy whose first word is its near plane, and a child test needs no
+// min/max sorting: 7 VALU instead of 13 (8 instead of 14 for segments), bit-for-bit the
+// same decision as slab_mask (MIRT_OPT_NO_OCTANT: the sorted test only).
+constexpr uint32_t kOctMixed = 8;
+__device__ __forceinline__ uint32_t packet_octant(const Ray32& r, bool live) {
+    const uint64_t lm = __ballot(live);
+    const uint64_t nx = __ballot(live && r.ix < 0.0f), ny = __ballot(live && r.iy < 0.0f),
+                   nz = __ballot(live && r.iz < 0.0f);
+    if ((nx && nx != lm) || (ny && ny != lm) || (nz && nz != lm)) return kOctMixed;
+    return (nx ? 1u : 0u) | (ny ? 2u : 0u) | (nz ? 4u : 0u);
+}
+// Child c's box with each axis pair loaded near-plane first (load_node with the octant).
+template <bool SEG>
+__device__ __forceinline__ uint64_t slab_mask_ordered(const NodeRegs& nd, int c, const Ray32& r, float tmax) {
+    const f32x2 p0 = {r.ix, r.iy}, p1 = {r.iz, r.oix}, p2 = {r.oiy, r.oiz};
+    const f32x2 tx = pk_slab<0, 1>((f32x2){nd.lo(0, c), nd.hi(0, c)}, p0, p1);
+    const f32x2 ty = pk_slab<1, 0>((f32x2){nd.lo(1, c), nd.hi(1, c)}, p0, p2);
+    const f32x2 tz = pk_slab<0, 1>((f32x2){nd.lo(2, c), nd.hi(2, c)}, p1, p2);
+    const float tn = a_max3(tx.x, ty.x, a_max(tz.x, 0.0f));
+    const float tf = SEG ? a_min3(tx.y, ty.y, a_min(tz.y, tmax)) : a_min3(tx.y, ty.y, tz.y);
+    return __builtin_amdgcn_fcmpf(tn, tf, 5 /* FCMP_OLE */);
+}
+// Bit c = some live lane's ray meets child c.
+template <bool ORDERED, bool SEG>
+__device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const Ray32& r, float tmax, uint64_t fmask,
+                                                     uint64_t lmask) {
+    uint32_t entered = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if (nd.child(c) == kBvhEmpty) continue;
+        const uint64_t m = ORDERED ? slab_mask_ordered<SEG>(nd, c, r, tmax) : slab_mask<SEG>(nd, c, r, tmax);
+        if (((m | fmask) & lmask) != 0) entered |= 1u << c;
+    }
+    return entered;
+}
+
 // Wave-uniform walk of one object's 8-wide BVH (packet traversal).  A child is entered
 // when ANY live lane's ray hits its box; leaves are tested immediately, inner children
 // go on the wave's register stack.  Lanes whose object-space origin is beyond the cull
@@ -399,26 +442,24 @@ __device__ __forceinline__ uint64_t slab_mask(const NodeRegs& nd, int c, const R
 //   the walk ends when no live lane is left.
 template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
-                                          Visits& vis, float tmax = 0.0f, double resolve = 0.0) {
+                                          Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true) {
     const Ray32 r = ray32(ro, d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
     const bool force = !(far <= m.cull_limit);
     bool live = lane_on;
     const uint64_t fmask = __ballot(force);
+    const uint32_t oct = octant ? packet_octant(r, lane_on) : kOctMixed;  // wave-uniform
     WaveStack stk;
     uint32_t cur = 0;
     for (;;) {
         cur = __builtin_amdgcn_readfirstlane(cur);
-        const NodeRegs nd = load_node((cnptr)m.nodes + cur);
+        const NodeRegs nd = load_node((cnptr)m.nodes + cur, oct);
         ++vis.nodes;
         // wave-uniform: bit c = some live lane's ray hits child c (each test's compare
         // result is the lane mask itself: no per-lane bit packing)
-        uint32_t entered = 0;
         const uint64_t lmask = __ballot(live);
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-            if (nd.child(c) != kBvhEmpty && ((slab_mask<SEG>(nd, c, r, tmax) | fmask) & lmask) != 0)
-                entered |= 1u << c;
+        const uint32_t entered = oct == kOctMixed ? children_entered<false, SEG>(nd, r, tmax, fmask, lmask)
+                                                  : children_entered<true, SEG>(nd, r, tmax, fmask, lmask);
         // classify the entered children (unrolled: SALU only), then test the leaves in ONE
         // loop so the triangle test is instantiated once (code size: instruction cache)
         uint32_t leafmask = 0;
@@ -710,9 +751,11 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
                 bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
                                                   vis.overflow);
         } else if (resident) {
-            bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis);
+            bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                             !(fa.flags & MIRT_OPT_NO_OCTANT));
         } else {
-            bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis);
+            bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                               !(fa.flags & MIRT_OPT_NO_OCTANT));
         }
         uint32_t face, pos;
         if (best_result(b, face, pos)) {
@@ -777,9 +820,11 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
             bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
                                              vis.overflow, tmax, resolve);
     } else if (resident) {
-        bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve);
+        bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                          !(fa.flags & MIRT_OPT_NO_OCTANT));
     } else {
-        bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve);
+        bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                          !(fa.flags & MIRT_OPT_NO_OCTANT));
     }
     if (b.has && b.d < resolve) return false;
     uint32_t face, p;
@@ -788,6 +833,11 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     uint32_t mat;
     winner(ob, p, ro, d, neg, world, normal, mat, false);
     return lh < len(sub(world, hit));
+}
+
+// A hit pixel's packed word: uint8(255 c) per channel (colour.go:59-61), valid = 1.
+__device__ __forceinline__ uint32_t pack_rgbv(const RGB& c) {
+    return (uint32_t)c_u8(c.r) | ((uint32_t)c_u8(c.g) << 8) | ((uint32_t)c_u8(c.b) << 16) | (1u << 24);
 }
 
 // ---------------------------------------------------------------- Phong
@@ -891,6 +941,40 @@ struct WaveClock {
     }
 };
 
+// MIRT_ITEM_TRACE (diagnostic builds only, with MIRT_OPT_TIMELINE): one record per work
+// item of k_trace instead of one per wave — {kind, workgroup, start, end (100 MHz), start,
+// end (shader clock), wave tests, nodes | hits << 32} — appended through a counter held in
+// the buffer's first record (tools/item_trace.py).
+#ifndef MIRT_ITEM_TRACE
+#define MIRT_ITEM_TRACE 0
+#endif
+struct ItemClock {
+    uint64_t real0 = 0, clk0 = 0;
+    __device__ __forceinline__ void start() {
+        if (MIRT_ITEM_TRACE) {
+            real0 = __builtin_amdgcn_s_memrealtime();
+            clk0 = __builtin_amdgcn_s_memtime();
+        }
+    }
+    uint32_t k = 0;  // records written by this wave (fixed region of kItemRecs per wave: no atomics)
+    static constexpr uint32_t kItemRecs = 32;
+    __device__ __forceinline__ void record(const WorkArgs& wa, uint32_t kind, uint64_t tests, uint64_t nodes,
+                                           uint64_t hits, uint64_t phases = 0) {
+        if (!MIRT_ITEM_TRACE || !wa.timeline) return;
+        const uint64_t real1 = __builtin_amdgcn_s_memrealtime(), clk1 = __builtin_amdgcn_s_memtime();
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        const uint32_t idx = gw * kItemRecs + k;
+        ++k;
+        if (k > kItemRecs || idx >= 2 * wa.timeline_cap || lane >= kTimelineRec) return;
+        const uint64_t v[kTimelineRec] = {kind, blockIdx.x, real0, real1, clk1 - clk0, phases, tests, nodes | (hits << 32)};
+        uint64_t x = 0;
+#pragma unroll
+        for (int k = 0; k < kTimelineRec; ++k) x = lane == (uint32_t)k ? v[k] : x;
+        wa.timeline[(size_t)idx * kTimelineRec + lane] = x;
+    }
+};
+
 // One ticket of counter c, issued by lane 0; resolve() broadcasts it (waits for the atomic).
 // Queue, hit-slot and primary-done counters are used through the low 32-bit word of
 // their line: a 32-bit returning atomic lands in one VGPR (a 64-bit one whose unused high
@@ -987,6 +1071,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                 out.rgb8[3 * oidx + 1] = 0;
                 out.rgb8[3 * oidx + 2] = 0;
             }
+            if (out.rgbv) out.rgbv[oidx] = 0u;
         }
         pc.lap(2);
         return;
@@ -1061,6 +1146,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                 out.rgb8[3 * oidx + 1] = 0;
                 out.rgb8[3 * oidx + 2] = 0;
             }
+            if (out.rgbv) out.rgbv[oidx] = 0u;  // a hit's word is written by the wave that shades it
         }
     }
     pc.lap(2);
@@ -1138,6 +1224,7 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
         out.rgb8[3 * oidx + 1] = c_u8(col.g);
         out.rgb8[3 * oidx + 2] = c_u8(col.b);
     }
+    if (out.rgbv) out.rgbv[oidx] = pack_rgbv(col);
 }
 
 // ---------------------------------------------------------------- primary kernel
@@ -1307,6 +1394,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
         if ((threadIdx.x & 63) == 0) t = atomicAdd(p, 1u);
         return (uint32_t)__builtin_amdgcn_readfirstlane(t);
     };
+    ItemClock ic;
     for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
         const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
         for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
@@ -1331,7 +1419,10 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 while (lds_ld(&ready[c]) == 0 && ++spins < kSpinLimit) __builtin_amdgcn_s_sleep(1);
                 if (spins >= kSpinLimit) break;
                 ++taken;
+                ic.start();
+                const WaveStats before = wsh;
                 shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l, wsh);
+                ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
             }
@@ -1343,8 +1434,13 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                                        (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
                                        (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
                     ++taken;
+                    ic.start();
+                    const WaveStats before = wp;
+                    const uint64_t ph0 = pc.acc[0], ph1 = pc.acc[1];
                     primary_block<false, PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, bd, 0, wp, pc, use_frustum,
                                                            frect, &lc);
+                    ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
+                              (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
                     lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated
                     continue;
                 }
@@ -1372,7 +1468,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, wp);
     __syncthreads();
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
-    if (wa.timeline) clock.record(wa, 0, taken);
+    if (wa.timeline && !MIRT_ITEM_TRACE) clock.record(wa, 0, taken);
     frame_fold(fa, wa);
 }
 
@@ -1483,6 +1579,7 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
                     out.rgb8[3 * rec.out + 1] = c_u8(c.g);
                     out.rgb8[3 * rec.out + 2] = c_u8(c.b);
                 }
+                if (out.rgbv) out.rgbv[rec.out] = pack_rgbv(c);
             }
             k = (wa.dynamic & kDynReflect) ? ticket_resolve(nxt) : k + sc.peers();
         }
@@ -1555,6 +1652,16 @@ __global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ til
             dst.rgb8[3 * q] = src.rgb8[3 * p];
             dst.rgb8[3 * q + 1] = src.rgb8[3 * p + 1];
             dst.rgb8[3 * q + 2] = src.rgb8[3 * p + 2];
+        }
+        if (src.rgbv) {  // packed word -> rgb8 + valid (and/or a packed framebuffer)
+            const uint32_t v = src.rgbv[p];
+            if (dst.rgbv) dst.rgbv[q] = v;
+            if (dst.valid && !src.valid) dst.valid[q] = (uint8_t)(v >> 24);
+            if (dst.rgb8 && !src.rgb8) {
+                dst.rgb8[3 * q] = (uint8_t)v;
+                dst.rgb8[3 * q + 1] = (uint8_t)(v >> 8);
+                dst.rgb8[3 * q + 2] = (uint8_t)(v >> 16);
+            }
         }
     }
 }

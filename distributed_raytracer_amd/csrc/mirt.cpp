@@ -102,6 +102,10 @@ struct ProfRec {
 struct mirt_ctx {
     int device = 0;
     int cus = 256;
+    // k_trace / k_primary grid: at least this many 8x8 blocks per workgroup (small tile
+    // lists launch fewer, fuller workgroups so frames in flight can share the chip)
+    uint32_t min_blocks_per_wg = 32;
+    uint32_t max_workgroups = 0;  // 0: two per CU
     std::mutex mu;
     std::vector<MeshDev> meshes;
     std::vector<std::unique_ptr<Slot>> slots;
@@ -138,7 +142,7 @@ int dev_grow(T*& p, size_t& cap, size_t need) {
 
 // Up to this many slots are created before a caller blocks on a busy one, so a caller
 // enqueueing frames back to back runs ahead of the GPU instead of waiting per frame.
-constexpr size_t kMaxIdleBlockSlots = 4;
+constexpr size_t kMaxIdleBlockSlots = 8;
 
 int slot_acquire(mirt_ctx* c, Slot*& out) {
     {
@@ -164,20 +168,27 @@ int slot_acquire(mirt_ctx* c, Slot*& out) {
         }
     }
     Slot* s = out;
-    if (!s->stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!s->done) {
+        // the slot's own stream is created only by the synchronous entry points that use
+        // it (slot_stream): every stream takes one of the process's few hardware queues,
+        // which the caller's streams of frames in flight need
         HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
         HIP_TRY(hipMalloc((void**)&s->counters, 2 * kCntN * sizeof(cnt_t)));
         HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
         HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
-        HIP_TRY(hipMemsetAsync(s->counters, 0, 2 * kCntN * sizeof(cnt_t), s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipMemset(s->counters, 0, 2 * kCntN * sizeof(cnt_t)));
     }
     // previous asynchronous use of this slot's staging/workspace must be finished
     if (s->pending) {
         HIP_TRY(hipEventSynchronize(s->done));
         s->pending = false;
     }
+    return MIRT_OK;
+}
+
+int slot_stream(Slot* s, hipStream_t& out) {
+    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    out = s->stream;
     return MIRT_OK;
 }
 
@@ -444,8 +455,13 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
     // persistent: two 512-thread workgroups per CU
-    const int pgrid = (int)std::max<uint64_t>(
-        1, std::min<uint64_t>(((uint64_t)sl->nblocks + kWG / 64 - 1) / (kWG / 64), (uint64_t)2 * c->cus));
+    uint64_t per_wg, max_wg;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        per_wg = std::max<uint32_t>(c->min_blocks_per_wg, 1);
+        max_wg = c->max_workgroups ? std::min<uint64_t>(c->max_workgroups, (uint64_t)2 * c->cus) : (uint64_t)2 * c->cus;
+    }
+    const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)sl->nblocks + per_wg - 1) / per_wg, max_wg));
     // k_trace: workgroup w's hit region holds one chunk per block it owns
     wa.wg_cap = (uint32_t)(((uint64_t)sl->nblocks + pgrid - 1) / pgrid * 64);
     const uint64_t hit_slots = std::max<uint64_t>((uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap);
@@ -472,7 +488,11 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if (c->flags & MIRT_OPT_TIMELINE) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->timeline) {
+#ifdef MIRT_ITEM_TRACE
+            const uint32_t cap = (uint32_t)(c->cus * (kWG / 64)) * 32;  // item records: 32 per wave (diagnostic build)
+#else
             const uint32_t cap = (uint32_t)(2 * c->cus * (kWG / 64));
+#endif
             HIP_TRY(hipMalloc((void**)&c->timeline, sizeof(uint64_t) * kTimelineRec * 2 * cap));
             c->timeline_cap = cap;
         }
@@ -714,6 +734,15 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         }
         mt[10 * m + 9] = mats[m].ns;
     }
+    // the (hi, lo) copies of every node's bounds (kernels.hip packet_octant)
+    for (Bvh8Node& n : bvh.nodes) {
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 8; ++c) {
+                n.sbox[a][c][0] = n.box[a][c][1];
+                n.sbox[a][c][1] = n.box[a][c][0];
+            }
+        for (uint32_t& w : n.pad2) w = 0;
+    }
     MeshDev md;
     md.ntri = nf;
     md.nmat = nm;
@@ -767,7 +796,7 @@ int mirt_trace_tiles_async(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_
     if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     hipStream_t s = (hipStream_t)stream;  // NULL is the HIP null stream, as in the HIP API
-    OutPlanes out{dout->rgb, dout->rgb8, dout->valid, dout->face, dout->object};
+    OutPlanes out{dout->rgb, dout->rgb8, dout->valid, dout->face, dout->object, dout->rgbv};
     uint64_t pixels = 0, tris = 0;
     if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, nullptr, &pixels, &tris)) != MIRT_OK) {
         (void)hipStreamSynchronize(s);
@@ -788,8 +817,8 @@ int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, ui
     if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     const uint64_t npx = (uint64_t)w * h;
-    // device staging for the requested planes: rgb(24) rgb8(3) valid(1) face(4) object(4)
-    const size_t need = npx * (24 + 4 + 4 + 3 + 1) + 64;
+    // device staging for the requested planes: rgb(24) rgb8(3) valid(1) face(4) object(4) rgbv(4)
+    const size_t need = npx * (24 + 4 + 4 + 3 + 1 + 4) + 96;
     uint8_t* base = (uint8_t*)sl->out_buf;
     size_t cap = sl->out_cap;
     if ((r = dev_grow(base, cap, need)) != MIRT_OK) return r;
@@ -807,9 +836,11 @@ int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, ui
     out.object = hout->object ? (int32_t*)carve(npx * 4) : nullptr;
     out.rgb8 = hout->rgb8 ? carve(npx * 3) : nullptr;
     out.valid = hout->valid ? carve(npx) : nullptr;
+    out.rgbv = hout->rgbv ? (uint32_t*)carve(npx * 4) : nullptr;
     mirt_tile t{x, y, w, h};
     uint64_t pixels = 0, tris = 0;
-    hipStream_t s = sl->stream;
+    hipStream_t s = nullptr;
+    if ((r = slot_stream(sl, s)) != MIRT_OK) return r;
     if ((r = enqueue_trace(c, sl, f, W, H, &t, 1, out, s, cancel, &pixels, &tris)) != MIRT_OK) {
         (void)hipStreamSynchronize(s);
         sl->pending = false;
@@ -820,6 +851,7 @@ int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, ui
     if (out.valid) HIP_TRY(hipMemcpyAsync(hout->valid, out.valid, npx, hipMemcpyDeviceToHost, s));
     if (out.face) HIP_TRY(hipMemcpyAsync(hout->face, out.face, npx * 4, hipMemcpyDeviceToHost, s));
     if (out.object) HIP_TRY(hipMemcpyAsync(hout->object, out.object, npx * 4, hipMemcpyDeviceToHost, s));
+    if (out.rgbv) HIP_TRY(hipMemcpyAsync(hout->rgbv, out.rgbv, npx * 4, hipMemcpyDeviceToHost, s));
     if (st) {
         if ((r = fill_stats(sl, s, pixels, tris, f->n_lights, st)) != MIRT_OK) return r;
     } else {
@@ -864,8 +896,8 @@ int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, con
         sl->unpack_key = td;
         sl->unpack_key_H = H;
     }
-    OutPlanes src{packed->rgb, packed->rgb8, packed->valid, packed->face, packed->object};
-    OutPlanes dst{fb->rgb, fb->rgb8, fb->valid, fb->face, fb->object};
+    OutPlanes src{packed->rgb, packed->rgb8, packed->valid, packed->face, packed->object, packed->rgbv};
+    OutPlanes dst{fb->rgb, fb->rgb8, fb->valid, fb->face, fb->object, fb->rgbv};
     HIP_TRY(launch_unpack(sl->d_tiles, n, span, H, src, dst, s));
     HIP_TRY(hipEventRecord(sl->done, s));
     sl->pending = true;
@@ -916,7 +948,8 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* 
     io.object = (int32_t*)carve((size_t)n * 4);
     io.ok = carve(n);
     io.n = n;
-    hipStream_t s = sl->stream;
+    hipStream_t s = nullptr;
+    if ((r = slot_stream(sl, s)) != MIRT_OK) return r;
     FrameArgs fa;
     uint64_t tris;
     fill_args(c, f, 1, 1, fa, tris);
@@ -1022,6 +1055,35 @@ int mirt_debug_fp64(mirt_ctx* c, int op, uint32_t n, const double* a, const doub
 int mirt_set_options(mirt_ctx* c, uint32_t flags) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
     c->flags = flags;
+    return MIRT_OK;
+}
+
+int mirt_stream_create(mirt_ctx* c, void** out) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<uint32_t> mask(((uint32_t)c->cus + 31) / 32, 0u);
+    for (int i = 0; i < c->cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    *out = (void*)s;
+    return MIRT_OK;
+}
+
+int mirt_stream_destroy(mirt_ctx* c, void* stream) {
+    if (!c || !stream) return fail(MIRT_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return MIRT_OK;
+}
+
+int mirt_set_grid(mirt_ctx* c, uint32_t min_blocks_per_wg, uint32_t max_workgroups) {
+    if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    if (min_blocks_per_wg == 0) return fail(MIRT_E_INVALID, "min_blocks_per_wg must be >= 1");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->min_blocks_per_wg = min_blocks_per_wg;
+    c->max_workgroups = max_workgroups;
     return MIRT_OK;
 }
 

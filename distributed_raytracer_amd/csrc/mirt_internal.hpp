@@ -34,6 +34,8 @@ struct alignas(64) Bvh8Node {
     float box[3][8][2];  // [axis][child][lo, hi]
     uint32_t child[8];
     uint32_t pad[8];
+    float sbox[3][8][2];  // [axis][child][hi, lo]: the copy a packet with 1/d < 0 on that axis loads
+    uint32_t pad2[16];
     float& lo(int a, int c) { return box[a][c][0]; }
     float& hi(int a, int c) { return box[a][c][1]; }
     float lo(int a, int c) const { return box[a][c][0]; }
@@ -114,6 +116,7 @@ struct OutPlanes {
     uint8_t* valid;
     int32_t* face;
     int32_t* object;
+    uint32_t* rgbv;  // r | g << 8 | b << 16 | valid << 24 (packed multi-GPU tiles)
 };
 
 // A primary hit handed from the primary kernel to the shadow and shade kernels.

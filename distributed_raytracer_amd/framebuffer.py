@@ -14,6 +14,7 @@ of (W, H, tile, world), so every rank computes it without communication.
 from __future__ import annotations
 
 import ctypes as C
+import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -35,9 +36,26 @@ def plan_tiles(W: int, H: int, tile: int = 64) -> List[TileT]:
     return out
 
 
+def skew(world: int) -> int:
+    """Row skew of the deal: the smallest s >= sqrt(world) coprime with world (8 -> 3)."""
+    s = 1
+    while s * s < world or math.gcd(s, world) != 1:
+        s += 1
+    return s
+
+
 def assign(tiles: Sequence[TileT], world: int, rank: int) -> List[TileT]:
-    """Interleaved deal: tile k goes to rank k % world."""
-    return list(tiles[rank::world])
+    """Interleaved deal of a raster tile list (plan_tiles): the tile in column c of tile
+    row r goes to rank (c + skew * r) % world, so every rank's tiles are spread over rows
+    AND columns (plain k % world puts a rank in the same few columns of every row when the
+    row length is a multiple of world's factors).  On the suzanne 1080p hit mask with
+    32-pixel tiles the busiest of 8 ranks holds 1.04x the mean hit count (k % world:
+    1.07; the master's bisection: 1.37)."""
+    if world <= 1:
+        return list(tiles)
+    cols = sum(1 for t in tiles if t[1] == tiles[0][1]) if tiles else 1
+    s = skew(world)
+    return [t for k, t in enumerate(tiles) if ((k % cols) + s * (k // cols)) % world == rank]
 
 
 def pixels_of(tiles: Sequence[TileT]) -> int:
@@ -107,28 +125,43 @@ def gather_packed(buf, world: int, rank: int, root: int = 0, group=None):
 @dataclass
 class DevicePlanes:
     """Device tensors of one packed or full-frame output (torch, on the context's GPU)."""
-    rgb8: object            # (n, 3) uint8
-    valid: object           # (n,)   uint8
+    rgb8: Optional[object] = None  # (n, 3) uint8
+    valid: Optional[object] = None  # (n,)   uint8
     rgb: Optional[object] = None   # (n, 3) float64
     face: Optional[object] = None  # (n,) int32
-    raw: Optional[object] = None   # (4n,) uint8: the allocation rgb8 ++ valid live in
+    rgbv: Optional[object] = None  # (n,) int32: r | g << 8 | b << 16 | valid << 24 (packed tiles)
 
     def outputs(self, offset: int = 0) -> L.Outputs:
+        if offset == 0 and getattr(self, "_out0", None) is not None:
+            return self._out0  # per-frame calls reuse one struct (host time per frame matters)
+
         def p(t, elem_bytes):
             return None if t is None else t.data_ptr() + offset * elem_bytes
-        return L.Outputs(p(self.rgb, 24), p(self.rgb8, 3), p(self.valid, 1), p(self.face, 4), None)
+        o = L.Outputs(p(self.rgb, 24), p(self.rgb8, 3), p(self.valid, 1), p(self.face, 4), None, p(self.rgbv, 4))
+        if offset == 0:
+            self._out0 = o
+        return o
 
 
-def alloc_planes(n: int, device, with_rgb: bool = False, with_face: bool = False) -> DevicePlanes:
+def alloc_planes(n: int, device, with_rgb: bool = False, with_face: bool = False,
+                 packed: bool = False) -> DevicePlanes:
+    """Framebuffer planes rgb8 + valid, or (packed) ONE rgbv word per pixel — the form a
+    rank's tiles travel in: one 32-bit store per pixel in the trace kernel and one
+    contiguous plane for the gather."""
     import torch
-    # rgb8 and valid share one allocation so a single gather moves both
-    buf = torch.empty(n * 4, dtype=torch.uint8, device=device)
-    return DevicePlanes(rgb8=buf[: n * 3].view(n, 3), valid=buf[n * 3:],
-                        rgb=torch.empty((n, 3), dtype=torch.float64, device=device) if with_rgb else None,
-                        face=torch.empty(n, dtype=torch.int32, device=device) if with_face else None, raw=buf)
+    rgb = torch.empty((n, 3), dtype=torch.float64, device=device) if with_rgb else None
+    face = torch.empty(n, dtype=torch.int32, device=device) if with_face else None
+    if packed:
+        return DevicePlanes(rgbv=torch.empty(n, dtype=torch.int32, device=device), rgb=rgb, face=face)
+    return DevicePlanes(rgb8=torch.empty((n, 3), dtype=torch.uint8, device=device),
+                        valid=torch.empty(n, dtype=torch.uint8, device=device), rgb=rgb, face=face)
 
 
-def _tiles_c(tiles: Sequence[TileT]):
+def _tiles_c(tiles):
+    """ctypes array of mirt_tile (an already built array is passed through: building one
+    costs ~0.3 us per tile of host time, which matters for per-frame calls)."""
+    if isinstance(tiles, C.Array):
+        return tiles
     arr = (L.Tile * len(tiles))()
     for i, t in enumerate(tiles):
         arr[i] = L.Tile(*t)
@@ -163,35 +196,58 @@ class FrameSharder:
     With world == 1 the frame is traced as ONE tile straight into the framebuffer
     (the worker/sequential draw), with no gather and no unpack.
 
-    With world > 1 frames are pipelined: frame k's gather (async on the collective's own
-    stream) overlaps frame k+1's tracing, so each rank keeps two packed buffers; frame k
-    is unpacked on the root once its gather is done, during render(k+1) or flush().
-    All ranks' tiles are unpacked by ONE launch (mirt_unpack_tiles_at_async with the
-    per-rank packed offsets).
+    Frames in flight (`inflight` = F): frame k runs on stream k % F with its own buffers
+    (framebuffer k % F; with world > 1, packed buffer and gathered buffer k % F), so the
+    persistent trace kernel of frame k+1 starts while frame k's last workgroups finish —
+    the frame tail is the largest inefficiency of a single frame — the
+    way the reference master keeps several frames in flight (master/main.go:264-266).
+    Frames are independent (each may have its own camera); results never change.
+
+    With world > 1 every frame's gather is issued right after its trace (RCCL, async on
+    the collective's own stream, which serialises the gathers in issue order on every
+    rank), and frame k-1 is completed while frame k is enqueued: its stream waits for its
+    gather and, on the root, ONE launch unpacks every rank's tiles (mirt_unpack_tiles_at_async
+    with the per-rank packed offsets).  Buffer reuse is stream-ordered: frame k+F traces
+    into packed buffer k % F only after stream k % F waited for frame k's gather.
     """
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: int = 64, root: int = 0,
-                 with_rgb: bool = False, group=None):
+                 with_rgb: bool = False, group=None, inflight: int = 1):
         import torch
         self.ctx, self.W, self.H = ctx, W, H
         self.rank, self.world, self.root, self.group = rank, world, root, group
         self.device = torch.device("cuda", ctx.device)
         self.with_rgb = with_rgb
+        self.F = max(1, int(inflight))
+        if self.F > 1:
+            # frames in flight share the chip: at most 2 x CUs x 2 / F workgroups per frame
+            # (measured: 4 in flight x 256 workgroups beats 4 x 512 by ~10 %, tools/inflight_probe.py)
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            ctx.set_grid(32, max(1, (4 * cus) // self.F) if self.F > 2 else 0)
         if world == 1:
             self.tiles_all = [(0, 0, W, H)]
         else:
             self.tiles_all = plan_tiles(W, H, tile)
         self.mine = assign(self.tiles_all, world, rank)
+        self._mine_c = _tiles_c(self.mine)
         self.cap = packed_capacity(self.tiles_all, world)
-        self._pending = None  # (works, gathered buffers) of the frame whose gather is in flight
+        self._pending = None  # (k, works) of the frame whose gather is in flight
         self._k = 0
+        self._synced = set()  # frame streams that already waited for the current stream (this epoch)
+        self._used = set()    # frame streams with frames since the last flush()
+        # one stream per frame slot (F == 1: torch's current stream, as before)
+        # (each on a hardware queue of its own: HIP shares at most GPU_MAX_HW_QUEUES queues
+        # among ordinary streams, and frames whose streams share a queue serialise)
+        self.streams = [ctx.stream_create() for _ in range(self.F)] if self.F > 1 else None
+        nb = self.F if self.F > 1 else 2  # F == 1: two packed buffers (gather k overlaps trace k+1)
         if world == 1:
             self.packed = None
-            self.frame = alloc_planes(W * H, self.device, with_rgb)
+            self.frames = [alloc_planes(W * H, self.device, with_rgb) for _ in range(self.F)]
         else:
-            self.bufs = [alloc_planes(self.cap, self.device, with_rgb) for _ in range(2)]
+            self.bufs = [alloc_planes(self.cap, self.device, with_rgb, packed=True) for _ in range(nb)]
             self.packed = self.bufs[0]
-            self.frame = alloc_planes(W * H, self.device, with_rgb) if rank == root else None
+            self.frames = ([alloc_planes(W * H, self.device, with_rgb) for _ in range(self.F)]
+                           if rank == root else None)
             if rank == root:
                 # every rank's tiles at its packed offset r * cap in the gathered buffer
                 tl, off = [], []
@@ -204,19 +260,34 @@ class FrameSharder:
                 self._unpack_tiles = _tiles_c(tl)
                 self._unpack_offsets = (C.c_uint64 * len(off))(*off)
                 self._unpack_n = len(tl)
-                self.gathered = [torch.empty(world * self.cap * 4, dtype=torch.uint8, device=self.device)
-                                 for _ in range(2)]
+                self.gathered = [torch.empty(world * self.cap, dtype=torch.int32, device=self.device)
+                                 for _ in range(nb)]
                 self.gathered_rgb = ([torch.empty((world * self.cap, 3), dtype=torch.float64, device=self.device)
-                                      for _ in range(2)] if with_rgb else None)
+                                      for _ in range(nb)] if with_rgb else None)
+        self._nb = nb
+
+    @property
+    def frame(self) -> Optional[DevicePlanes]:
+        """Framebuffer of the last rendered frame (root only when world > 1; complete
+        after flush())."""
+        if self.frames is None:
+            return None
+        return self.frames[(self._k - 1) % self.F] if self._k else self.frames[0]
+
+    def _stream(self, k: int):
+        import torch
+        return self.streams[k % self.F] if self.streams else torch.cuda.current_stream(self.device)
 
     def _gather(self, k: int):
-        """Issue the gather of packed buffer k % 2 to the root (async with RCCL)."""
+        """Issue the gather of packed buffer k to the root (async with RCCL; the current
+        stream must be frame k's)."""
         import torch.distributed as dist
-        buf = self.bufs[k % 2]
+        j = k % self._nb
+        buf = self.bufs[j]
         works = []
-        pairs = [(buf.raw, self.gathered[k % 2] if self.rank == self.root else None)]
+        pairs = [(buf.rgbv, self.gathered[j] if self.rank == self.root else None)]
         if self.with_rgb:
-            pairs.append((buf.rgb, self.gathered_rgb[k % 2] if self.rank == self.root else None))
+            pairs.append((buf.rgb, self.gathered_rgb[j] if self.rank == self.root else None))
         for src, dst in pairs:
             if src.is_cuda and dist.get_backend(self.group) == "gloo":
                 got = gather_packed(src, self.world, self.rank, self.root, self.group)  # synchronous staging
@@ -231,48 +302,64 @@ class FrameSharder:
         return works
 
     def _unpack(self, k: int, stream_ptr: int) -> None:
-        # rank r's gathered region is its packed raw buffer [rgb8 (3 cap) | valid (cap)]:
-        # make each plane contiguous over the ranks (two strided copies), then one launch
-        raw = self.gathered[k % 2].view(self.world, self.cap * 4)
-        self._rgb8_all = raw[:, : self.cap * 3].reshape(self.world * self.cap, 3)
-        self._valid_all = raw[:, self.cap * 3:].reshape(self.world * self.cap)
-        src = DevicePlanes(rgb8=self._rgb8_all, valid=self._valid_all,
-                           rgb=self.gathered_rgb[k % 2] if self.with_rgb else None)
-        s_out, d_out = src.outputs(), self.frame.outputs()
+        # the gathered rgbv plane is contiguous over the ranks (rank r's packed buffer at
+        # pixel r * cap), so one launch expands every rank's tiles into rgb8 + valid
+        j = k % self._nb
+        s_out = DevicePlanes(rgbv=self.gathered[j], rgb=self.gathered_rgb[j] if self.with_rgb else None).outputs()
+        d_out = self.frames[k % self.F].outputs()
         L.check(L.lib().mirt_unpack_tiles_at_async(self.ctx.handle, self.W, self.H, self._unpack_tiles,
                                                    self._unpack_offsets, self._unpack_n, C.byref(s_out),
                                                    C.byref(d_out), C.c_void_p(stream_ptr) if stream_ptr else None))
 
     def render(self, frame_and_keep) -> None:
-        """Enqueue one frame on torch's current stream (no host sync)."""
+        """Enqueue one frame (no host sync).  F == 1: on torch's current stream; F > 1:
+        on the sharder's stream k % F (a frame stream's first frame after construction or
+        flush() waits for the work already queued on the current stream)."""
         import torch
-        s = torch.cuda.current_stream(self.device).cuda_stream
-        if self.world == 1:
-            trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.tiles_all, self.frame, s)
-            return
         k = self._k
         self._k += 1
-        trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self.mine, self.bufs[k % 2], s)
-        works = self._gather(k)
-        self._finish_pending(s)
+        sk = self._stream(k)
+        if self.streams and (k % self.F) not in self._synced:
+            sk.wait_stream(torch.cuda.current_stream(self.device))
+            self._synced.add(k % self.F)
+            self._used.add(k % self.F)
+        if self.world == 1:
+            trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self._mine_c, self.frames[k % self.F],
+                               sk.cuda_stream)
+            return
+        with torch.cuda.stream(sk):
+            trace_tiles_device(self.ctx, frame_and_keep, self.W, self.H, self._mine_c, self.bufs[k % self._nb],
+                               sk.cuda_stream)
+            works = self._gather(k)
+        self._finish_pending()
         self._pending = (k, works)
 
-    def _finish_pending(self, s) -> None:
+    def _finish_pending(self) -> None:
+        import torch
         if self._pending is None:
             return
         k, works = self._pending
         self._pending = None
-        for w in works:
-            w.wait()  # the current stream waits for the collective (no host block with RCCL)
-        if self.rank == self.root:
-            self._unpack(k, s)
+        sk = self._stream(k)
+        with torch.cuda.stream(sk):
+            for w in works:
+                w.wait()  # frame k's stream waits for its collective (no host block with RCCL)
+            if self.rank == self.root:
+                self._unpack(k, sk.cuda_stream)
 
     def flush(self) -> None:
-        """Complete the frame whose gather is still in flight (unpack on the root)."""
+        """Complete every frame in flight: the current stream waits for all of them (and,
+        with world > 1, for the last gather and unpack)."""
         import torch
         if self.world > 1:
-            self._finish_pending(torch.cuda.current_stream(self.device).cuda_stream)
+            self._finish_pending()
+        if self.streams:
+            cur = torch.cuda.current_stream(self.device)
+            for j in sorted(self._used):
+                cur.wait_stream(self.streams[j])
+        self._synced.clear()
+        self._used.clear()
 
     @property
     def last_packed(self):
-        return self.bufs[(self._k - 1) % 2] if self.world > 1 else None
+        return self.bufs[(self._k - 1) % self._nb] if self.world > 1 else None

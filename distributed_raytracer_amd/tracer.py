@@ -61,6 +61,7 @@ class Context:
         L.check(L.lib().mirt_create(int(device), C.byref(self._h)))
         self.device = device
         self._lock = threading.Lock()
+        self._streams = []  # mirt_stream_create handles, destroyed by close()
 
     @property
     def handle(self) -> C.c_void_p:
@@ -70,6 +71,9 @@ class Context:
 
     def close(self) -> None:
         if self._h:
+            for s in self._streams:
+                L.lib().mirt_stream_destroy(self._h, C.c_void_p(s))
+            self._streams = []
             L.lib().mirt_destroy(self._h)
             self._h = C.c_void_p()
 
@@ -102,6 +106,19 @@ class Context:
 
     def set_options(self, flags: int) -> None:
         L.check(L.lib().mirt_set_options(self.handle, flags))
+
+    def stream_create(self):
+        """A torch stream on a hardware queue of its own (mirt.h mirt_stream_create),
+        destroyed with the context."""
+        import torch
+        p = C.c_void_p()
+        L.check(L.lib().mirt_stream_create(self.handle, C.byref(p)))
+        self._streams.append(p.value)
+        return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", self.device))
+
+    def set_grid(self, min_blocks_per_wg: int = 32, max_workgroups: int = 0) -> None:
+        """Frame-kernel launch shape (mirt.h mirt_set_grid); results never change."""
+        L.check(L.lib().mirt_set_grid(self.handle, min_blocks_per_wg, max_workgroups))
 
     def profile_enable(self, on: bool) -> None:
         L.check(L.lib().mirt_profile_enable(self.handle, 1 if on else 0))

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 1
+#define MIRT_ABI_VERSION 2
 
 /* error codes */
 #define MIRT_OK 0
@@ -112,6 +112,9 @@ typedef struct {
  *   valid  1 u8 per pixel, Trace's bool
  *   face   winning face index inside its mesh (-1 on a miss)      [diagnostic]
  *   object winning object index inside mirt_frame.objects (-1)    [diagnostic]
+ *   rgbv   rgb8 and valid in ONE 32-bit word per pixel, r | g << 8 | b << 16 | valid << 24
+ *          (the packed form of a multi-GPU tile buffer: one store per pixel, one
+ *          contiguous plane to gather; the unpack expands it into rgb8 + valid)
  */
 typedef struct {
     double *rgb;
@@ -119,6 +122,7 @@ typedef struct {
     uint8_t *valid;
     int32_t *face;
     int32_t *object;
+    uint32_t *rgbv; /* ABI 2 */
 } mirt_outputs;
 
 /* Counters of one call; timings are device time from HIP events (0 if not recorded). */
@@ -229,7 +233,24 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_NO_SEGMENT 16u     /* shadow rays as full nearest-hit queries (no segment / any-hit) */
 #define MIRT_OPT_SPLIT_KERNELS 32u  /* k_primary then k_shadow (default: one k_trace launch per frame) */
 #define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
+#define MIRT_OPT_NO_OCTANT 128u     /* generic child-box test (no sign-octant variants; same decisions) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
+/*
+ * Launch shape of the frame kernel: every workgroup owns at least min_blocks_per_wg 8x8
+ * pixel blocks (default 32) and a frame uses at most max_workgroups workgroups (0 = the
+ * default, two per CU, the most that can be resident).  With several frames in flight
+ * (one stream each) fewer, fuller workgroups per frame let the frames share the chip:
+ * one frame's tail runs beside the next frame's start.  Results never change.
+ */
+int mirt_set_grid(mirt_ctx *ctx, uint32_t min_blocks_per_wg, uint32_t max_workgroups);
+/*
+ * A stream on a hardware queue of its own, for one of several frames in flight.  HIP maps
+ * ordinary streams onto at most GPU_MAX_HW_QUEUES queues per process (default 4) and
+ * streams sharing a queue serialise; a stream created with an explicit CU mask (here:
+ * every CU) always gets a new queue.  Destroy with mirt_stream_destroy.
+ */
+int mirt_stream_create(mirt_ctx *ctx, void **stream);
+int mirt_stream_destroy(mirt_ctx *ctx, void *stream);
 
 /*
  * Diagnostic: evaluate one fp64 primitive of the kernels on the device for n inputs

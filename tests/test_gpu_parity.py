@@ -259,12 +259,13 @@ def test_device_tiles_packed_and_unpacked(ctx, env):
     dev = torch.device("cuda", 0)
     mut = env.mutable()
     frame = mut.to_frame()
-    for world in (1, 3):
+    for world, rgbv in ((1, False), (3, False), (3, True)):
         full = fbm.alloc_planes(W * H, dev, with_rgb=True)
         full.valid.zero_()
         for r in range(world):
             mine = fbm.assign(tiles, world, r)
-            packed = fbm.alloc_planes(fbm.pixels_of(mine), dev, with_rgb=True)
+            # rgbv: the multi-GPU packed form (one r|g|b|valid word per pixel), expanded by k_unpack
+            packed = fbm.alloc_planes(fbm.pixels_of(mine), dev, with_rgb=True, packed=rgbv)
             fbm.trace_tiles_device(ctx, frame, W, H, mine, packed, torch.cuda.current_stream().cuda_stream)
             fbm.unpack_device(ctx, W, H, mine, packed, full, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
@@ -412,3 +413,71 @@ def test_profile_counters(ctx, env):
     assert 0 < p["primary_tri_tests"] < 2 * 76800 * 968 / 5
     assert p["primary_ms_sum"] > 0 and p["frame_ms_sum"] >= p["primary_ms_sum"]
     assert p["stack_overflows"] == 0 and b["stack_overflows"] == 0
+
+
+@pytest.mark.parametrize("inflight,grid", [(3, (32, 0)), (4, (1, 0)), (2, (8, 7))])
+def test_frames_in_flight_alternating_cameras(ctx, env, inflight, grid):
+    """FrameSharder with several frames in flight (one stream and framebuffer each):
+    consecutive frames with DIFFERENT cameras overlap on the GPU; every framebuffer must
+    equal its own camera's frame drawn alone (a buffer reused too early would mix
+    frames).  Also exercises the launch-shape knob (mirt_set_grid: 1 block per
+    workgroup and the default), which never changes results."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import FrameSharder
+    W, H = 160, 120
+    base = env.mutable()
+    c = base.cam
+    cams = [c, rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.7, 0.3, 0.0])), c.forward, c.fov),
+            rt.Camera.new(tuple(np.asarray(c.pos) + np.array([-0.5, -0.2, 0.4])), c.forward, c.fov * 0.8)]
+    muts = [rt.EnvMutables(base.objects, base.lights, cm) for cm in cams]
+    frames = [m.to_frame() for m in muts]
+    refs = [rt.draw(env, W, H, m) for m in muts]
+    assert len({int(r.valid.sum()) for r in refs}) == 3  # three different images
+    ctx.set_grid(*grid)
+    try:
+        sh = FrameSharder(ctx, W, H, 0, 1, inflight=inflight)
+        order = [0, 1, 2, 1, 0, 2, 2, 1, 0, 1, 2, 0]
+        for q in order:
+            sh.render(frames[q])
+        sh.flush()
+        torch.cuda.synchronize()
+        for k in range(len(order) - inflight, len(order)):  # the last `inflight` frames' buffers
+            q = order[k]
+            got = sh.frames[k % inflight]
+            assert np.array_equal(got.valid.cpu().numpy(), refs[q].valid), f"frame {k} (camera {q}) valid differs"
+            assert np.array_equal(got.rgb8.cpu().numpy(), refs[q].rgb8), f"frame {k} (camera {q}) rgb8 differs"
+        assert sh.frame is sh.frames[(len(order) - 1) % inflight]
+    finally:
+        ctx.set_grid()
+
+
+def test_octant_child_test_changes_nothing(ctx, env):
+    """The sign-octant child-box test (near/far planes loaded pre-ordered, no min/max
+    sorting) must make exactly the culling decisions of the generic test: identical frames
+    AND identical traversal counters (node visits, leaf visits, ray-triangle tests) with
+    MIRT_OPT_NO_OCTANT, for views whose packets are uniform and views that mix signs."""
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    c = base.cam
+    cams = [c,
+            rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.9, 0.6, 0.2])), tuple(-np.asarray(c.pos)), c.fov),
+            rt.Camera.new((0.3, 0.2, 0.1), (0.2, -0.1, -1.0), 2.0)]  # inside the mesh's box: mixed signs
+    keys = ("primary_node_visits", "primary_leaf_visits", "primary_tri_tests", "shadow_node_visits",
+            "shadow_leaf_visits", "shadow_tri_tests", "hits")
+    try:
+        for cam in cams:
+            mut = rt.EnvMutables(base.objects, base.lights, cam)
+            res = []
+            for opt in (0, rt._lib.MIRT_OPT_NO_OCTANT):
+                ctx.set_options(opt)
+                ctx.profile_enable(True)
+                fb = rt.draw(env, 320, 240, mut)
+                ctx.profile_enable(False)
+                res.append((fb, ctx.profile_read()))
+            (a, pa), (b, pb) = res
+            assert np.array_equal(a.valid, b.valid) and np.array_equal(a.rgb, b.rgb) and np.array_equal(a.face, b.face)
+            assert {k: pa[k] for k in keys} == {k: pb[k] for k in keys}
+            assert pa["primary_node_visits"] > 0
+    finally:
+        ctx.set_options(0)

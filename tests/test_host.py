@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in sorted(names):
         assert hasattr(lib, n), f"libmirt.so does not export {n}"
     assert names == set(L.SIGNATURES), "ctypes signatures out of sync with include/*.h"
-    assert lib.mirt_abi_version() == 1
+    assert lib.mirt_abi_version() == 2
 
 
 def test_no_gpu_is_a_loud_error():
@@ -129,6 +129,20 @@ def test_camera_and_go_math_match_oracle():
     assert e.value.code == L.MIRT_E_CAMERA
 
 
+def test_tile_deal_spreads_rows_and_columns():
+    """assign(): column c of tile row r goes to rank (c + skew * r) % world; every rank
+    holds tiles in every row band and in many columns."""
+    from distributed_raytracer_amd.framebuffer import assign, plan_tiles, skew
+    assert [skew(n) for n in (1, 2, 3, 4, 6, 8)] == [1, 3, 2, 3, 5, 3]
+    tiles = plan_tiles(1920, 1080, 32)
+    for world in (2, 3, 8):
+        for r in range(world):
+            mine = assign(tiles, world, r)
+            assert len({y for _, y, _, _ in mine}) == 34  # every tile row
+            assert len({x for x, _, _, _ in mine}) == 60  # every tile column (skew spreads columns)
+            assert all(((x // 32) + skew(world) * (y // 32)) % world == r for x, y, _, _ in mine)
+
+
 def test_tile_plan_covers_screen_once():
     from distributed_raytracer_amd.framebuffer import assign, packed_capacity, pixels_of, plan_tiles
     for W, H, t in ((1920, 1080, 64), (320, 240, 48), (7, 5, 3), (64, 64, 64)):
@@ -183,7 +197,7 @@ def test_interleaved_tiles_balance_better_than_bisection():
         loads = [sum(work[x:x + w, y:y + h].sum() for x, y, w, h in rs) for rs in rects_per_rank]
         return max(loads) / (sum(loads) / len(loads))
 
-    tiles = plan_tiles(W, H, 16)
+    tiles = plan_tiles(W, H, 8)  # 1/16 of the 1080p frame's pixels: the bench's 32-px tiles scaled down
     inter = imbalance([assign(tiles, 8, r) for r in range(8)])
     bis = imbalance([[p] for p in master_partition((0, 0, W, H), 8)[0]])
     assert inter < 1.05 < bis
