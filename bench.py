@@ -260,7 +260,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), static frame-0 camera",
+            "data": ("synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), static frame-0 camera"
+                     if os.path.abspath(a.scene) == os.path.abspath(SCENE) else
+                     f"synthetic: {os.path.relpath(a.scene, ROOT)} ({tris} tris, {nl} lights), the scene's camera"),
             "config": {"workload": workload_name(a, W, H, tris, nl), "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
