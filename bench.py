@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--grid", default="",
                     help="frame-kernel launch shape 'MIN_BLOCKS_PER_WG,MAX_WORKGROUPS' (mirt_set_grid; "
                          "default: FrameSharder's choice for the frames in flight)")
+    ap.add_argument("--sharder", choices=("native", "torch"), default="native",
+                    help="per-frame driver: native (libmirt mirt_trace_frame, RCCL called from C) or torch "
+                         "(framebuffer.FrameSharder over torch.distributed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
@@ -148,7 +151,7 @@ def main():
             dist.init_process_group(backend)
 
     import distributed_raytracer_amd as rt
-    from distributed_raytracer_amd.framebuffer import FrameSharder
+    from distributed_raytracer_amd.framebuffer import FrameSharder, NativeFrameGroup
 
     W, H = a.width, a.height
     ctx = rt.Context(local)
@@ -161,7 +164,19 @@ def main():
     frame = dataclasses.replace(env.mutable(), max_bounces=a.bounces).to_frame()
     tris = sum(len(m.face_v) for m in env.meshes)
     nl = len(env.mutable().lights)
-    sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight)
+    # native: the per-frame trace + RCCL gather + unpack in libmirt (mirt_trace_frame), one C
+    # call per frame; torch: the same sequence through torch.distributed (FrameSharder), used
+    # for the gloo rehearsal (RCCL cannot put two ranks on one GPU) and as a fallback
+    sharder = a.sharder if not (world > 1 and backend != "nccl") else "torch"
+    sh = None
+    if sharder == "native":
+        try:
+            sh = NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight)
+        except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
+            print(f"native frame group unavailable ({e}); using the torch.distributed sharder", file=sys.stderr)
+            sharder = f"torch (native failed: {e})"
+    if sh is None:
+        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight)
     if a.grid:
         ctx.set_grid(*(int(x) for x in a.grid.split(",")))
     dev = torch.device("cuda", local)
@@ -268,6 +283,7 @@ def main():
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
             "frames_in_flight": sh.F,
+            "sharder": sharder,
             "frame_latency_ms": round(latency * 1e3, 4),
             "primary_mrays_s": round(primary / (ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),

@@ -5,7 +5,9 @@
 // frames.  Each call takes a "slot" (HIP stream + workspace + events) from a pool under
 // a mutex and returns it afterwards; meshes are immutable after upload.  hipSetDevice is
 // called on every entry because cgo calls can land on any OS thread.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
@@ -461,7 +463,11 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         per_wg = std::max<uint32_t>(c->min_blocks_per_wg, 1);
         max_wg = c->max_workgroups ? std::min<uint64_t>(c->max_workgroups, (uint64_t)2 * c->cus) : (uint64_t)2 * c->cus;
     }
-    const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)sl->nblocks + per_wg - 1) / per_wg, max_wg));
+    // at least min(blocks, CUs) workgroups: a small tile list (a BulkTrace order, one
+    // rank's share) keeps one block per wave rather than queueing heavy blocks on few waves
+    const uint64_t want = std::max<uint64_t>(((uint64_t)sl->nblocks + per_wg - 1) / per_wg,
+                                             std::min<uint64_t>(sl->nblocks, (uint64_t)c->cus));
+    const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, max_wg));
     // k_trace: workgroup w's hit region holds one chunk per block it owns
     wa.wg_cap = (uint32_t)(((uint64_t)sl->nblocks + pgrid - 1) / pgrid * 64);
     const uint64_t hit_slots = std::max<uint64_t>((uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap);
@@ -1084,6 +1090,336 @@ int mirt_set_grid(mirt_ctx* c, uint32_t min_blocks_per_wg, uint32_t max_workgrou
     std::lock_guard<std::mutex> g(c->mu);
     c->min_blocks_per_wg = min_blocks_per_wg;
     c->max_workgroups = max_workgroups;
+    return MIRT_OK;
+}
+
+}  // extern "C"
+
+// ==================================================================== multi-GPU frame group
+// SURVEY.md §8(b) mirt_trace_frame: the frame split over the GPUs of one box, one process
+// per GPU, the packed tiles gathered to the root over RCCL and unpacked there — the whole
+// per-frame sequence in native code (the torch.distributed version in framebuffer.py costs
+// ~60 us of host time per frame, tools/dist_host_probe.py).  RCCL is opened at run time
+// (dlopen of librccl.so.1: the copy torch already loaded, else /opt/rocm's), so the library
+// loads without it and single-GPU callers never touch it.
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl load_rccl() {
+    Rccl R;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        const char* e = dlerror();
+        R.err = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+        return R;
+    }
+#define MIRT_RCCL_SYM(field, name)                                  \
+    R.field = (decltype(R.field))dlsym(h, name);                    \
+    if (!R.field) {                                                 \
+        R.err = std::string("librccl.so.1 does not export ") + name; \
+        return R;                                                   \
+    }
+    MIRT_RCCL_SYM(get_unique_id, "ncclGetUniqueId")
+    MIRT_RCCL_SYM(comm_init_rank, "ncclCommInitRank")
+    MIRT_RCCL_SYM(comm_destroy, "ncclCommDestroy")
+    MIRT_RCCL_SYM(send, "ncclSend")
+    MIRT_RCCL_SYM(recv, "ncclRecv")
+    MIRT_RCCL_SYM(group_start, "ncclGroupStart")
+    MIRT_RCCL_SYM(group_end, "ncclGroupEnd")
+    MIRT_RCCL_SYM(error_string, "ncclGetErrorString")
+#undef MIRT_RCCL_SYM
+    R.ok = true;
+    return R;
+}
+
+const Rccl& rccl() {
+    static const Rccl R = load_rccl();  // thread-safe one-time initialisation
+    return R;
+}
+
+#define RCCL_TRY(expr)                                                                           \
+    do {                                                                                         \
+        ncclResult_t _r = (expr);                                                                \
+        if (_r != ncclSuccess) return fail(MIRT_E_DEVICE, std::string(#expr) + ": " + rccl().error_string(_r)); \
+    } while (0)
+
+// The tile deal of framebuffer.py (plan_tiles + assign): raster tiles; the tile in column c
+// of tile row r goes to rank (c + s r) % world, s the smallest integer >= sqrt(world)
+// coprime with world.
+uint32_t deal_skew(uint32_t world) {
+    uint32_t s = 1;
+    auto gcd = [](uint32_t a, uint32_t b) {
+        while (b) {
+            const uint32_t t = a % b;
+            a = b;
+            b = t;
+        }
+        return a;
+    };
+    while (s * s < world || gcd(s, world) != 1) ++s;
+    return s;
+}
+
+void plan_rank_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t world, uint32_t rank, std::vector<mirt_tile>& out) {
+    out.clear();
+    const uint32_t cols = (W + tile - 1) / tile;
+    const uint32_t s = deal_skew(world);
+    uint64_t k = 0;
+    for (uint32_t y = 0; y < H; y += tile)
+        for (uint32_t x = 0; x < W; x += tile, ++k)
+            if (world <= 1 || ((k % cols) + (uint64_t)s * (k / cols)) % world == rank)
+                out.push_back(mirt_tile{x, y, std::min(tile, W - x), std::min(tile, H - y)});
+}
+
+uint64_t tiles_pixels(const std::vector<mirt_tile>& t) {
+    uint64_t n = 0;
+    for (const mirt_tile& x : t) n += (uint64_t)x.w * x.h;
+    return n;
+}
+
+// Trace a tile list into device planes on stream s (the body of mirt_trace_tiles_async).
+int trace_tiles_on(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
+                   const OutPlanes& out, hipStream_t s) {
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    Slot* sl = nullptr;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    uint64_t pixels = 0, tris = 0;
+    if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, nullptr, &pixels, &tris)) != MIRT_OK) {
+        (void)hipStreamSynchronize(s);
+        sl->pending = false;
+        return r;
+    }
+    return MIRT_OK;
+}
+
+hipError_t stream_with_queue(int cus, hipStream_t* s) {
+    std::vector<uint32_t> mask(((uint32_t)cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
+}  // namespace
+
+struct mirt_group {
+    mirt_ctx* c = nullptr;
+    int rank = 0, world = 1, root = 0;
+    uint32_t W = 0, H = 0, F = 1;
+    bool tiled = false;               // packed rgbv tiles + unpack (world > 1, or a tiled rehearsal)
+    ncclComm_t comm = nullptr;
+    hipStream_t comm_stream = nullptr;  // every RCCL call, in issue order (the same on every rank)
+    std::vector<hipStream_t> streams;   // frame k runs on streams[k % F]
+    std::vector<hipEvent_t> ev_traced, ev_gathered, ev_done;
+    std::vector<mirt_tile> mine;
+    uint64_t cap = 0;                   // largest rank share (pixels): every rank's gather size
+    std::vector<uint32_t*> packed;      // non-root: my packed rgbv plane per frame slot
+    std::vector<uint32_t*> gathered;    // root: world * cap rgbv words per frame slot
+    std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
+    TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
+    uint32_t n_unpack = 0;
+    uint64_t k = 0;                     // frames enqueued
+};
+
+extern "C" {
+
+int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t world, uint32_t rank, mirt_tile* out,
+                    uint32_t cap) {
+    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
+    std::vector<mirt_tile> t;
+    plan_rank_tiles(W, H, tile, world, rank, t);
+    if (out) {
+        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
+        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
+    }
+    return (int)t.size();
+}
+
+int mirt_group_unique_id(uint8_t* id) {
+    if (!id) return fail(MIRT_E_INVALID, "id is NULL");
+    if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
+    ncclUniqueId u;
+    RCCL_TRY(rccl().get_unique_id(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return MIRT_OK;
+}
+
+void mirt_group_destroy(mirt_group* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->c->device);
+    for (hipStream_t s : g->streams)
+        if (s) (void)hipStreamSynchronize(s);
+    if (g->comm_stream) (void)hipStreamSynchronize(g->comm_stream);
+    if (g->comm) (void)rccl().comm_destroy(g->comm);
+    for (uint32_t* p : g->packed)
+        if (p) (void)hipFree(p);
+    for (uint32_t* p : g->gathered)
+        if (p) (void)hipFree(p);
+    if (g->d_unpack) (void)hipFree(g->d_unpack);
+    for (auto* v : {&g->ev_traced, &g->ev_gathered, &g->ev_done})
+        for (hipEvent_t e : *v)
+            if (e) (void)hipEventDestroy(e);
+    for (hipStream_t s : g->streams)
+        if (s) (void)hipStreamDestroy(s);
+    if (g->comm_stream) (void)hipStreamDestroy(g->comm_stream);
+    delete g;
+}
+
+int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world, uint32_t W, uint32_t H,
+                      uint32_t tile, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL context or out");
+    *out = nullptr;
+    if (world < 1 || rank < 0 || rank >= world) return fail(MIRT_E_INVALID, "bad rank / world");
+    if (!W || !H || W > 65535 || H > 65535) return fail(MIRT_E_INVALID, "bad screen size");
+    if (inflight < 1 || inflight > 16) return fail(MIRT_E_INVALID, "inflight must be 1..16");
+    if (world > 1 && !unique_id) return fail(MIRT_E_INVALID, "world > 1 needs the root's unique id");
+    if (world > 1 && tile == 0) return fail(MIRT_E_INVALID, "world > 1 needs a tile size");
+    const bool is_root = rank == 0;
+    if (is_root && !fbs) return fail(MIRT_E_INVALID, "the root needs its framebuffers");
+    HIP_TRY(hipSetDevice(c->device));
+    std::unique_ptr<mirt_group, void (*)(mirt_group*)> g(new mirt_group(), mirt_group_destroy);
+    g->c = c;
+    g->rank = rank;
+    g->world = world;
+    g->W = W;
+    g->H = H;
+    g->F = inflight;
+    g->tiled = tile > 0;
+    if (g->tiled) {
+        plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)rank, g->mine);
+        for (int r = 0; r < world; ++r) {
+            std::vector<mirt_tile> t;
+            plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)r, t);
+            g->cap = std::max(g->cap, tiles_pixels(t));
+        }
+        if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
+    } else {
+        g->mine.push_back(mirt_tile{0, 0, W, H});
+        g->cap = (uint64_t)W * H;
+    }
+    g->streams.assign(inflight, nullptr);
+    g->ev_traced.assign(inflight, nullptr);
+    g->ev_gathered.assign(inflight, nullptr);
+    g->ev_done.assign(inflight, nullptr);
+    for (uint32_t j = 0; j < inflight; ++j) {
+        HIP_TRY(stream_with_queue(c->cus, &g->streams[j]));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
+    }
+    if (is_root)
+        for (uint32_t j = 0; j < inflight; ++j)
+            g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
+    if (g->tiled) {
+        if (is_root) {
+            g->gathered.assign(inflight, nullptr);
+            for (uint32_t j = 0; j < inflight; ++j)
+                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)world * g->cap * 4));
+            std::vector<TileDesc> td;
+            for (int r = 0; r < world; ++r) {
+                std::vector<mirt_tile> t;
+                plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)r, t);
+                uint64_t o = (uint64_t)r * g->cap;
+                for (const mirt_tile& x : t) {
+                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, {0, 0}});
+                    o += (uint64_t)x.w * x.h;
+                }
+            }
+            g->n_unpack = (uint32_t)td.size();
+            HIP_TRY(hipMalloc((void**)&g->d_unpack, td.size() * sizeof(TileDesc)));
+            HIP_TRY(hipMemcpy(g->d_unpack, td.data(), td.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+        } else {
+            g->packed.assign(inflight, nullptr);
+            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->packed[j], g->cap * 4));
+        }
+    }
+    if (world > 1) {
+        if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
+        HIP_TRY(stream_with_queue(c->cus, &g->comm_stream));
+        ncclUniqueId u;
+        memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
+        RCCL_TRY(rccl().comm_init_rank(&g->comm, world, u, rank));
+    }
+    *out = g.release();
+    return MIRT_OK;
+}
+
+int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
+    if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
+    mirt_ctx* c = g->c;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t j = (uint32_t)(g->k % g->F);
+    hipStream_t s = g->streams[j];
+    const bool is_root = g->rank == g->root;
+    // frame k - F used this slot's buffers: its gather must be done with them
+    if (g->tiled && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
+    OutPlanes out{};
+    if (!g->tiled) {
+        out = g->fb[j];
+    } else {
+        out.rgbv = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->packed[j];
+    }
+    int r = trace_tiles_on(c, f, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), out, s);
+    if (r != MIRT_OK) return r;
+    if (g->tiled) {
+        if (g->world > 1) {
+            const Rccl& R = rccl();
+            HIP_TRY(hipEventRecord(g->ev_traced[j], s));
+            HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[j], 0));
+            const size_t bytes = g->cap * 4;
+            RCCL_TRY(R.group_start());
+            if (is_root) {
+                for (int q = 0; q < g->world; ++q)
+                    if (q != g->root)
+                        RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, bytes, ncclUint8, q, g->comm,
+                                        g->comm_stream));
+            } else {
+                RCCL_TRY(R.send(g->packed[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
+            }
+            RCCL_TRY(R.group_end());
+            HIP_TRY(hipEventRecord(g->ev_gathered[j], g->comm_stream));
+            if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
+        } else {
+            HIP_TRY(hipEventRecord(g->ev_gathered[j], s));
+        }
+        if (is_root) {
+            OutPlanes src{};
+            src.rgbv = g->gathered[j];
+            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, (uint64_t)g->world * g->cap, g->H, src, g->fb[j], s));
+        }
+    }
+    HIP_TRY(hipEventRecord(g->ev_done[j], s));
+    if (index) *index = g->k;
+    ++g->k;
+    return MIRT_OK;
+}
+
+int mirt_group_wait(mirt_group* g, void* stream) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    HIP_TRY(hipSetDevice(g->c->device));
+    const uint64_t used = std::min<uint64_t>(g->k, g->F);
+    for (uint64_t j = 0; j < used; ++j) {
+        if (stream) {
+            HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[j], 0));
+        } else {
+            HIP_TRY(hipEventSynchronize(g->ev_done[j]));
+        }
+    }
+    if (!stream && g->comm_stream) HIP_TRY(hipStreamSynchronize(g->comm_stream));
     return MIRT_OK;
 }
 

@@ -363,3 +363,83 @@ class FrameSharder:
     @property
     def last_packed(self):
         return self.bufs[(self._k - 1) % self._nb] if self.world > 1 else None
+
+
+def plan_rank_tiles_native(W: int, H: int, tile: int, world: int, rank: int) -> List[TileT]:
+    """The C++ tile deal of mirt_group (mirt_plan_tiles); equals assign(plan_tiles(...))."""
+    n = L.lib().mirt_plan_tiles(W, H, tile, world, rank, None, 0)
+    L.check(min(n, 0))
+    arr = (L.Tile * max(n, 1))()
+    L.check(min(L.lib().mirt_plan_tiles(W, H, tile, world, rank, C.cast(arr, C.c_void_p), n), 0))
+    return [(t.x, t.y, t.w, t.h) for t in arr[:n]]
+
+
+class NativeFrameGroup:
+    """The multi-GPU frame in native code (mirt.h mirt_group_* / mirt_trace_frame): the
+    same tile deal, rgbv packing, RCCL gather and unpack as FrameSharder, but one C call per
+    frame — the RCCL send/recv group runs on the library's own stream, so no Python
+    collective, stream switch or event is on the per-frame path.  torch.distributed is only
+    the bootstrap: rank 0's RCCL unique id is broadcast over the caller's process group.
+
+    world == 1: the whole screen as one tile straight into the framebuffer (tile=None), or
+    the tiled path rehearsed on one GPU (tile > 0: packed rgbv + unpack, no RCCL).
+    Frames in flight: frame k on the library's stream k % F, framebuffer frames[k % F]
+    (rank 0 only), every stream on a hardware queue of its own."""
+
+    def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 32,
+                 inflight: int = 4, group=None, with_rgb: bool = False):
+        import torch
+        self.ctx, self.W, self.H, self.rank, self.world = ctx, W, H, rank, world
+        self.F = max(1, int(inflight))
+        self.device = torch.device("cuda", ctx.device)
+        tile = (tile or 0) if world == 1 else int(tile or 32)
+        self.tiles_all = [(0, 0, W, H)] if tile == 0 else plan_tiles(W, H, tile)
+        self.mine = [(0, 0, W, H)] if tile == 0 else plan_rank_tiles_native(W, H, tile, world, rank)
+        if self.F > 1:
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            ctx.set_grid(32, max(1, (4 * cus) // self.F) if self.F > 2 else 0)
+        uid = (C.c_uint8 * 128)()
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.zeros(128, dtype=torch.uint8, device=self.device if dist.get_backend(group) == "nccl" else "cpu")
+            if rank == 0:
+                L.check(L.lib().mirt_group_unique_id(C.cast(uid, C.c_void_p)))
+                t.copy_(torch.frombuffer(bytearray(bytes(uid)), dtype=torch.uint8))
+            dist.broadcast(t, src=0, group=group)
+            uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+        self.frames = [alloc_planes(W * H, self.device, with_rgb) for _ in range(self.F)] if rank == 0 else None
+        fbs = (L.Outputs * self.F)(*[p.outputs() for p in self.frames]) if self.frames else None
+        self._h = C.c_void_p()
+        L.check(L.lib().mirt_group_create(ctx.handle, C.cast(uid, C.c_void_p) if world > 1 else None, rank, world,
+                                          W, H, tile, self.F, C.cast(fbs, C.c_void_p) if fbs else None,
+                                          C.byref(self._h)))
+        self._k = 0
+        self._idx = C.c_uint64()
+
+    def render(self, frame_and_keep) -> None:
+        """Enqueue the next frame (no host sync, no Python collective)."""
+        fr, _keep = frame_and_keep
+        L.check(L.lib().mirt_trace_frame(self._h, C.byref(fr), C.byref(self._idx)))
+        self._k += 1
+
+    def flush(self) -> None:
+        """torch's current stream waits for every enqueued frame (gathers and unpacks included)."""
+        import torch
+        L.check(L.lib().mirt_group_wait(self._h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    @property
+    def frame(self) -> Optional[DevicePlanes]:
+        if self.frames is None:
+            return None
+        return self.frames[(self._k - 1) % self.F] if self._k else self.frames[0]
+
+    def close(self) -> None:
+        if self._h:
+            L.lib().mirt_group_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -481,3 +481,36 @@ def test_octant_child_test_changes_nothing(ctx, env):
             assert pa["primary_node_visits"] > 0
     finally:
         ctx.set_options(0)
+
+
+@pytest.mark.parametrize("tile,inflight", [(None, 4), (32, 3), (48, 1)])
+def test_native_frame_group_matches_draw(ctx, env, tile, inflight):
+    """mirt_trace_frame (the native multi-GPU frame driver) on one GPU: the whole screen
+    (tile=None) or the tiled path rehearsed with world = 1 (packed rgbv tiles, the unpack
+    table with per-rank offsets), frames in flight with alternating cameras; every
+    framebuffer equals its camera's frame drawn alone."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W, H = 160, 120
+    base = env.mutable()
+    c = base.cam
+    cams = [c, rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.7, 0.3, 0.0])), c.forward, c.fov)]
+    muts = [rt.EnvMutables(base.objects, base.lights, cm) for cm in cams]
+    frames = [m.to_frame() for m in muts]
+    refs = [rt.draw(env, W, H, m) for m in muts]
+    try:
+        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight)
+        order = [0, 1, 1, 0, 1, 0, 0, 1]
+        for q in order:
+            g.render(frames[q])
+        g.flush()
+        torch.cuda.synchronize()
+        for k in range(len(order) - inflight, len(order)):
+            got = g.frames[k % inflight]
+            q = order[k]
+            assert np.array_equal(got.valid.cpu().numpy(), refs[q].valid), f"frame {k} valid differs"
+            assert np.array_equal(got.rgb8.cpu().numpy(), refs[q].rgb8), f"frame {k} rgb8 differs"
+        g.close()
+    finally:
+        ctx.set_grid()

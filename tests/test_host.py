@@ -201,3 +201,13 @@ def test_interleaved_tiles_balance_better_than_bisection():
     inter = imbalance([assign(tiles, 8, r) for r in range(8)])
     bis = imbalance([[p] for p in master_partition((0, 0, W, H), 8)[0]])
     assert inter < 1.05 < bis
+
+
+def test_native_tile_deal_equals_python():
+    """mirt_plan_tiles (the C++ deal of mirt_group) == assign(plan_tiles(...))."""
+    from distributed_raytracer_amd.framebuffer import assign, plan_rank_tiles_native, plan_tiles
+    for W, H, t in ((1920, 1080, 32), (1920, 1080, 64), (320, 240, 48), (7, 5, 3)):
+        tiles = plan_tiles(W, H, t)
+        for world in (1, 2, 3, 4, 6, 8):
+            for r in range(world):
+                assert plan_rank_tiles_native(W, H, t, world, r) == assign(tiles, world, r), (W, H, t, world, r)
