@@ -146,6 +146,31 @@ int dev_grow(T*& p, size_t& cap, size_t need) {
 // enqueueing frames back to back runs ahead of the GPU instead of waiting per frame.
 constexpr size_t kMaxIdleBlockSlots = 8;
 
+// First use of a slot: its event and counters.  The slot's own stream is created only by
+// the synchronous entry points that use it (slot_stream): every stream takes one of the
+// process's few hardware queues, which the caller's streams of frames in flight need.
+int slot_init(Slot* s) {
+    if (s->done) return MIRT_OK;
+    HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    HIP_TRY(hipMalloc((void**)&s->counters, 2 * kCntN * sizeof(cnt_t)));
+    HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
+    HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
+    HIP_TRY(hipMemset(s->counters, 0, 2 * kCntN * sizeof(cnt_t)));
+    return MIRT_OK;
+}
+
+void slot_free(Slot* s) {
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0,
+                    (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf})
+        if (p) (void)hipFree(p);
+    if (s->h_blocks) (void)hipHostFree(s->h_blocks);
+    if (s->h_tiles) (void)hipHostFree(s->h_tiles);
+    if (s->h_summary) (void)hipHostFree(s->h_summary);
+    if (s->done) (void)hipEventDestroy(s->done);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+}
+
 int slot_acquire(mirt_ctx* c, Slot*& out) {
     {
         std::lock_guard<std::mutex> g(c->mu);
@@ -170,16 +195,8 @@ int slot_acquire(mirt_ctx* c, Slot*& out) {
         }
     }
     Slot* s = out;
-    if (!s->done) {
-        // the slot's own stream is created only by the synchronous entry points that use
-        // it (slot_stream): every stream takes one of the process's few hardware queues,
-        // which the caller's streams of frames in flight need
-        HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
-        HIP_TRY(hipMalloc((void**)&s->counters, 2 * kCntN * sizeof(cnt_t)));
-        HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
-        HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
-        HIP_TRY(hipMemset(s->counters, 0, 2 * kCntN * sizeof(cnt_t)));
-    }
+    int r = slot_init(s);
+    if (r != MIRT_OK) return r;
     // previous asynchronous use of this slot's staging/workspace must be finished
     if (s->pending) {
         HIP_TRY(hipEventSynchronize(s->done));
@@ -597,25 +614,7 @@ int mirt_create(int device, mirt_ctx** out) {
 void mirt_destroy(mirt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (auto& sp : c->slots) {
-        Slot* s = sp.get();
-        if (s->stream) (void)hipStreamSynchronize(s->stream);
-        if (s->hits) (void)hipFree(s->hits);
-        if (s->litw) (void)hipFree(s->litw);
-        if (s->blkdone) (void)hipFree(s->blkdone);
-        if (s->dir0) (void)hipFree(s->dir0);
-        if (s->ph0) (void)hipFree(s->ph0);
-        if (s->counters) (void)hipFree(s->counters);
-        if (s->d_tiles) (void)hipFree(s->d_tiles);
-        if (s->d_blocks) (void)hipFree(s->d_blocks);
-        if (s->h_blocks) (void)hipHostFree(s->h_blocks);
-        if (s->h_tiles) (void)hipHostFree(s->h_tiles);
-        if (s->summary) (void)hipFree(s->summary);
-        if (s->h_summary) (void)hipHostFree(s->h_summary);
-        if (s->out_buf) (void)hipFree(s->out_buf);
-        if (s->done) (void)hipEventDestroy(s->done);
-        if (s->stream) (void)hipStreamDestroy(s->stream);
-    }
+    for (auto& sp : c->slots) slot_free(sp.get());
     for (auto* v : {&c->prof_pending, &c->prof_free})
         for (auto& r : *v) {
             for (auto e : r.ev)
@@ -1191,23 +1190,6 @@ uint64_t tiles_pixels(const std::vector<mirt_tile>& t) {
     return n;
 }
 
-// Trace a tile list into device planes on stream s (the body of mirt_trace_tiles_async).
-int trace_tiles_on(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                   const OutPlanes& out, hipStream_t s) {
-    int r = check_frame(c, f);
-    if (r != MIRT_OK) return r;
-    Slot* sl = nullptr;
-    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
-    SlotGuard guard{c, sl};
-    uint64_t pixels = 0, tris = 0;
-    if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, nullptr, &pixels, &tris)) != MIRT_OK) {
-        (void)hipStreamSynchronize(s);
-        sl->pending = false;
-        return r;
-    }
-    return MIRT_OK;
-}
-
 hipError_t stream_with_queue(int cus, hipStream_t* s) {
     std::vector<uint32_t> mask(((uint32_t)cus + 31) / 32, 0u);
     for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
@@ -1232,6 +1214,9 @@ struct mirt_group {
     std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
     TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
     uint32_t n_unpack = 0;
+    // one workspace per frame slot: frame k reuses slot k % F after frame k - F on the same
+    // stream, so no slot pool, event query or host wait is on the per-frame path
+    std::vector<std::unique_ptr<Slot>> slots;
     uint64_t k = 0;                     // frames enqueued
 };
 
@@ -1265,6 +1250,7 @@ void mirt_group_destroy(mirt_group* g) {
         if (s) (void)hipStreamSynchronize(s);
     if (g->comm_stream) (void)hipStreamSynchronize(g->comm_stream);
     if (g->comm) (void)rccl().comm_destroy(g->comm);
+    for (auto& sl : g->slots) slot_free(sl.get());
     for (uint32_t* p : g->packed)
         if (p) (void)hipFree(p);
     for (uint32_t* p : g->gathered)
@@ -1310,6 +1296,11 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     } else {
         g->mine.push_back(mirt_tile{0, 0, W, H});
         g->cap = (uint64_t)W * H;
+    }
+    for (uint32_t j = 0; j < inflight; ++j) {
+        g->slots.emplace_back(new Slot());
+        int r = slot_init(g->slots.back().get());
+        if (r != MIRT_OK) return r;
     }
     g->streams.assign(inflight, nullptr);
     g->ev_traced.assign(inflight, nullptr);
@@ -1365,6 +1356,8 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     const uint32_t j = (uint32_t)(g->k % g->F);
     hipStream_t s = g->streams[j];
     const bool is_root = g->rank == g->root;
+    // back-pressure: the host runs at most F frames ahead (frame k - F must have finished)
+    if (g->k >= g->F) HIP_TRY(hipEventSynchronize(g->ev_done[j]));
     // frame k - F used this slot's buffers: its gather must be done with them
     if (g->tiled && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
     OutPlanes out{};
@@ -1373,8 +1366,14 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     } else {
         out.rgbv = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->packed[j];
     }
-    int r = trace_tiles_on(c, f, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), out, s);
+    int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
+    uint64_t pixels = 0, tris = 0;
+    if ((r = enqueue_trace(c, g->slots[j].get(), f, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), out, s,
+                           nullptr, &pixels, &tris)) != MIRT_OK) {
+        (void)hipStreamSynchronize(s);
+        return r;
+    }
     if (g->tiled) {
         if (g->world > 1) {
             const Rccl& R = rccl();
