@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--tile", type=int, default=8, help="multi-GPU deal unit: tile width (pixels)")
+    ap.add_argument("--tile-h", type=int, default=0,
+                    help="tile height; 0 = full-height column strips (contiguous in the column-major framebuffer)")
     ap.add_argument("--scene", default=SCENE)
     ap.add_argument("--bounces", type=int, default=0,
                     help="configs[4] reflection EXTENSION: bounces per primary hit (0 = the reference)")
@@ -171,12 +173,13 @@ def main():
     sh = None
     if sharder == "native":
         try:
-            sh = NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight)
+            sh = NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
+                                  tile_h=a.tile_h)
         except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
             print(f"native frame group unavailable ({e}); using the torch.distributed sharder", file=sys.stderr)
             sharder = f"torch (native failed: {e})"
     if sh is None:
-        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight)
+        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight, tile_h=a.tile_h)
     if a.grid:
         ctx.set_grid(*(int(x) for x in a.grid.split(",")))
     dev = torch.device("cuda", local)

@@ -123,12 +123,13 @@ SIGNATURES = {
     "mirt_set_grid": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "mirt_stream_create": (C.c_int, [_P, C.POINTER(_P)]),
     "mirt_group_unique_id": (C.c_int, [_P]),
-    "mirt_group_create": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
-                                    C.POINTER(_P)]),
+    "mirt_group_create": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, _P, C.POINTER(_P)]),
     "mirt_trace_frame": (C.c_int, [_P, C.POINTER(Frame), C.POINTER(C.c_uint64)]),
     "mirt_group_wait": (C.c_int, [_P, _P]),
     "mirt_group_destroy": (None, [_P]),
-    "mirt_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint32]),
+    "mirt_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
+                                  C.c_uint32]),
     "mirt_stream_destroy": (C.c_int, [_P, _P]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),

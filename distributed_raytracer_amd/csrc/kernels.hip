@@ -1622,45 +1622,65 @@ MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
 }
 
 // ---------------------------------------------------------------- unpack
-// packed tile-major planes -> W x H framebuffer, pixel (x, y) at x*H + y.
-__global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint64_t npix,
-                                                uint32_t H, OutPlanes src, OutPlanes dst) {
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix;
-         p += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t lo = 0, hi = ntiles - 1;
-        while (lo < hi) {
-            uint32_t mid = (lo + hi + 1) >> 1;
-            if (tiles[mid].out_off <= p)
-                lo = mid;
-            else
-                hi = mid - 1;
+// packed tile-major planes -> W x H framebuffer, pixel (x, y) at x*H + y.  One workgroup
+// per tile (grid-stride over tiles): the tile's descriptor is one scalar load, and the
+// tile's column runs are contiguous in both layouts.  A packed rgbv plane with 4-aligned
+// columns (tile height, tile row and H multiples of 4: the 32-px multi-GPU tiles) goes four
+// pixels per thread — one 16-byte load, the rgb8 run as three dwords, the valid run as one
+// — instead of byte stores; anything else goes pixel by pixel.  Planes absent from the
+// source are not written.
+__device__ __forceinline__ void unpack_pixel(const OutPlanes& src, const OutPlanes& dst, uint64_t p, uint64_t q) {
+    if (src.valid && dst.valid) dst.valid[q] = src.valid[p];
+    if (src.face && dst.face) dst.face[q] = src.face[p];
+    if (src.object && dst.object) dst.object[q] = src.object[p];
+    if (src.rgb && dst.rgb) {
+        dst.rgb[3 * q] = src.rgb[3 * p];
+        dst.rgb[3 * q + 1] = src.rgb[3 * p + 1];
+        dst.rgb[3 * q + 2] = src.rgb[3 * p + 2];
+    }
+    if (src.rgb8 && dst.rgb8) {
+        dst.rgb8[3 * q] = src.rgb8[3 * p];
+        dst.rgb8[3 * q + 1] = src.rgb8[3 * p + 1];
+        dst.rgb8[3 * q + 2] = src.rgb8[3 * p + 2];
+    }
+    if (src.rgbv) {  // packed word -> rgb8 + valid (and/or a packed framebuffer)
+        const uint32_t v = src.rgbv[p];
+        if (dst.rgbv) dst.rgbv[q] = v;
+        if (dst.valid && !src.valid) dst.valid[q] = (uint8_t)(v >> 24);
+        if (dst.rgb8 && !src.rgb8) {
+            dst.rgb8[3 * q] = (uint8_t)v;
+            dst.rgb8[3 * q + 1] = (uint8_t)(v >> 8);
+            dst.rgb8[3 * q + 2] = (uint8_t)(v >> 16);
         }
-        const TileDesc td = tiles[lo];
-        const uint64_t local = p - td.out_off;
-        if (local >= (uint64_t)td.w * td.h) continue;  // padding between ranks' packed buffers
-        const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
-        const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
-        if (src.valid && dst.valid) dst.valid[q] = src.valid[p];
-        if (src.face && dst.face) dst.face[q] = src.face[p];
-        if (src.object && dst.object) dst.object[q] = src.object[p];
-        if (src.rgb && dst.rgb) {
-            dst.rgb[3 * q] = src.rgb[3 * p];
-            dst.rgb[3 * q + 1] = src.rgb[3 * p + 1];
-            dst.rgb[3 * q + 2] = src.rgb[3 * p + 2];
-        }
-        if (src.rgb8 && dst.rgb8) {
-            dst.rgb8[3 * q] = src.rgb8[3 * p];
-            dst.rgb8[3 * q + 1] = src.rgb8[3 * p + 1];
-            dst.rgb8[3 * q + 2] = src.rgb8[3 * p + 2];
-        }
-        if (src.rgbv) {  // packed word -> rgb8 + valid (and/or a packed framebuffer)
-            const uint32_t v = src.rgbv[p];
-            if (dst.rgbv) dst.rgbv[q] = v;
-            if (dst.valid && !src.valid) dst.valid[q] = (uint8_t)(v >> 24);
-            if (dst.rgb8 && !src.rgb8) {
-                dst.rgb8[3 * q] = (uint8_t)v;
-                dst.rgb8[3 * q + 1] = (uint8_t)(v >> 8);
-                dst.rgb8[3 * q + 2] = (uint8_t)(v >> 16);
+    }
+}
+__global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t H,
+                                                OutPlanes src, OutPlanes dst) {
+    const bool only_rgbv = src.rgbv && !src.rgb && !src.rgb8 && !src.valid && !src.face && !src.object;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t tt = __builtin_amdgcn_readfirstlane(t);
+        const TileDesc td = tiles[tt];
+        const uint64_t n = (uint64_t)td.w * td.h;
+        if (only_rgbv && (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0 && (td.out_off & 3u) == 0) {
+            for (uint64_t p4 = threadIdx.x; p4 < n / 4; p4 += blockDim.x) {
+                const uint64_t local = p4 * 4;
+                const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
+                const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);  // multiple of 4
+                const uint4 v = *(const uint4*)(src.rgbv + td.out_off + local);
+                if (dst.rgbv) *(uint4*)(dst.rgbv + q) = v;
+                if (dst.valid)
+                    *(uint32_t*)(dst.valid + q) = (v.x >> 24) | ((v.y >> 24) << 8) | ((v.z >> 24) << 16) | ((v.w >> 24) << 24);
+                if (dst.rgb8) {  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3 (3q is a multiple of 4)
+                    uint32_t* o = (uint32_t*)(dst.rgb8 + 3 * q);
+                    o[0] = (v.x & 0xffffffu) | (v.y << 24);
+                    o[1] = ((v.y >> 8) & 0xffffu) | (v.z << 16);
+                    o[2] = ((v.z >> 16) & 0xffu) | ((v.w & 0xffffffu) << 8);
+                }
+            }
+        } else {
+            for (uint64_t local = threadIdx.x; local < n; local += blockDim.x) {
+                const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
+                unpack_pixel(src, dst, td.out_off + local, (uint64_t)(td.x + lx) * H + (td.y + ly));
             }
         }
     }
@@ -1749,9 +1769,9 @@ hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes
 
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s) {
-    uint64_t blocks = (npix + 255) / 256;
-    int grid = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
-    hipLaunchKernelGGL(k_unpack, dim3(grid), dim3(256), 0, s, tiles, ntiles, npix, H, src, dst);
+    (void)npix;
+    const int grid = (int)(ntiles < 8192u ? (ntiles ? ntiles : 1u) : 8192u);
+    hipLaunchKernelGGL(k_unpack, dim3(grid), dim3(256), 0, s, tiles, ntiles, H, src, dst);
     return hipGetLastError();
 }
 

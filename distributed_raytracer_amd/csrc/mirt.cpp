@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1173,15 +1174,18 @@ uint32_t deal_skew(uint32_t world) {
     return s;
 }
 
-void plan_rank_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t world, uint32_t rank, std::vector<mirt_tile>& out) {
+// tile_h == 0: full-height column strips (contiguous in the column-major framebuffer).
+void plan_rank_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                     std::vector<mirt_tile>& out) {
     out.clear();
+    const uint32_t th = tile_h ? tile_h : H;
     const uint32_t cols = (W + tile - 1) / tile;
     const uint32_t s = deal_skew(world);
     uint64_t k = 0;
-    for (uint32_t y = 0; y < H; y += tile)
+    for (uint32_t y = 0; y < H; y += th)
         for (uint32_t x = 0; x < W; x += tile, ++k)
             if (world <= 1 || ((k % cols) + (uint64_t)s * (k / cols)) % world == rank)
-                out.push_back(mirt_tile{x, y, std::min(tile, W - x), std::min(tile, H - y)});
+                out.push_back(mirt_tile{x, y, std::min(tile, W - x), std::min(th, H - y)});
 }
 
 uint64_t tiles_pixels(const std::vector<mirt_tile>& t) {
@@ -1218,15 +1222,16 @@ struct mirt_group {
     // stream, so no slot pool, event query or host wait is on the per-frame path
     std::vector<std::unique_ptr<Slot>> slots;
     uint64_t k = 0;                     // frames enqueued
+    int plan_world = 1;                 // ranks of the tile deal (== world except in a rehearsal)
 };
 
 extern "C" {
 
-int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t world, uint32_t rank, mirt_tile* out,
-                    uint32_t cap) {
+int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                    mirt_tile* out, uint32_t cap) {
     if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
     std::vector<mirt_tile> t;
-    plan_rank_tiles(W, H, tile, world, rank, t);
+    plan_rank_tiles(W, H, tile, tile_h, world, rank, t);
     if (out) {
         if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
         memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
@@ -1266,7 +1271,7 @@ void mirt_group_destroy(mirt_group* g) {
 }
 
 int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world, uint32_t W, uint32_t H,
-                      uint32_t tile, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
+                      uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
     if (!c || !out) return fail(MIRT_E_INVALID, "NULL context or out");
     *out = nullptr;
     if (world < 1 || rank < 0 || rank >= world) return fail(MIRT_E_INVALID, "bad rank / world");
@@ -1285,11 +1290,17 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->H = H;
     g->F = inflight;
     g->tiled = tile > 0;
+    // MIRT_GROUP_REHEARSE=N (diagnostic, world == 1 only): trace rank 0's share of an N-way
+    // deal and unpack all N shares' regions (the others hold stale words), i.e. the root's
+    // per-frame work at N GPUs without the RCCL transfers (tools/native_host_probe.py)
+    const char* reh = getenv("MIRT_GROUP_REHEARSE");
+    const int plan_world = (world == 1 && g->tiled && reh && atoi(reh) > 1) ? atoi(reh) : world;
+    g->plan_world = plan_world;
     if (g->tiled) {
-        plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)rank, g->mine);
-        for (int r = 0; r < world; ++r) {
+        plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)rank, g->mine);
+        for (int r = 0; r < plan_world; ++r) {
             std::vector<mirt_tile> t;
-            plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)r, t);
+            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t);
             g->cap = std::max(g->cap, tiles_pixels(t));
         }
         if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
@@ -1319,11 +1330,11 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
         if (is_root) {
             g->gathered.assign(inflight, nullptr);
             for (uint32_t j = 0; j < inflight; ++j)
-                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)world * g->cap * 4));
+                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->cap * 4));
             std::vector<TileDesc> td;
-            for (int r = 0; r < world; ++r) {
+            for (int r = 0; r < plan_world; ++r) {
                 std::vector<mirt_tile> t;
-                plan_rank_tiles(W, H, tile, (uint32_t)world, (uint32_t)r, t);
+                plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t);
                 uint64_t o = (uint64_t)r * g->cap;
                 for (const mirt_tile& x : t) {
                     td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, {0, 0}});
@@ -1398,7 +1409,7 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
         if (is_root) {
             OutPlanes src{};
             src.rgbv = g->gathered[j];
-            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, (uint64_t)g->world * g->cap, g->H, src, g->fb[j], s));
+            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, (uint64_t)g->plan_world * g->cap, g->H, src, g->fb[j], s));
         }
     }
     HIP_TRY(hipEventRecord(g->ev_done[j], s));

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -25,14 +26,17 @@ from . import _lib as L
 TileT = Tuple[int, int, int, int]
 
 
-def plan_tiles(W: int, H: int, tile: int = 64) -> List[TileT]:
-    """Raster-order tiles (x, y, w, h) covering W x H; edge tiles are clipped."""
-    if W <= 0 or H <= 0 or tile <= 0:
+def plan_tiles(W: int, H: int, tile: int = 64, tile_h: Optional[int] = None) -> List[TileT]:
+    """Raster-order tiles (x, y, w, h) covering W x H, tile wide and tile_h high (None: square;
+    0: full-height column strips, contiguous in the column-major framebuffer); edge tiles
+    are clipped."""
+    th = tile if tile_h is None else (tile_h or H)
+    if W <= 0 or H <= 0 or tile <= 0 or th <= 0:
         raise ValueError("W, H and tile must be positive")
     out = []
-    for y in range(0, H, tile):
+    for y in range(0, H, th):
         for x in range(0, W, tile):
-            out.append((x, y, min(tile, W - x), min(tile, H - y)))
+            out.append((x, y, min(tile, W - x), min(th, H - y)))
     return out
 
 
@@ -212,7 +216,7 @@ class FrameSharder:
     """
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: int = 64, root: int = 0,
-                 with_rgb: bool = False, group=None, inflight: int = 1):
+                 with_rgb: bool = False, group=None, inflight: int = 1, tile_h: Optional[int] = None):
         import torch
         self.ctx, self.W, self.H = ctx, W, H
         self.rank, self.world, self.root, self.group = rank, world, root, group
@@ -227,7 +231,7 @@ class FrameSharder:
         if world == 1:
             self.tiles_all = [(0, 0, W, H)]
         else:
-            self.tiles_all = plan_tiles(W, H, tile)
+            self.tiles_all = plan_tiles(W, H, tile, tile_h)
         self.mine = assign(self.tiles_all, world, rank)
         self._mine_c = _tiles_c(self.mine)
         self.cap = packed_capacity(self.tiles_all, world)
@@ -365,12 +369,13 @@ class FrameSharder:
         return self.bufs[(self._k - 1) % self._nb] if self.world > 1 else None
 
 
-def plan_rank_tiles_native(W: int, H: int, tile: int, world: int, rank: int) -> List[TileT]:
+def plan_rank_tiles_native(W: int, H: int, tile: int, world: int, rank: int, tile_h: Optional[int] = None) -> List[TileT]:
     """The C++ tile deal of mirt_group (mirt_plan_tiles); equals assign(plan_tiles(...))."""
-    n = L.lib().mirt_plan_tiles(W, H, tile, world, rank, None, 0)
+    th = tile if tile_h is None else tile_h
+    n = L.lib().mirt_plan_tiles(W, H, tile, th, world, rank, None, 0)
     L.check(min(n, 0))
     arr = (L.Tile * max(n, 1))()
-    L.check(min(L.lib().mirt_plan_tiles(W, H, tile, world, rank, C.cast(arr, C.c_void_p), n), 0))
+    L.check(min(L.lib().mirt_plan_tiles(W, H, tile, th, world, rank, C.cast(arr, C.c_void_p), n), 0))
     return [(t.x, t.y, t.w, t.h) for t in arr[:n]]
 
 
@@ -386,18 +391,22 @@ class NativeFrameGroup:
     Frames in flight: frame k on the library's stream k % F, framebuffer frames[k % F]
     (rank 0 only), every stream on a hardware queue of its own."""
 
-    def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 32,
-                 inflight: int = 4, group=None, with_rgb: bool = False):
+    def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 8,
+                 inflight: int = 4, group=None, with_rgb: bool = False, tile_h: Optional[int] = 0):
         import torch
         self.ctx, self.W, self.H, self.rank, self.world = ctx, W, H, rank, world
         self.F = max(1, int(inflight))
         self.device = torch.device("cuda", ctx.device)
-        tile = (tile or 0) if world == 1 else int(tile or 32)
-        self.tiles_all = [(0, 0, W, H)] if tile == 0 else plan_tiles(W, H, tile)
-        self.mine = [(0, 0, W, H)] if tile == 0 else plan_rank_tiles_native(W, H, tile, world, rank)
+        tile = (tile or 0) if world == 1 else int(tile or 8)
+        th = tile if tile_h is None else int(tile_h)  # 0: full-height strips
+        self.tiles_all = [(0, 0, W, H)] if tile == 0 else plan_tiles(W, H, tile, th)
+        self.mine = [(0, 0, W, H)] if tile == 0 else plan_rank_tiles_native(W, H, tile, world, rank, th)
         if self.F > 1:
+            # frames in flight share the chip: at most wg_factor * CUs / F workgroups per frame
+            # (2 per CU can be resident; factor 4 = twice what fits)
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-            ctx.set_grid(32, max(1, (4 * cus) // self.F) if self.F > 2 else 0)
+            wg_factor = float(os.environ.get("MIRT_WG_FACTOR", "4"))
+            ctx.set_grid(int(os.environ.get("MIRT_MIN_BLOCKS", "32")), max(1, int(wg_factor * cus / self.F)))
         uid = (C.c_uint8 * 128)()
         if world > 1:
             import torch.distributed as dist
@@ -411,7 +420,7 @@ class NativeFrameGroup:
         fbs = (L.Outputs * self.F)(*[p.outputs() for p in self.frames]) if self.frames else None
         self._h = C.c_void_p()
         L.check(L.lib().mirt_group_create(ctx.handle, C.cast(uid, C.c_void_p) if world > 1 else None, rank, world,
-                                          W, H, tile, self.F, C.cast(fbs, C.c_void_p) if fbs else None,
+                                          W, H, tile, th if tile else 0, self.F, C.cast(fbs, C.c_void_p) if fbs else None,
                                           C.byref(self._h)))
         self._k = 0
         self._idx = C.c_uint64()

@@ -273,8 +273,9 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 
 /*
  * Multi-GPU frames (one process per GPU of a box; SURVEY.md §8(b) mirt_trace_frame).  The
- * screen is cut into tile x tile tiles dealt to the ranks (column c of tile row r goes to
- * rank (c + s r) % world, s the smallest integer >= sqrt(world) coprime with world); each
+ * screen is cut into tile x tile_h tiles (tile_h == 0: full-height column strips, which are
+ * contiguous in the column-major framebuffer) dealt to the ranks (column c of tile row r
+ * goes to rank (c + s r) % world, s the smallest integer >= sqrt(world) coprime with world); each
  * rank traces its tiles into a packed rgbv plane, RCCL (send/recv in one group, on a stream
  * of its own, frames in issue order) gathers the planes to rank 0, and rank 0 unpacks them
  * into the frame's framebuffer.  `inflight` frames overlap, frame k on stream k % inflight
@@ -290,12 +291,12 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 typedef struct mirt_group mirt_group;
 int mirt_group_unique_id(uint8_t *id);
 int mirt_group_create(mirt_ctx *ctx, const uint8_t *unique_id, int rank, int world, uint32_t W, uint32_t H,
-                      uint32_t tile, uint32_t inflight, const mirt_outputs *fbs, mirt_group **out);
+                      uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs *fbs, mirt_group **out);
 int mirt_trace_frame(mirt_group *group, const mirt_frame *frame, uint64_t *index);
 int mirt_group_wait(mirt_group *group, void *stream);
 void mirt_group_destroy(mirt_group *group);
-int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t world, uint32_t rank, mirt_tile *out,
-                    uint32_t cap);
+int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                    mirt_tile *out, uint32_t cap);
 
 #ifdef __cplusplus
 }

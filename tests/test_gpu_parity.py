@@ -483,11 +483,12 @@ def test_octant_child_test_changes_nothing(ctx, env):
         ctx.set_options(0)
 
 
-@pytest.mark.parametrize("tile,inflight", [(None, 4), (32, 3), (48, 1)])
-def test_native_frame_group_matches_draw(ctx, env, tile, inflight):
+@pytest.mark.parametrize("tile,tile_h,inflight", [(None, 0, 4), (32, 32, 3), (8, 0, 2), (48, 0, 1)])
+def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight):
     """mirt_trace_frame (the native multi-GPU frame driver) on one GPU: the whole screen
-    (tile=None) or the tiled path rehearsed with world = 1 (packed rgbv tiles, the unpack
-    table with per-rank offsets), frames in flight with alternating cameras; every
+    (tile=None) or the tiled path rehearsed with world = 1 (packed rgbv tiles or
+    full-height strips, the unpack table with per-rank offsets), frames in flight with
+    alternating cameras; every
     framebuffer equals its camera's frame drawn alone."""
     import torch
     import distributed_raytracer_amd as rt
@@ -500,7 +501,7 @@ def test_native_frame_group_matches_draw(ctx, env, tile, inflight):
     frames = [m.to_frame() for m in muts]
     refs = [rt.draw(env, W, H, m) for m in muts]
     try:
-        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight)
+        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight, tile_h=tile_h)
         order = [0, 1, 1, 0, 1, 0, 0, 1]
         for q in order:
             g.render(frames[q])

@@ -206,8 +206,9 @@ def test_interleaved_tiles_balance_better_than_bisection():
 def test_native_tile_deal_equals_python():
     """mirt_plan_tiles (the C++ deal of mirt_group) == assign(plan_tiles(...))."""
     from distributed_raytracer_amd.framebuffer import assign, plan_rank_tiles_native, plan_tiles
-    for W, H, t in ((1920, 1080, 32), (1920, 1080, 64), (320, 240, 48), (7, 5, 3)):
-        tiles = plan_tiles(W, H, t)
+    for W, H, t, th in ((1920, 1080, 32, None), (1920, 1080, 64, None), (320, 240, 48, None), (7, 5, 3, None),
+                        (1920, 1080, 8, 0), (320, 240, 16, 0), (1920, 1080, 32, 16)):
+        tiles = plan_tiles(W, H, t, th)
         for world in (1, 2, 3, 4, 6, 8):
             for r in range(world):
-                assert plan_rank_tiles_native(W, H, t, world, r) == assign(tiles, world, r), (W, H, t, world, r)
+                assert plan_rank_tiles_native(W, H, t, world, r, th) == assign(tiles, world, r), (W, H, t, th, world, r)
