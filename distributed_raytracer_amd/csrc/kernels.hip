@@ -1029,6 +1029,19 @@ __device__ __forceinline__ uint32_t block_frustum(const FrustumArgs& fr, const f
                       fmaxf(t0, t1) >= r.z;
     return (uint32_t)__ballot(meet);
 }
+// The same predicate evaluated by one thread over all 8 rectangles: true iff
+// block_frustum(...) != 0 for that block.
+__device__ __forceinline__ bool block_may_meet(const FrustumArgs& fr, const float4* __restrict__ rects, uint32_t px,
+                                               uint32_t py, uint32_t vw, uint32_t vh) {
+    const float s0 = (float)(fr.sB - fr.sA * (double)px), s1 = (float)(fr.sB - fr.sA * (double)(px + vw - 1));
+    const float t0 = (float)(fr.tB - fr.tA * (double)py), t1 = (float)(fr.tB - fr.tA * (double)(py + vh - 1));
+    bool meet = false;
+    for (int c = 0; c < 8; ++c) {
+        const float4 r = rects[c];
+        meet |= fminf(s0, s1) <= r.y && fmaxf(s0, s1) >= r.x && fminf(t0, t1) <= r.w && fmaxf(t0, t1) >= r.z;
+    }
+    return meet;
+}
 
 // ---------------------------------------------------------------- primary block
 // One 8x8 pixel block: raygen (tracer.go:15-22, :86), nearest hit, outputs of misses,
@@ -1046,7 +1059,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
                                               bool frustum = false, const float4* __restrict__ frect = nullptr,
-                                              const LocalChunks* lc = nullptr) {
+                                              const LocalChunks* lc = nullptr, uint32_t classified = 0) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1054,7 +1067,8 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
     const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
     const bool active = lx < vw && ly < vh;
-    if (frustum && block_frustum(wa.fr, frect, px, py, vw, vh) == 0) {  // whole-block pre-test
+    // classified (k_trace staging, block_may_meet): 1 culled, 2 may meet, 0 test here
+    if (frustum && (classified == 1 || (classified == 0 && block_frustum(wa.fr, frect, px, py, vw, vh) == 0))) {
         ++ws.nodes;
         if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
             const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
@@ -1366,8 +1380,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     __shared__ cnt_t red[kWG / 64][4];
     __shared__ float4 frect[8];
     __shared__ uint32_t bq[kBlkQ][3];
+    __shared__ uint8_t bq_cull[kBlkQ];  // 1: the block frustum pre-test culled it at staging
     __shared__ uint32_t ready[kBlkQ];
-    __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item;
+    __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     WaveClock clock;
     uint32_t taken = 0;
@@ -1395,14 +1410,32 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
         return (uint32_t)__builtin_amdgcn_readfirstlane(t);
     };
     ItemClock ic;
+    // Blocks the frustum pre-test cannot cull go to the front of the workgroup's queue:
+    // their primary trace and shadow items are the long single-wave chains, and starting
+    // them first keeps the cheap culled blocks as filler instead of delaying a chain to the
+    // end of the workgroup's life (the frame's tail; with a small tile list, its latency).
+    const bool classify = use_frustum && !(fa.flags & MIRT_OPT_STATIC_SCHEDULE);
+    if (classify) __syncthreads();  // the frustum rectangles are staged
     for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
         const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
+        if (threadIdx.x == 0) {
+            s_front = 0;
+            s_back = nc;
+        }
+        if (classify) __syncthreads();
         for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
             const uint32_t b = blockIdx.x + (c0 + t) * G;
             const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(b % kQShards) * wa.per_shard + b / kQShards];
-            bq[t][0] = v[0];
-            bq[t][1] = v[1];
-            bq[t][2] = v[2];
+            uint32_t slot = t;
+            bool culled = false;
+            if (classify) {
+                culled = !block_may_meet(wa.fr, frect, v[1] & 0xffffu, v[1] >> 16, (v[2] >> 16) & 0xffu, v[2] >> 24);
+                slot = culled ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
+            }
+            bq[slot][0] = v[0];
+            bq[slot][1] = v[1];
+            bq[slot][2] = v[2];
+            bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
             ready[t] = 0;
         }
         if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
@@ -1438,7 +1471,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                     const WaveStats before = wp;
                     const uint64_t ph0 = pc.acc[0], ph1 = pc.acc[1];
                     primary_block<false, PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, bd, 0, wp, pc, use_frustum,
-                                                           frect, &lc);
+                                                           frect, &lc, __builtin_amdgcn_readfirstlane(bq_cull[t]));
                     ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
                               (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
                     lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated
