@@ -1687,17 +1687,22 @@ __device__ __forceinline__ void unpack_pixel(const OutPlanes& src, const OutPlan
         }
     }
 }
+// Grid: x runs over tiles, y over 1024-pixel chunks of a tile (a chunk per workgroup, a
+// 4-pixel group per thread), so a frame of few large tiles (full-height strips) still
+// spreads over thousands of short workgroups instead of a few long per-tile loops.
+constexpr uint32_t kUnpackChunk = 1024;
 __global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t H,
                                                 OutPlanes src, OutPlanes dst) {
     const bool only_rgbv = src.rgbv && !src.rgb && !src.rgb8 && !src.valid && !src.face && !src.object;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t tt = __builtin_amdgcn_readfirstlane(t);
         const TileDesc td = tiles[tt];
-        const uint64_t n = (uint64_t)td.w * td.h;
-        if (only_rgbv && (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0 && (td.out_off & 3u) == 0) {
-            for (uint64_t p4 = threadIdx.x; p4 < n / 4; p4 += blockDim.x) {
-                const uint64_t local = p4 * 4;
-                const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
+        const uint32_t n = td.w * td.h;  // w, h <= 65535
+        for (uint32_t c0 = blockIdx.y * kUnpackChunk; c0 < n; c0 += gridDim.y * kUnpackChunk) {
+            if (only_rgbv && (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0 && (td.out_off & 3u) == 0) {
+                const uint32_t local = c0 + threadIdx.x * 4;
+                if (local >= n) continue;
+                const uint32_t lx = local / td.h, ly = local - lx * td.h;
                 const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);  // multiple of 4
                 const uint4 v = *(const uint4*)(src.rgbv + td.out_off + local);
                 if (dst.rgbv) *(uint4*)(dst.rgbv + q) = v;
@@ -1709,11 +1714,12 @@ __global__ __launch_bounds__(256) void k_unpack(const TileDesc* __restrict__ til
                     o[1] = ((v.y >> 8) & 0xffffu) | (v.z << 16);
                     o[2] = ((v.z >> 16) & 0xffu) | ((v.w & 0xffffffu) << 8);
                 }
-            }
-        } else {
-            for (uint64_t local = threadIdx.x; local < n; local += blockDim.x) {
-                const uint32_t lx = (uint32_t)(local / td.h), ly = (uint32_t)(local - (uint64_t)lx * td.h);
-                unpack_pixel(src, dst, td.out_off + local, (uint64_t)(td.x + lx) * H + (td.y + ly));
+            } else {
+                const uint32_t end = min(n, c0 + kUnpackChunk);
+                for (uint32_t local = c0 + threadIdx.x; local < end; local += blockDim.x) {
+                    const uint32_t lx = local / td.h, ly = local - lx * td.h;
+                    unpack_pixel(src, dst, td.out_off + local, (uint64_t)(td.x + lx) * H + (td.y + ly));
+                }
             }
         }
     }
@@ -1800,11 +1806,12 @@ hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes
     return hipGetLastError();
 }
 
-hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
+hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s) {
-    (void)npix;
-    const int grid = (int)(ntiles < 8192u ? (ntiles ? ntiles : 1u) : 8192u);
-    hipLaunchKernelGGL(k_unpack, dim3(grid), dim3(256), 0, s, tiles, ntiles, H, src, dst);
+    const uint32_t gx = ntiles < 8192u ? (ntiles ? ntiles : 1u) : 8192u;
+    const uint64_t chunks = (max_tile_px + kUnpackChunk - 1) / kUnpackChunk;
+    const uint32_t gy = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunks, std::max<uint64_t>(1, 16384 / gx)));
+    hipLaunchKernelGGL(k_unpack, dim3(gx, gy), dim3(256), 0, s, tiles, ntiles, H, src, dst);
     return hipGetLastError();
 }
 

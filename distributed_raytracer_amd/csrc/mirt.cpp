@@ -62,6 +62,7 @@ struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool pending = false;
+    bool dedicated = false;  // a frame group's slot: ordered by its stream, no done event needed
     HitRec* hits = nullptr;
     size_t hits_cap = 0;
     uint32_t* litw = nullptr;
@@ -566,8 +567,10 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         std::lock_guard<std::mutex> g(c->mu);
         c->prof_pending.push_back(pr);
     }
-    HIP_TRY(hipEventRecord(sl->done, s));
-    sl->pending = true;
+    if (!sl->dedicated) {
+        HIP_TRY(hipEventRecord(sl->done, s));
+        sl->pending = true;
+    }
     *pixels_out = pixels;
     *tris_out = tris;
     return MIRT_OK;
@@ -883,7 +886,7 @@ int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, con
     const size_t cap_before = sl->tiles_cap;
     if ((r = tiles_grow(sl, n)) != MIRT_OK) return r;
     if (sl->tiles_cap != cap_before) sl->unpack_key.clear();  // reallocated: the device copy is gone
-    uint64_t pixels = 0, span = 0;
+    uint64_t pixels = 0, span = 0, max_px = 0;
     std::vector<TileDesc> td(n);
     for (uint32_t t = 0; t < n; ++t) {
         if ((uint64_t)tiles[t].x + tiles[t].w > W || (uint64_t)tiles[t].y + tiles[t].h > H || !tiles[t].w ||
@@ -894,6 +897,7 @@ int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, con
         td[t] = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, off, {0, 0}};
         pixels += (uint64_t)tiles[t].w * tiles[t].h;
         span = off + (uint64_t)tiles[t].w * tiles[t].h;
+        max_px = std::max<uint64_t>(max_px, (uint64_t)tiles[t].w * tiles[t].h);
     }
     if (sl->unpack_key_H != H || sl->unpack_key.size() != n ||
         memcmp(sl->unpack_key.data(), td.data(), sizeof(TileDesc) * n) != 0) {
@@ -904,7 +908,7 @@ int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, con
     }
     OutPlanes src{packed->rgb, packed->rgb8, packed->valid, packed->face, packed->object, packed->rgbv};
     OutPlanes dst{fb->rgb, fb->rgb8, fb->valid, fb->face, fb->object, fb->rgbv};
-    HIP_TRY(launch_unpack(sl->d_tiles, n, span, H, src, dst, s));
+    HIP_TRY(launch_unpack(sl->d_tiles, n, max_px, H, src, dst, s));
     HIP_TRY(hipEventRecord(sl->done, s));
     sl->pending = true;
     return MIRT_OK;
@@ -1218,6 +1222,7 @@ struct mirt_group {
     std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
     TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
     uint32_t n_unpack = 0;
+    uint64_t max_tile_px = 0;           // root: largest tile (unpack grid)
     // one workspace per frame slot: frame k reuses slot k % F after frame k - F on the same
     // stream, so no slot pool, event query or host wait is on the per-frame path
     std::vector<std::unique_ptr<Slot>> slots;
@@ -1310,6 +1315,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     }
     for (uint32_t j = 0; j < inflight; ++j) {
         g->slots.emplace_back(new Slot());
+        g->slots.back()->dedicated = true;
         int r = slot_init(g->slots.back().get());
         if (r != MIRT_OK) return r;
     }
@@ -1339,6 +1345,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
                 for (const mirt_tile& x : t) {
                     td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, {0, 0}});
                     o += (uint64_t)x.w * x.h;
+                    g->max_tile_px = std::max<uint64_t>(g->max_tile_px, (uint64_t)x.w * x.h);
                 }
             }
             g->n_unpack = (uint32_t)td.size();
@@ -1369,8 +1376,9 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     const bool is_root = g->rank == g->root;
     // back-pressure: the host runs at most F frames ahead (frame k - F must have finished)
     if (g->k >= g->F) HIP_TRY(hipEventSynchronize(g->ev_done[j]));
-    // frame k - F used this slot's buffers: its gather must be done with them
-    if (g->tiled && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
+    // frame k - F used this slot's buffers: its send must be done with them (the root's
+    // stream already waited for its gather before that frame's unpack; world == 1 has no gather)
+    if (g->tiled && g->world > 1 && !is_root && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
     OutPlanes out{};
     if (!g->tiled) {
         out = g->fb[j];
@@ -1403,13 +1411,11 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
             RCCL_TRY(R.group_end());
             HIP_TRY(hipEventRecord(g->ev_gathered[j], g->comm_stream));
             if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
-        } else {
-            HIP_TRY(hipEventRecord(g->ev_gathered[j], s));
         }
         if (is_root) {
             OutPlanes src{};
             src.rgbv = g->gathered[j];
-            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, (uint64_t)g->plan_world * g->cap, g->H, src, g->fb[j], s));
+            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, src, g->fb[j], s));
         }
     }
     HIP_TRY(hipEventRecord(g->ev_done[j], s));

@@ -231,7 +231,7 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
-hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t npix, uint32_t H, const OutPlanes& src,
+hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);
 
 }  // namespace mirt

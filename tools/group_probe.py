@@ -35,13 +35,19 @@ def main():
     g.flush()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    calls = []
     for _ in range(a.frames):
+        c0 = time.perf_counter()
         g.render(fr)
+        calls.append(time.perf_counter() - c0)
+    t1 = time.perf_counter()
     g.flush()
     torch.cuda.synchronize()
     print(json.dumps({"tile": a.tile, "inflight": a.inflight, "view": a.view,
                       "rehearse": os.environ.get("MIRT_GROUP_REHEARSE", "1"),
-                      "frame_interval_us": round((time.perf_counter() - t0) / a.frames * 1e6, 1)}))
+                      "frame_interval_us": round((time.perf_counter() - t0) / a.frames * 1e6, 1),
+                      "host_enqueue_us": round((t1 - t0) / a.frames * 1e6, 1),
+                      "call_us_p10_50_90": [round(float(np.percentile(calls, q)) * 1e6, 1) for q in (10, 50, 90)]}))
     g.close()
 
 
