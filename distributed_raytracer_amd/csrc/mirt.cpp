@@ -58,6 +58,24 @@ struct MeshDev {
 };
 
 // Device workspace of one in-flight call.
+// -DMIRT_HOST_TIMERS (diagnostic build): host time per phase of mirt_trace_frame,
+// printed when the group is destroyed (tools/group_probe.py with MIRT_LIB).
+#ifdef MIRT_HOST_TIMERS
+#include <chrono>
+static double g_ht[8];
+static std::chrono::steady_clock::time_point g_ht_t;
+#define HT_START() (g_ht_t = std::chrono::steady_clock::now())
+#define HT(i)                                                                                   \
+    do {                                                                                        \
+        auto n_ = std::chrono::steady_clock::now();                                             \
+        g_ht[i] += std::chrono::duration<double, std::micro>(n_ - g_ht_t).count();             \
+        g_ht_t = n_;                                                                            \
+    } while (0)
+#else
+#define HT_START() ((void)0)
+#define HT(i) ((void)0)
+#endif
+
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -542,7 +560,9 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
     if (!(c->flags & MIRT_OPT_SPLIT_KERNELS) && !wa.bounces) {
         // one launch per frame (k_trace); its time lands in the primary slot of the profile
+        HT(2);
         HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
+        HT(3);
         if (prof) {
             HIP_TRY(hipEventRecord(pr.ev[1], s));
             HIP_TRY(hipEventRecord(pr.ev[2], s));
@@ -1255,6 +1275,10 @@ int mirt_group_unique_id(uint8_t* id) {
 
 void mirt_group_destroy(mirt_group* g) {
     if (!g) return;
+#ifdef MIRT_HOST_TIMERS
+    fprintf(stderr, "host_timers_us_per_frame sync %.2f check %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
+            g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k);
+#endif
     (void)hipSetDevice(g->c->device);
     for (hipStream_t s : g->streams)
         if (s) (void)hipStreamSynchronize(s);
@@ -1370,12 +1394,14 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
 int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
     mirt_ctx* c = g->c;
+    HT_START();
     HIP_TRY(hipSetDevice(c->device));
     const uint32_t j = (uint32_t)(g->k % g->F);
     hipStream_t s = g->streams[j];
     const bool is_root = g->rank == g->root;
     // back-pressure: the host runs at most F frames ahead (frame k - F must have finished)
     if (g->k >= g->F) HIP_TRY(hipEventSynchronize(g->ev_done[j]));
+    HT(0);
     // frame k - F used this slot's buffers: its send must be done with them (the root's
     // stream already waited for its gather before that frame's unpack; world == 1 has no gather)
     if (g->tiled && g->world > 1 && !is_root && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
@@ -1387,6 +1413,7 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     }
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
+    HT(1);
     uint64_t pixels = 0, tris = 0;
     if ((r = enqueue_trace(c, g->slots[j].get(), f, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), out, s,
                            nullptr, &pixels, &tris)) != MIRT_OK) {
@@ -1412,13 +1439,16 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
             HIP_TRY(hipEventRecord(g->ev_gathered[j], g->comm_stream));
             if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
         }
+        HT(4);
         if (is_root) {
             OutPlanes src{};
             src.rgbv = g->gathered[j];
             HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, src, g->fb[j], s));
         }
     }
+    HT(5);
     HIP_TRY(hipEventRecord(g->ev_done[j], s));
+    HT(6);
     if (index) *index = g->k;
     ++g->k;
     return MIRT_OK;
