@@ -53,7 +53,13 @@ def parse():
     ap.add_argument("--scene", default=SCENE)
     ap.add_argument("--bounces", type=int, default=0,
                     help="configs[4] reflection EXTENSION: bounces per primary hit (0 = the reference)")
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("MIRT_INFLIGHT", "4")),
+    # defaults measured on one MI355X (tools/batch_sweep.sh): the whole 1080p frame runs
+    # best as 8 in flight, 2 per launch; a rank's 1/N share needs more frames per launch
+    # (each workgroup then owns enough blocks to hide its heaviest block's chain)
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIRT_BATCH", "4" if multi else "2")),
+                    help="frames per k_trace launch (native sharder; 1..min(8, inflight))")
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "8")),
                     help="frames in flight (one stream and one set of buffers each; frame k+1's kernel "
                          "starts while frame k's last workgroups finish)")
     ap.add_argument("--grid", default="",
@@ -174,12 +180,13 @@ def main():
     if sharder == "native":
         try:
             sh = NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
-                                  tile_h=a.tile_h)
+                                  tile_h=a.tile_h, batch=a.batch)
         except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
             print(f"native frame group unavailable ({e}); using the torch.distributed sharder", file=sys.stderr)
             sharder = f"torch (native failed: {e})"
     if sh is None:
-        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=a.inflight, tile_h=a.tile_h)
+        # the torch.distributed path was tuned at 4 in flight (one frame per launch)
+        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=min(a.inflight, 4), tile_h=a.tile_h)
     if a.grid:
         ctx.set_grid(*(int(x) for x in a.grid.split(",")))
     dev = torch.device("cuda", local)
@@ -231,7 +238,7 @@ def main():
     prof = ctx.profile_read()
 
     elapsed = t1 - t0
-    pl = max(prof["launches"], 1)
+    pl = max(prof["frames"], 1)  # per-frame device counters (a launch may trace several frames)
     counts = torch.tensor([elapsed, latency, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
                            prof["reflection_rays"] / pl], dtype=torch.float64,
                           device=dev if backend == "nccl" else "cpu")
@@ -286,13 +293,14 @@ def main():
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
             "frames_in_flight": sh.F,
+            "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,
             "frame_latency_ms": round(latency * 1e3, 4),
             "primary_mrays_s": round(primary / (ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
             "hits_per_frame": int(hits),
-            "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / launches),
-            "bvh_visits_per_frame": {k: int(prof[k] / launches) for k in (
+            "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / pl),
+            "bvh_visits_per_frame": {k: int(prof[k] / pl) for k in (
                 "primary_node_visits", "primary_leaf_visits", "shadow_node_visits", "shadow_leaf_visits")},
             "ms_kernels": {("frame_kernel" if one else "primary"): round(prim_ms, 4),
                            "shadow": round(prof["shadow_ms_sum"] / launches, 4),

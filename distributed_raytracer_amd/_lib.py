@@ -79,7 +79,8 @@ class Profile(C.Structure):
                 ("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("hits", C.c_uint64),
                 ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64),
-                ("stack_overflows", C.c_uint64), ("reflection_rays", C.c_uint64), ("reflect_ms_sum", C.c_double)]
+                ("stack_overflows", C.c_uint64), ("reflection_rays", C.c_uint64), ("reflect_ms_sum", C.c_double),
+                ("frames", C.c_uint64)]
 
 
 class MeshView(C.Structure):
@@ -126,6 +127,7 @@ SIGNATURES = {
     "mirt_group_create": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_uint32, _P, C.POINTER(_P)]),
     "mirt_trace_frame": (C.c_int, [_P, C.POINTER(Frame), C.POINTER(C.c_uint64)]),
+    "mirt_group_set_batch": (C.c_int, [_P, C.c_uint32]),
     "mirt_group_wait": (C.c_int, [_P, _P]),
     "mirt_group_destroy": (None, [_P]),
     "mirt_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,

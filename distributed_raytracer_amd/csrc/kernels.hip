@@ -1053,6 +1053,8 @@ struct LocalChunks {
     uint32_t* count;
     uint32_t* ready;
     size_t base;
+    uint8_t* frame_of;  // per chunk: its frame within the launch (k_trace)
+    uint32_t frame;
 };
 template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
@@ -1142,7 +1144,10 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
             // wave of this CU) before its ready flag is raised in LDS
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) __hip_atomic_store(&lc->ready[base], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0) {
+                lc->frame_of[base] = (uint8_t)lc->frame;  // LDS, in order before the flag
+                __hip_atomic_store(&lc->ready[base], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
     }
     if (active) {
@@ -1373,14 +1378,23 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
 // workgroup shares that L2, so no device-scope coherence is needed).  One mesh staging,
 // no second launch, and the shadow work of early blocks fills the primary tail.  The mesh
 // is staged in absolute coordinates (the shadow rays' origins differ per lane).
+// The launch's frame records, read through the constant address space: the kernel never
+// writes them, so their loads stay scalar and are not repeated after the kernel's stores.
+typedef const __attribute__((address_space(4))) FrameRec ConstFrameRec;
+__device__ __forceinline__ const FrameRec& frame_rec(const WorkArgs& wa, uint32_t f) {
+    return *(const FrameRec*)((ConstFrameRec*)wa.frames + f);
+}
+
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
     __shared__ uint32_t wstk[kWG / 64][(MIRT_PRIMARY_WIDE || MIRT_SHADOW_WIDE) ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
-    __shared__ float4 frect[8];
+    __shared__ float4 frect[kMaxFrames][8];
     __shared__ uint32_t bq[kBlkQ][3];
-    __shared__ uint8_t bq_cull[kBlkQ];  // 1: the block frustum pre-test culled it at staging
+    __shared__ uint8_t bq_cull[kBlkQ];   // 1: the block frustum pre-test culled it at staging
+    __shared__ uint8_t bq_frame[kBlkQ];  // the block's frame within the launch
+    __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
     __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
@@ -1388,8 +1402,12 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     uint32_t taken = 0;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
         for (int i = threadIdx.x; i < kCntN; i += kWG) wa.counters_next[i] = 0;
-    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;
-    if (use_frustum) stage_frustum(frect, wa.fr);
+    const uint32_t NF = wa.nframes, nbf = wa.nblocks_frame;  // the host checks NF <= kMaxFrames
+    const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;  // same for every frame (host)
+    if (use_frustum && threadIdx.x < 8 * NF) {
+        const float* r = wa.frames[threadIdx.x >> 3].fr.rect[threadIdx.x & 7];
+        frect[threadIdx.x >> 3][threadIdx.x & 7] = make_float4(r[0], r[1], r[2], r[3]);
+    }
     if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
     uint32_t* stk = wstk[threadIdx.x >> 6];
     WaveStats wp{0, 0, 0, 0, 0}, wsh{0, 0, 0, 0, 0};
@@ -1414,7 +1432,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     // their primary trace and shadow items are the long single-wave chains, and starting
     // them first keeps the cheap culled blocks as filler instead of delaying a chain to the
     // end of the workgroup's life (the frame's tail; with a small tile list, its latency).
-    const bool classify = use_frustum && !(fa.flags & MIRT_OPT_STATIC_SCHEDULE);
+    const bool classify = use_frustum;
+    const bool partition = classify && !(fa.flags & MIRT_OPT_STATIC_SCHEDULE);
     if (classify) __syncthreads();  // the frustum rectangles are staged
     for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
         const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
@@ -1424,24 +1443,27 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
         }
         if (classify) __syncthreads();
         for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
-            const uint32_t b = blockIdx.x + (c0 + t) * G;
-            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(b % kQShards) * wa.per_shard + b / kQShards];
+            const uint32_t b = blockIdx.x + (c0 + t) * G;  // over every frame's blocks
+            const uint32_t f = b / nbf, bl = b - f * nbf;
+            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(bl % kQShards) * wa.per_shard + bl / kQShards];
             uint32_t slot = t;
             bool culled = false;
             if (classify) {
-                culled = !block_may_meet(wa.fr, frect, v[1] & 0xffffu, v[1] >> 16, (v[2] >> 16) & 0xffu, v[2] >> 24);
-                slot = culled ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
+                culled = !block_may_meet(wa.frames[f].fr, frect[f], v[1] & 0xffffu, v[1] >> 16, (v[2] >> 16) & 0xffu,
+                                         v[2] >> 24);
+                if (partition) slot = culled ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
             }
             bq[slot][0] = v[0];
             bq[slot][1] = v[1];
             bq[slot][2] = v[2];
             bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
+            bq_frame[slot] = (uint8_t)f;
             ready[t] = 0;
         }
         if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
         if (c0 == 0) clock.mark_staged();
         __syncthreads();
-        const LocalChunks lc{&s_chunks, ready, chunk0};
+        LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
         for (;;) {
             // 1. a shadow item of an allocated chunk
@@ -1454,7 +1476,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 ++taken;
                 ic.start();
                 const WaveStats before = wsh;
-                shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l, wsh);
+                const FrameRec& fr = frame_rec(wa, __builtin_amdgcn_readfirstlane(chunk_frame[c]));
+                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
+                                              wsh);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -1470,8 +1494,12 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                     ic.start();
                     const WaveStats before = wp;
                     const uint64_t ph0 = pc.acc[0], ph1 = pc.acc[1];
-                    primary_block<false, PREFILTER, BRUTE>(fa, wa, out, lds, stk, RESIDENT, bd, 0, wp, pc, use_frustum,
-                                                           frect, &lc, __builtin_amdgcn_readfirstlane(bq_cull[t]));
+                    const uint32_t f = __builtin_amdgcn_readfirstlane(bq_frame[t]);
+                    const FrameRec& fr = frame_rec(wa, f);
+                    lc.frame = f;
+                    primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
+                                                           use_frustum, frect[f], &lc,
+                                                           __builtin_amdgcn_readfirstlane(bq_cull[t]));
                     ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
                               (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
                     lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated
@@ -1812,6 +1840,18 @@ hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_ti
     const uint64_t chunks = (max_tile_px + kUnpackChunk - 1) / kUnpackChunk;
     const uint32_t gy = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunks, std::max<uint64_t>(1, 16384 / gx)));
     hipLaunchKernelGGL(k_unpack, dim3(gx, gy), dim3(256), 0, s, tiles, ntiles, H, src, dst);
+    return hipGetLastError();
+}
+
+// Copy a launch's frame records from pinned host memory to the device (one workgroup; a
+// hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there).
+__global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      uint32_t n16) {
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+}
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s) {
+    const uint32_t n16 = (uint32_t)(n * sizeof(FrameRec) / 16);
+    hipLaunchKernelGGL(k_stage_frames, dim3(1), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16);
     return hipGetLastError();
 }
 

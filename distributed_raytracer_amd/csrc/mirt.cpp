@@ -107,6 +107,8 @@ struct Slot {
     // pixelToPoint per column / per row (tracer.go:19-20), cached per (fov, W, H)
     cnt_t* summary = nullptr;     // kStatN totals of the last frame (device)
     cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
+    FrameRec* h_frames = nullptr; // kMaxFrames pinned records of the next k_trace launch
+    FrameRec* d_frames = nullptr; // their device copy
     bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
     uint32_t parity = 0;          // counter set of the next frame (two sets of kCntN)
     // device-side outputs for the host-buffer API
@@ -117,6 +119,7 @@ struct Slot {
 struct ProfRec {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     uint64_t pixels = 0;
+    uint32_t frames = 1;
 };
 
 }  // namespace
@@ -175,6 +178,8 @@ int slot_init(Slot* s) {
     HIP_TRY(hipMalloc((void**)&s->counters, 2 * kCntN * sizeof(cnt_t)));
     HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
     HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
+    HIP_TRY(hipHostMalloc((void**)&s->h_frames, kMaxFrames * sizeof(FrameRec)));
+    HIP_TRY(hipMalloc((void**)&s->d_frames, kMaxFrames * sizeof(FrameRec)));
     HIP_TRY(hipMemset(s->counters, 0, 2 * kCntN * sizeof(cnt_t)));
     return MIRT_OK;
 }
@@ -182,11 +187,13 @@ int slot_init(Slot* s) {
 void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0,
-                    (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf})
+                    (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
+                    (void*)s->d_frames})
         if (p) (void)hipFree(p);
     if (s->h_blocks) (void)hipHostFree(s->h_blocks);
     if (s->h_tiles) (void)hipHostFree(s->h_tiles);
     if (s->h_summary) (void)hipHostFree(s->h_summary);
+    if (s->h_frames) (void)hipHostFree(s->h_frames);
     if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
 }
@@ -466,14 +473,11 @@ int blocks_prepare(Slot* sl, uint32_t W, uint32_t H, const mirt_tile* tiles, uin
     return MIRT_OK;
 }
 
-// Enqueue primary -> shadow -> shade for a tile list on stream s.
-int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
-                  uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel, uint64_t* pixels_out,
-                  uint64_t* tris_out) {
+// Validate a tile list against the screen; its pixel count.
+int check_tiles(uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n, uint64_t& pixels) {
     if (W == 0 || H == 0) return fail(MIRT_E_INVALID, "screen width/height must be > 0");
     if (n == 0 || !tiles) return fail(MIRT_E_INVALID, "empty tile list");
-    uint64_t pixels = 0;
-    int r = MIRT_OK;
+    pixels = 0;
     for (uint32_t t = 0; t < n; ++t) {
         const mirt_tile& tl = tiles[t];
         if (tl.w == 0 || tl.h == 0) return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty");
@@ -483,14 +487,66 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     }
     if (pixels > 0xffffffffull) return fail(MIRT_E_LIMIT, "more than 2^32 pixels in one call");
     if (W > 65535 || H > 65535) return fail(MIRT_E_LIMIT, "screen width/height above 65535");
-    FrameArgs fa;
-    uint64_t tris = 0;
-    fill_args(c, f, W, H, fa, tris);
+    return MIRT_OK;
+}
+
+// One frame's launch record: its arguments, output planes and frustum rectangles.
+void frame_record(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const OutPlanes& out, FrameRec& rec,
+                  uint64_t& tris) {
+    fill_args(c, f, W, H, rec.fa, tris);
+    frustum_args(c, f, rec.fa, rec.fr);
+    rec.out = out;
+}
+
+// Frames whose records can share one k_trace launch (same mesh, objects, lights, options
+// and frustum mode: the kernel takes those from the first record).
+bool frames_batchable(const FrameRec& a, const FrameRec& b) {
+    if (a.fa.n_objects != b.fa.n_objects || a.fa.n_lights != b.fa.n_lights || a.fa.flags != b.fa.flags ||
+        a.fa.W != b.fa.W || a.fa.H != b.fa.H || a.fr.on != b.fr.on)
+        return false;
+    for (uint32_t o = 0; o < a.fa.n_objects; ++o)
+        if (memcmp(&a.fa.obj[o].m, &b.fa.obj[o].m, sizeof(DevMesh)) != 0) return false;
+    return true;
+}
+
+int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel);
+
+// Enqueue primary -> shadow -> shade for a tile list on stream s.
+int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
+                  uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel, uint64_t* pixels_out,
+                  uint64_t* tris_out) {
+    uint64_t pixels = 0, tris = 0;
+    int r = check_tiles(W, H, tiles, n, pixels);
+    if (r != MIRT_OK) return r;
+    frame_record(c, f, W, H, out, sl->h_frames[0], tris);
+    if ((r = launch_frames(c, sl, 1, W, H, tiles, n, f->max_bounces, s, cancel)) != MIRT_OK) return r;
+    *pixels_out = pixels;
+    *tris_out = tris;
+    return MIRT_OK;
+}
+
+// Launch the nf frames staged in sl->h_frames (k_trace: one launch for all of them; the
+// split kernels and reflections take one frame).
+int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel) {
+    int r = MIRT_OK;
+    if (nf == 0 || nf > kMaxFrames) return fail(MIRT_E_INVALID, "1..8 frames per launch");
+    const bool one_launch = !(c->flags & MIRT_OPT_SPLIT_KERNELS) && !bounces;
+    if (nf > 1 && !one_launch) return fail(MIRT_E_INVALID, "several frames per launch need the single-kernel path");
+    const FrameArgs& fa = sl->h_frames[0].fa;
+    const OutPlanes out = sl->h_frames[0].out;
     if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
-    const uint32_t nl = f->n_lights;
+    uint64_t pixels = 0;
+    for (uint32_t t = 0; t < n; ++t) pixels += (uint64_t)tiles[t].w * tiles[t].h;
+    const uint32_t nl = fa.n_lights;
+    const uint64_t total = (uint64_t)sl->nblocks * nf;  // every frame's blocks
+    if (total > 0x7fffffffull) return fail(MIRT_E_LIMIT, "too many 8x8 blocks in one launch");
     WorkArgs wa{};
     wa.blocks = sl->d_blocks;
-    wa.nblocks = sl->nblocks;
+    wa.nblocks = (uint32_t)total;
+    wa.nblocks_frame = sl->nblocks;
+    wa.nframes = nf;
     wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
     // persistent: two 512-thread workgroups per CU
@@ -502,16 +558,15 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     }
     // at least min(blocks, CUs) workgroups: a small tile list (a BulkTrace order, one
     // rank's share) keeps one block per wave rather than queueing heavy blocks on few waves
-    const uint64_t want = std::max<uint64_t>(((uint64_t)sl->nblocks + per_wg - 1) / per_wg,
-                                             std::min<uint64_t>(sl->nblocks, (uint64_t)c->cus));
+    const uint64_t want = std::max<uint64_t>((total + per_wg - 1) / per_wg, std::min<uint64_t>(total, (uint64_t)c->cus));
     const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, max_wg));
     // k_trace: workgroup w's hit region holds one chunk per block it owns
-    wa.wg_cap = (uint32_t)(((uint64_t)sl->nblocks + pgrid - 1) / pgrid * 64);
+    wa.wg_cap = (uint32_t)((total + pgrid - 1) / pgrid * 64);
     const uint64_t hit_slots = std::max<uint64_t>((uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap);
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
-    wa.bounces = f->max_bounces;
+    wa.bounces = bounces;
     if (wa.bounces) {
         if ((r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
         if ((r = dev_grow(sl->ph0, sl->ph0_cap, 3 * hit_slots)) != MIRT_OK) return r;
@@ -524,7 +579,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     wa.counters = sl->counters + (size_t)sl->parity * kCntN;
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
-    frustum_args(c, f, fa, wa.fr);
+    wa.fr = sl->h_frames[0].fr;
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
                      ? 0u
                      : (uint32_t)(kDynPrimary | kDynShadow | kDynReflect);
@@ -558,8 +613,12 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
-    if (!(c->flags & MIRT_OPT_SPLIT_KERNELS) && !wa.bounces) {
-        // one launch per frame (k_trace); its time lands in the primary slot of the profile
+    if (one_launch) {
+        // one launch for the frames (k_trace); its time lands in the primary slot of the profile
+        FrameRec* src = nullptr;
+        HIP_TRY(hipHostGetDevicePointer((void**)&src, sl->h_frames, 0));
+        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
+        wa.frames = sl->d_frames;
         HT(2);
         HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
         HT(3);
@@ -583,7 +642,8 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     sl->dirty = false;
     if (prof) {
         HIP_TRY(hipEventRecord(pr.ev[3], s));
-        pr.pixels = pixels;
+        pr.pixels = pixels * nf;
+        pr.frames = nf;
         std::lock_guard<std::mutex> g(c->mu);
         c->prof_pending.push_back(pr);
     }
@@ -591,8 +651,6 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
         HIP_TRY(hipEventRecord(sl->done, s));
         sl->pending = true;
     }
-    *pixels_out = pixels;
-    *tris_out = tris;
     return MIRT_OK;
 }
 
@@ -1024,6 +1082,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         HIP_TRY(hipEventElapsedTime(&d, r.ev[2], r.ev[3]));
         HIP_TRY(hipEventElapsedTime(&t, r.ev[0], r.ev[3]));
         out->launches++;
+        out->frames += r.frames;
         out->primary_ms_sum += a;
         out->shadow_ms_sum += b;
         out->reflect_ms_sum += d;
@@ -1248,6 +1307,15 @@ struct mirt_group {
     std::vector<std::unique_ptr<Slot>> slots;
     uint64_t k = 0;                     // frames enqueued
     int plan_world = 1;                 // ranks of the tile deal (== world except in a rehearsal)
+    // frames per k_trace launch (mirt_group_set_batch): frames accumulate in the open batch,
+    // which launches when full, when an incompatible frame arrives, or at mirt_group_wait.
+    // Batch b uses batch slot b % FB (its workspace, stream and events), FB = F / B, so the
+    // F framebuffers (frame k: k % F) are never reused before their frame completed.
+    uint32_t B = 1, FB = 1;
+    uint64_t nb = 0;                    // batches launched
+    uint32_t bn = 0;                    // frames in the open batch
+    uint32_t bj[kMaxFrames] = {};       // their frame slots (k % F)
+    uint32_t bbounces = 0;
 };
 
 extern "C" {
@@ -1276,7 +1344,7 @@ int mirt_group_unique_id(uint8_t* id) {
 void mirt_group_destroy(mirt_group* g) {
     if (!g) return;
 #ifdef MIRT_HOST_TIMERS
-    fprintf(stderr, "host_timers_us_per_frame sync %.2f check %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
+    fprintf(stderr, "host_timers_us_per_frame wait %.2f record %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
             g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k);
 #endif
     (void)hipSetDevice(g->c->device);
@@ -1318,6 +1386,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->W = W;
     g->H = H;
     g->F = inflight;
+    g->FB = inflight;  // one frame per launch until mirt_group_set_batch
     g->tiled = tile > 0;
     // MIRT_GROUP_REHEARSE=N (diagnostic, world == 1 only): trace rank 0's share of an N-way
     // deal and unpack all N shares' regions (the others hold stale words), i.e. the root's
@@ -1391,73 +1460,114 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     return MIRT_OK;
 }
 
-int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
-    if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
+// Launch the open batch on its slot's stream: trace, then (tiled) the gather of every frame
+// of the batch as ONE RCCL group and, on the root, one unpack per frame.
+static int group_flush(mirt_group* g) {
+    if (g->bn == 0) return MIRT_OK;
     mirt_ctx* c = g->c;
-    HT_START();
-    HIP_TRY(hipSetDevice(c->device));
-    const uint32_t j = (uint32_t)(g->k % g->F);
-    hipStream_t s = g->streams[j];
+    const uint32_t bs = (uint32_t)(g->nb % g->FB);
+    hipStream_t s = g->streams[bs];
     const bool is_root = g->rank == g->root;
-    // back-pressure: the host runs at most F frames ahead (frame k - F must have finished)
-    if (g->k >= g->F) HIP_TRY(hipEventSynchronize(g->ev_done[j]));
-    HT(0);
-    // frame k - F used this slot's buffers: its send must be done with them (the root's
-    // stream already waited for its gather before that frame's unpack; world == 1 has no gather)
-    if (g->tiled && g->world > 1 && !is_root && g->k >= g->F) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
-    OutPlanes out{};
-    if (!g->tiled) {
-        out = g->fb[j];
-    } else {
-        out.rgbv = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->packed[j];
-    }
-    int r = check_frame(c, f);
-    if (r != MIRT_OK) return r;
-    HT(1);
-    uint64_t pixels = 0, tris = 0;
-    if ((r = enqueue_trace(c, g->slots[j].get(), f, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), out, s,
-                           nullptr, &pixels, &tris)) != MIRT_OK) {
+    const uint32_t n = g->bn;
+    g->bn = 0;
+    // a sender reuses its packed planes only after their previous batch's sends are done (the
+    // root's stream already waited for that gather before its unpacks)
+    if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
+    int r = launch_frames(c, g->slots[bs].get(), n, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), g->bbounces,
+                          s, nullptr);
+    if (r != MIRT_OK) {
         (void)hipStreamSynchronize(s);
         return r;
     }
     if (g->tiled) {
         if (g->world > 1) {
             const Rccl& R = rccl();
-            HIP_TRY(hipEventRecord(g->ev_traced[j], s));
-            HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[j], 0));
+            HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
+            HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
             const size_t bytes = g->cap * 4;
             RCCL_TRY(R.group_start());
-            if (is_root) {
-                for (int q = 0; q < g->world; ++q)
-                    if (q != g->root)
-                        RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, bytes, ncclUint8, q, g->comm,
-                                        g->comm_stream));
-            } else {
-                RCCL_TRY(R.send(g->packed[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t j = g->bj[i];
+                if (is_root) {
+                    for (int q = 0; q < g->world; ++q)
+                        if (q != g->root)
+                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, bytes, ncclUint8, q, g->comm,
+                                            g->comm_stream));
+                } else {
+                    RCCL_TRY(R.send(g->packed[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
+                }
             }
             RCCL_TRY(R.group_end());
-            HIP_TRY(hipEventRecord(g->ev_gathered[j], g->comm_stream));
-            if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[j], 0));
+            HIP_TRY(hipEventRecord(g->ev_gathered[bs], g->comm_stream));
+            if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
         }
         HT(4);
-        if (is_root) {
-            OutPlanes src{};
-            src.rgbv = g->gathered[j];
-            HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, src, g->fb[j], s));
-        }
+        if (is_root)
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t j = g->bj[i];
+                OutPlanes src{};
+                src.rgbv = g->gathered[j];
+                HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, src, g->fb[j], s));
+            }
     }
     HT(5);
-    HIP_TRY(hipEventRecord(g->ev_done[j], s));
+    HIP_TRY(hipEventRecord(g->ev_done[bs], s));
     HT(6);
+    ++g->nb;
+    return MIRT_OK;
+}
+
+int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (g->k != 0) return fail(MIRT_E_INVALID, "set the batch before the first frame");
+    if (frames_per_launch < 1 || frames_per_launch > kMaxFrames || frames_per_launch > g->F)
+        return fail(MIRT_E_INVALID, "frames per launch must be 1..min(8, inflight)");
+    g->B = frames_per_launch;
+    g->FB = g->F / g->B;
+    return MIRT_OK;
+}
+
+int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
+    if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
+    mirt_ctx* c = g->c;
+    HT_START();
+    HIP_TRY(hipSetDevice(c->device));
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    const uint32_t j = (uint32_t)(g->k % g->F);
+    const bool is_root = g->rank == g->root;
+    OutPlanes out{};
+    if (!g->tiled) {
+        out = g->fb[j];
+    } else {
+        out.rgbv = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->packed[j];
+    }
+    FrameRec rec{};
+    uint64_t tris = 0;
+    frame_record(c, f, g->W, g->H, out, rec, tris);
+    HT(1);
+    if (g->bn > 0 && (g->bbounces || f->max_bounces || !frames_batchable(g->slots[g->nb % g->FB]->h_frames[0], rec)))
+        if ((r = group_flush(g)) != MIRT_OK) return r;
+    const uint32_t bs = (uint32_t)(g->nb % g->FB);
+    // back-pressure when a batch opens: batch nb - FB (the last user of this slot, and of
+    // every framebuffer this batch can touch) must have finished
+    if (g->bn == 0 && g->nb >= g->FB) HIP_TRY(hipEventSynchronize(g->ev_done[bs]));
+    HT(0);
+    g->slots[bs]->h_frames[g->bn] = rec;
+    g->bj[g->bn++] = j;
+    g->bbounces = f->max_bounces;
     if (index) *index = g->k;
     ++g->k;
+    if (g->bn == g->B || g->bbounces) return group_flush(g);
     return MIRT_OK;
 }
 
 int mirt_group_wait(mirt_group* g, void* stream) {
     if (!g) return fail(MIRT_E_INVALID, "NULL group");
     HIP_TRY(hipSetDevice(g->c->device));
-    const uint64_t used = std::min<uint64_t>(g->k, g->F);
+    int r = group_flush(g);
+    if (r != MIRT_OK) return r;
+    const uint64_t used = std::min<uint64_t>(g->nb, g->FB);
     for (uint64_t j = 0; j < used; ++j) {
         if (stream) {
             HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[j], 0));

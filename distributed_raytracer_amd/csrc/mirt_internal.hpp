@@ -181,6 +181,16 @@ struct FrustumArgs {
     uint32_t pad;
 };
 
+// One frame of a k_trace launch, in device memory (a launch traces up to kMaxFrames
+// frames that share the mesh, object count, light count and options; the kernel
+// argument FrameArgs is the first frame's).
+constexpr uint32_t kMaxFrames = 8;
+struct alignas(16) FrameRec {
+    FrameArgs fa;
+    OutPlanes out;
+    FrustumArgs fr;
+};
+
 // Per-frame work description shared by the primary, shadow and shade kernels.
 struct WorkArgs {
     const BlockDesc* blocks;
@@ -202,6 +212,9 @@ struct WorkArgs {
     uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
     cnt_t* summary;        // kStatN totals of this frame (written by k_shade's last workgroup)
     cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
+    const FrameRec* frames;  // k_trace: nframes records; blocks [f * nblocks_frame, ...) are frame f's
+    uint32_t nframes;
+    uint32_t nblocks_frame;  // nblocks = nframes * nblocks_frame; the table describes one frame
 };
 constexpr int kTimelineRec = 8;
 // WorkArgs::dynamic: kernels whose waves take work items dynamically (primary: LDS tickets
@@ -221,6 +234,7 @@ struct RayIO {
     uint32_t n;
 };
 
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s);
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,

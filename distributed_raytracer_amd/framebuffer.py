@@ -392,10 +392,12 @@ class NativeFrameGroup:
     (rank 0 only), every stream on a hardware queue of its own."""
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 8,
-                 inflight: int = 4, group=None, with_rgb: bool = False, tile_h: Optional[int] = 0):
+                 inflight: int = 4, group=None, with_rgb: bool = False, tile_h: Optional[int] = 0,
+                 batch: int = 1):
         import torch
         self.ctx, self.W, self.H, self.rank, self.world = ctx, W, H, rank, world
         self.F = max(1, int(inflight))
+        self.B = max(1, min(int(batch), self.F, 8))  # frames per k_trace launch
         self.device = torch.device("cuda", ctx.device)
         tile = (tile or 0) if world == 1 else int(tile or 8)
         th = tile if tile_h is None else int(tile_h)  # 0: full-height strips
@@ -406,7 +408,8 @@ class NativeFrameGroup:
             # (2 per CU can be resident; factor 4 = twice what fits)
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
             wg_factor = float(os.environ.get("MIRT_WG_FACTOR", "4"))
-            ctx.set_grid(int(os.environ.get("MIRT_MIN_BLOCKS", "32")), max(1, int(wg_factor * cus / self.F)))
+            launches = max(1, self.F // self.B)  # launches in flight
+            ctx.set_grid(int(os.environ.get("MIRT_MIN_BLOCKS", "32")), max(1, int(wg_factor * cus / launches)))
         uid = (C.c_uint8 * 128)()
         if world > 1:
             import torch.distributed as dist
@@ -422,6 +425,8 @@ class NativeFrameGroup:
         L.check(L.lib().mirt_group_create(ctx.handle, C.cast(uid, C.c_void_p) if world > 1 else None, rank, world,
                                           W, H, tile, th if tile else 0, self.F, C.cast(fbs, C.c_void_p) if fbs else None,
                                           C.byref(self._h)))
+        if self.B > 1:
+            L.check(L.lib().mirt_group_set_batch(self._h, self.B))
         self._k = 0
         self._idx = C.c_uint64()
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 2
+#define MIRT_ABI_VERSION 3
 
 /* error codes */
 #define MIRT_OK 0
@@ -151,6 +151,9 @@ typedef struct {
     /* configs[4] extension: reflection rays traced and the reflect kernel's device time */
     uint64_t reflection_rays;
     double reflect_ms_sum;
+    /* frames traced (a frame group launches up to 8 frames at once: per-frame figures
+       divide by frames, per-launch kernel times by launches) */
+    uint64_t frames;
 } mirt_profile;
 
 int mirt_abi_version(void);
@@ -292,6 +295,11 @@ typedef struct mirt_group mirt_group;
 int mirt_group_unique_id(uint8_t *id);
 int mirt_group_create(mirt_ctx *ctx, const uint8_t *unique_id, int rank, int world, uint32_t W, uint32_t H,
                       uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs *fbs, mirt_group **out);
+/* Frames per k_trace launch (1..min(8, inflight), default 1), before the first frame:
+ * mirt_trace_frame then only stages a frame until the batch is full (or the next frame
+ * differs in mesh, objects, lights or options, or mirt_group_wait flushes it); the batch's
+ * frames are traced by one launch and gathered by one RCCL group.  Results are the same. */
+int mirt_group_set_batch(mirt_group *g, uint32_t frames_per_launch);
 int mirt_trace_frame(mirt_group *group, const mirt_frame *frame, uint64_t *index);
 int mirt_group_wait(mirt_group *group, void *stream);
 void mirt_group_destroy(mirt_group *group);

@@ -483,13 +483,16 @@ def test_octant_child_test_changes_nothing(ctx, env):
         ctx.set_options(0)
 
 
-@pytest.mark.parametrize("tile,tile_h,inflight", [(None, 0, 4), (32, 32, 3), (8, 0, 2), (48, 0, 1)])
-def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight):
+@pytest.mark.parametrize("tile,tile_h,inflight,batch", [
+    (None, 0, 4, 1), (32, 32, 3, 1), (8, 0, 2, 1), (48, 0, 1, 1),
+    (None, 0, 4, 4), (8, 0, 4, 2), (32, 32, 6, 3), (None, 0, 3, 2), (8, 0, 8, 8)])
+def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight, batch):
     """mirt_trace_frame (the native multi-GPU frame driver) on one GPU: the whole screen
     (tile=None) or the tiled path rehearsed with world = 1 (packed rgbv tiles or
     full-height strips, the unpack table with per-rank offsets), frames in flight with
-    alternating cameras; every
-    framebuffer equals its camera's frame drawn alone."""
+    alternating cameras, and several frames per k_trace launch (batch; a frame with
+    fewer lights cannot share a launch and closes the batch early); every framebuffer
+    equals its frame drawn alone."""
     import torch
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd.framebuffer import NativeFrameGroup
@@ -498,11 +501,12 @@ def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight):
     c = base.cam
     cams = [c, rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.7, 0.3, 0.0])), c.forward, c.fov)]
     muts = [rt.EnvMutables(base.objects, base.lights, cm) for cm in cams]
+    muts.append(rt.EnvMutables(base.objects, base.lights[:2], cams[1]))  # fewer lights
     frames = [m.to_frame() for m in muts]
     refs = [rt.draw(env, W, H, m) for m in muts]
     try:
-        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight, tile_h=tile_h)
-        order = [0, 1, 1, 0, 1, 0, 0, 1]
+        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight, tile_h=tile_h, batch=batch)
+        order = [0, 1, 1, 0, 1, 0, 0, 1, 2, 0, 1, 1, 0, 2, 1, 0]
         for q in order:
             g.render(frames[q])
         g.flush()

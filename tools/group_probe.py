@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--view", default="default", choices=("default", "away"))
     ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--batch", type=int, default=1)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -31,7 +32,7 @@ def main():
         mut = rt.EnvMutables(mut.objects, mut.lights, rt.Camera.new(c.pos, tuple(-np.asarray(c.forward)), c.fov))
     fr = mut.to_frame()
     W, H = (int(x) for x in a.size.split("x"))
-    g = NativeFrameGroup(ctx, W, H, 0, 1, a.tile or None, inflight=a.inflight)
+    g = NativeFrameGroup(ctx, W, H, 0, 1, a.tile or None, inflight=a.inflight, batch=a.batch)
     for _ in range(20):
         g.render(fr)
     g.flush()
@@ -45,7 +46,7 @@ def main():
     t1 = time.perf_counter()
     g.flush()
     torch.cuda.synchronize()
-    print(json.dumps({"tile": a.tile, "inflight": a.inflight, "view": a.view, "size": a.size,
+    print(json.dumps({"tile": a.tile, "inflight": a.inflight, "batch": a.batch, "view": a.view, "size": a.size,
                       "rehearse": os.environ.get("MIRT_GROUP_REHEARSE", "1"),
                       "frame_interval_us": round((time.perf_counter() - t0) / a.frames * 1e6, 1),
                       "host_enqueue_us": round((t1 - t0) / a.frames * 1e6, 1),
