@@ -313,7 +313,7 @@ def main():
                          # with frames in flight a launch shares the chip with its neighbours,
                          # so per-launch time overstates the cost: the same bytes per frame
                          # over the steady-state frame interval
-                         "chip_rate_gbs": round(k_tests * BYTES_PER_TRI_TEST / (ms / 1e3) / 1e9, 1),
+                         "chip_rate_gbs": round(k_tests * launches / pl * BYTES_PER_TRI_TEST / (ms / 1e3) / 1e9, 1),
                          "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
                                  "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
                                  "VALU, see DESIGN.md; kernel time = HIP events on the trace stream over a second "
