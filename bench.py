@@ -43,8 +43,8 @@ HOST_CORES = 16  # the GPU box's CPU share for one GPU (os.cpu_count() shows the
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tile", type=int, default=8, help="multi-GPU deal unit: tile width (pixels)")
