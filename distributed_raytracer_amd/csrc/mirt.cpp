@@ -1307,6 +1307,7 @@ struct mirt_group {
     std::vector<std::unique_ptr<Slot>> slots;
     uint64_t k = 0;                     // frames enqueued
     int plan_world = 1;                 // ranks of the tile deal (== world except in a rehearsal)
+    bool skip_unpack = false;           // rehearsal diagnostic: a non-root rank's work (trace only)
     // frames per k_trace launch (mirt_group_set_batch): frames accumulate in the open batch,
     // which launches when full, when an incompatible frame arrives, or at mirt_group_wait.
     // Batch b uses batch slot b % FB (its workspace, stream and events), FB = F / B, so the
@@ -1394,6 +1395,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     const char* reh = getenv("MIRT_GROUP_REHEARSE");
     const int plan_world = (world == 1 && g->tiled && reh && atoi(reh) > 1) ? atoi(reh) : world;
     g->plan_world = plan_world;
+    g->skip_unpack = plan_world != world && getenv("MIRT_GROUP_REHEARSE_NO_UNPACK");
     if (g->tiled) {
         plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)rank, g->mine);
         for (int r = 0; r < plan_world; ++r) {
@@ -1502,7 +1504,7 @@ static int group_flush(mirt_group* g) {
             if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
         }
         HT(4);
-        if (is_root)
+        if (is_root && !g->skip_unpack)
             for (uint32_t i = 0; i < n; ++i) {
                 const uint32_t j = g->bj[i];
                 OutPlanes src{};
