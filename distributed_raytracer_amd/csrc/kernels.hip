@@ -1843,6 +1843,103 @@ hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_ti
     return hipGetLastError();
 }
 
+// rgbv words -> the transfer form (rgb24_region_bytes), every frame of a batch in one launch
+// (grid y): a thread packs 8 pixels (6 colour dwords and one valid byte).  npix is rounded
+// up to 8 (the plane holds cap >= that words).
+__global__ __launch_bounds__(256) void k_pack24(PackJobs jobs, uint64_t n8, uint64_t cap) {
+    const uint4* __restrict__ src = (const uint4*)jobs.src[blockIdx.y];  // frame blockIdx.y of the batch
+    uint8_t* __restrict__ region = jobs.dst[blockIdx.y];
+    uint32_t* rgb = (uint32_t*)region;
+    uint8_t* vb = region + rgb24_valid_offset(cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        uint32_t* o = rgb + 6 * i;  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3 (x2)
+        o[0] = (a.x & 0xffffffu) | (a.y << 24);
+        o[1] = ((a.y >> 8) & 0xffffu) | (a.z << 16);
+        o[2] = ((a.z >> 16) & 0xffu) | ((a.w & 0xffffffu) << 8);
+        o[3] = (b.x & 0xffffffu) | (b.y << 24);
+        o[4] = ((b.y >> 8) & 0xffffu) | (b.z << 16);
+        o[5] = ((b.z >> 16) & 0xffu) | ((b.w & 0xffffffu) << 8);
+        vb[i] = (uint8_t)((a.x >> 24) | ((a.y >> 24) << 1) | ((a.z >> 24) << 2) | ((a.w >> 24) << 3) |
+                          ((b.x >> 24) << 4) | ((b.y >> 24) << 5) | ((b.z >> 24) << 6) | ((b.w >> 24) << 7));
+    }
+}
+hipError_t launch_pack24(const PackJobs& jobs, uint32_t nframes, uint64_t npix, uint64_t cap, hipStream_t s) {
+    const uint64_t n8 = (npix + 7) / 8;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n8 + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_pack24, dim3(grid, nframes), dim3(256), 0, s, jobs, n8, cap);
+    return hipGetLastError();
+}
+
+// The transfer form -> framebuffer planes (rgb8 is a straight copy of the colour bytes).
+// Grid as k_unpack: x over tiles, y over 1024-pixel chunks.
+__global__ __launch_bounds__(256) void k_unpack24(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t H,
+                                                  UnpackJobs jobs, uint64_t cap) {
+    const uint8_t* __restrict__ regions = jobs.src[blockIdx.z];  // frame blockIdx.z of the batch
+    const OutPlanes dst = jobs.dst[blockIdx.z];
+    const uint64_t rbytes = rgb24_region_bytes(cap), voff = rgb24_valid_offset(cap);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const TileDesc td = tiles[__builtin_amdgcn_readfirstlane(t)];
+        const uint8_t* rgb = regions + (uint64_t)td.region * rbytes;
+        const uint8_t* vb = rgb + voff;
+        const uint32_t n = td.w * td.h;
+        const bool fast = (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0 && (td.out_off & 3u) == 0;
+        for (uint32_t c0 = blockIdx.y * kUnpackChunk; c0 < n; c0 += gridDim.y * kUnpackChunk) {
+            if (fast) {
+                const uint32_t local = c0 + threadIdx.x * 4;
+                if (local >= n) continue;
+                const uint32_t lx = local / td.h, ly = local - lx * td.h;
+                const uint64_t p = td.out_off + local;  // multiple of 4
+                const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
+                const uint32_t* c = (const uint32_t*)(rgb + 3 * p);
+                const uint32_t c0w = c[0], c1w = c[1], c2w = c[2];
+                const uint32_t v4 = (vb[p >> 3] >> (p & 7u)) & 0xfu;
+                if (dst.rgb8) {
+                    uint32_t* o = (uint32_t*)(dst.rgb8 + 3 * q);
+                    o[0] = c0w;
+                    o[1] = c1w;
+                    o[2] = c2w;
+                }
+                if (dst.valid)
+                    *(uint32_t*)(dst.valid + q) = (v4 & 1u) | (((v4 >> 1) & 1u) << 8) | (((v4 >> 2) & 1u) << 16) |
+                                                  (((v4 >> 3) & 1u) << 24);
+                if (dst.rgbv) {
+                    uint4 w;
+                    w.x = (c0w & 0xffffffu) | ((v4 & 1u) << 24);
+                    w.y = (c0w >> 24) | ((c1w & 0xffffu) << 8) | (((v4 >> 1) & 1u) << 24);
+                    w.z = (c1w >> 16) | ((c2w & 0xffu) << 16) | (((v4 >> 2) & 1u) << 24);
+                    w.w = (c2w >> 8) | (((v4 >> 3) & 1u) << 24);
+                    *(uint4*)(dst.rgbv + q) = w;
+                }
+            } else {
+                const uint32_t end = min(n, c0 + kUnpackChunk);
+                for (uint32_t local = c0 + threadIdx.x; local < end; local += blockDim.x) {
+                    const uint32_t lx = local / td.h, ly = local - lx * td.h;
+                    const uint64_t p = td.out_off + local;
+                    const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
+                    const uint8_t r = rgb[3 * p], g = rgb[3 * p + 1], b = rgb[3 * p + 2];
+                    const uint32_t v = (vb[p >> 3] >> (p & 7u)) & 1u;
+                    if (dst.rgb8) {
+                        dst.rgb8[3 * q] = r;
+                        dst.rgb8[3 * q + 1] = g;
+                        dst.rgb8[3 * q + 2] = b;
+                    }
+                    if (dst.valid) dst.valid[q] = (uint8_t)v;
+                    if (dst.rgbv) dst.rgbv[q] = r | ((uint32_t)g << 8) | ((uint32_t)b << 16) | (v << 24);
+                }
+            }
+        }
+    }
+}
+hipError_t launch_unpack24(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H,
+                           const UnpackJobs& jobs, uint32_t nframes, uint64_t cap, hipStream_t s) {
+    const uint32_t gx = ntiles < 8192u ? (ntiles ? ntiles : 1u) : 8192u;
+    const uint64_t chunks = (max_tile_px + kUnpackChunk - 1) / kUnpackChunk;
+    const uint32_t gy = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunks, std::max<uint64_t>(1, 16384 / gx)));
+    hipLaunchKernelGGL(k_unpack24, dim3(gx, gy, nframes), dim3(256), 0, s, tiles, ntiles, H, jobs, cap);
+    return hipGetLastError();
+}
+
 // Copy a launch's frame records from pinned host memory to the device (one workgroup; a
 // hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there).
 __global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,

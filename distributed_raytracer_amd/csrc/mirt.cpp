@@ -972,7 +972,7 @@ int unpack_impl(mirt_ctx* c, uint32_t W, uint32_t H, const mirt_tile* tiles, con
             return fail(MIRT_E_INVALID, "tile " + std::to_string(t) + " is empty or exceeds the screen");
         const uint64_t off = offsets ? offsets[t] : pixels;
         if (off < span) return fail(MIRT_E_INVALID, "tile offsets must ascend without overlap");
-        td[t] = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, off, {0, 0}};
+        td[t] = TileDesc{tiles[t].x, tiles[t].y, tiles[t].w, tiles[t].h, off, 0, 0};
         pixels += (uint64_t)tiles[t].w * tiles[t].h;
         span = off + (uint64_t)tiles[t].w * tiles[t].h;
         max_px = std::max<uint64_t>(max_px, (uint64_t)tiles[t].w * tiles[t].h);
@@ -1296,8 +1296,10 @@ struct mirt_group {
     std::vector<hipEvent_t> ev_traced, ev_gathered, ev_done;
     std::vector<mirt_tile> mine;
     uint64_t cap = 0;                   // largest rank share (pixels): every rank's gather size
-    std::vector<uint32_t*> packed;      // non-root: my packed rgbv plane per frame slot
-    std::vector<uint32_t*> gathered;    // root: world * cap rgbv words per frame slot
+    std::vector<uint32_t*> packed;      // tiled: my tiles' rgbv plane per frame slot (the trace's output)
+    std::vector<uint8_t*> send24;       // non-root: its transfer form (rgb24_region_bytes(cap)) per frame slot
+    std::vector<uint8_t*> gathered;     // root: world regions in the transfer form per frame slot
+    uint64_t rbytes = 0;                // bytes of one region
     std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
     TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
     uint32_t n_unpack = 0;
@@ -1356,7 +1358,9 @@ void mirt_group_destroy(mirt_group* g) {
     for (auto& sl : g->slots) slot_free(sl.get());
     for (uint32_t* p : g->packed)
         if (p) (void)hipFree(p);
-    for (uint32_t* p : g->gathered)
+    for (uint8_t* p : g->gathered)
+        if (p) (void)hipFree(p);
+    for (uint8_t* p : g->send24)
         if (p) (void)hipFree(p);
     if (g->d_unpack) (void)hipFree(g->d_unpack);
     for (auto* v : {&g->ev_traced, &g->ev_gathered, &g->ev_done})
@@ -1404,6 +1408,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             g->cap = std::max(g->cap, tiles_pixels(t));
         }
         if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
+        g->cap = (g->cap + 31) & ~31ull;  // k_pack24 packs 8 pixels per thread
+        g->rbytes = rgb24_region_bytes(g->cap);
     } else {
         g->mine.push_back(mirt_tile{0, 0, W, H});
         g->cap = (uint64_t)W * H;
@@ -1428,17 +1434,19 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
         for (uint32_t j = 0; j < inflight; ++j)
             g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
     if (g->tiled) {
+        g->packed.assign(inflight, nullptr);
+        for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->packed[j], g->cap * 4));
         if (is_root) {
             g->gathered.assign(inflight, nullptr);
             for (uint32_t j = 0; j < inflight; ++j)
-                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->cap * 4));
+                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->rbytes));
             std::vector<TileDesc> td;
             for (int r = 0; r < plan_world; ++r) {
                 std::vector<mirt_tile> t;
                 plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t);
-                uint64_t o = (uint64_t)r * g->cap;
+                uint64_t o = 0;  // within region r
                 for (const mirt_tile& x : t) {
-                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, {0, 0}});
+                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, (uint32_t)r, 0});
                     o += (uint64_t)x.w * x.h;
                     g->max_tile_px = std::max<uint64_t>(g->max_tile_px, (uint64_t)x.w * x.h);
                 }
@@ -1447,8 +1455,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             HIP_TRY(hipMalloc((void**)&g->d_unpack, td.size() * sizeof(TileDesc)));
             HIP_TRY(hipMemcpy(g->d_unpack, td.data(), td.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
         } else {
-            g->packed.assign(inflight, nullptr);
-            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->packed[j], g->cap * 4));
+            g->send24.assign(inflight, nullptr);
+            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->send24[j], g->rbytes));
         }
     }
     if (world > 1) {
@@ -1482,21 +1490,29 @@ static int group_flush(mirt_group* g) {
         return r;
     }
     if (g->tiled) {
+        // every frame's rgbv tiles -> the transfer form (the root packs into its own region)
+        PackJobs jobs{};
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t j = g->bj[i];
+            jobs.src[i] = g->packed[j];
+            jobs.dst[i] = is_root ? g->gathered[j] + (uint64_t)g->root * g->rbytes : g->send24[j];
+        }
+        HIP_TRY(launch_pack24(jobs, n, tiles_pixels(g->mine), g->cap, s));
         if (g->world > 1) {
             const Rccl& R = rccl();
             HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
             HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
-            const size_t bytes = g->cap * 4;
+            const size_t bytes = g->rbytes;
             RCCL_TRY(R.group_start());
             for (uint32_t i = 0; i < n; ++i) {
                 const uint32_t j = g->bj[i];
                 if (is_root) {
                     for (int q = 0; q < g->world; ++q)
                         if (q != g->root)
-                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, bytes, ncclUint8, q, g->comm,
+                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->rbytes, bytes, ncclUint8, q, g->comm,
                                             g->comm_stream));
                 } else {
-                    RCCL_TRY(R.send(g->packed[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
+                    RCCL_TRY(R.send(g->send24[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
                 }
             }
             RCCL_TRY(R.group_end());
@@ -1504,13 +1520,14 @@ static int group_flush(mirt_group* g) {
             if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
         }
         HT(4);
-        if (is_root && !g->skip_unpack)
+        if (is_root && !g->skip_unpack) {
+            UnpackJobs uj{};
             for (uint32_t i = 0; i < n; ++i) {
-                const uint32_t j = g->bj[i];
-                OutPlanes src{};
-                src.rgbv = g->gathered[j];
-                HIP_TRY(launch_unpack(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, src, g->fb[j], s));
+                uj.src[i] = g->gathered[g->bj[i]];
+                uj.dst[i] = g->fb[g->bj[i]];
             }
+            HIP_TRY(launch_unpack24(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, uj, n, g->cap, s));
+        }
     }
     HT(5);
     HIP_TRY(hipEventRecord(g->ev_done[bs], s));
@@ -1537,12 +1554,11 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
     const uint32_t j = (uint32_t)(g->k % g->F);
-    const bool is_root = g->rank == g->root;
     OutPlanes out{};
     if (!g->tiled) {
         out = g->fb[j];
     } else {
-        out.rgbv = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->packed[j];
+        out.rgbv = g->packed[j];
     }
     FrameRec rec{};
     uint64_t tris = 0;
