@@ -612,13 +612,13 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     const int sgrid = (int)std::max<uint64_t>(
         1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-    if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
     if (one_launch) {
         // one launch for the frames (k_trace); its time lands in the primary slot of the profile
         FrameRec* src = nullptr;
         HIP_TRY(hipHostGetDevicePointer((void**)&src, sl->h_frames, 0));
         HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
         wa.frames = sl->d_frames;
+        if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
         HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
         HT(3);
@@ -627,6 +627,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             HIP_TRY(hipEventRecord(pr.ev[2], s));
         }
     } else {
+        if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
         HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
         if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");

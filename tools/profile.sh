@@ -9,7 +9,7 @@ W=${W:-1920}; H=${H:-1080}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity --width $W --height $H ${BENCH_ARGS:-}"
+BENCH="bench.py --steps ${STEPS:-500} --warmup 20 --no-cpu-baseline --no-parity --width $W --height $H ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH \
   > "$OUT/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 echo "trace pass ok"
