@@ -1843,100 +1843,123 @@ hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_ti
     return hipGetLastError();
 }
 
-// rgbv words -> the transfer form (rgb24_region_bytes), every frame of a batch in one launch
-// (grid y): a thread packs 8 pixels (6 colour dwords and one valid byte).  npix is rounded
-// up to 8 (the plane holds cap >= that words).
-__global__ __launch_bounds__(256) void k_pack24(PackJobs jobs, uint64_t n8, uint64_t cap) {
-    const uint4* __restrict__ src = (const uint4*)jobs.src[blockIdx.y];  // frame blockIdx.y of the batch
-    uint8_t* __restrict__ region = jobs.dst[blockIdx.y];
-    uint32_t* rgb = (uint32_t*)region;
-    uint8_t* vb = region + rgb24_valid_offset(cap);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 a = src[2 * i], b = src[2 * i + 1];
-        uint32_t* o = rgb + 6 * i;  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3 (x2)
-        o[0] = (a.x & 0xffffffu) | (a.y << 24);
-        o[1] = ((a.y >> 8) & 0xffffu) | (a.z << 16);
-        o[2] = ((a.z >> 16) & 0xffu) | ((a.w & 0xffffffu) << 8);
-        o[3] = (b.x & 0xffffffu) | (b.y << 24);
-        o[4] = ((b.y >> 8) & 0xffffu) | (b.z << 16);
-        o[5] = ((b.z >> 16) & 0xffu) | ((b.w & 0xffffffu) << 8);
-        vb[i] = (uint8_t)((a.x >> 24) | ((a.y >> 24) << 1) | ((a.z >> 24) << 2) | ((a.w >> 24) << 3) |
-                          ((b.x >> 24) << 4) | ((b.y >> 24) << 5) | ((b.z >> 24) << 6) | ((b.w >> 24) << 7));
+// The transfer form of the multi-GPU frame (mirt_group): for each of a rank's tiles only
+// its pixels inside the frame's hit rectangle (mirt.cpp hit_rect: no pixel outside it can
+// meet the object), column-major per tile, tiles back to back, as rgbv words.  Every rank
+// derives the same rectangle from the same frame, so the sizes need no exchange.
+__device__ __forceinline__ uint32_t tile_rect(const TileDesc& td, const uint32_t* R, uint32_t& cx0, uint32_t& cy0,
+                                              uint32_t& cw, uint32_t& ch) {
+    cx0 = max(td.x, R[0]);
+    cy0 = max(td.y, R[1]);
+    const uint32_t cx1 = min(td.x + td.w, R[2]), cy1 = min(td.y + td.h, R[3]);
+    cw = cx1 > cx0 ? cx1 - cx0 : 0u;
+    ch = cy1 > cy0 ? cy1 - cy0 : 0u;
+    return cw * ch;
+}
+// words of tiles [first, t) inside R (tiles of one rank are contiguous in the table): the
+// wave's lanes take every 64th tile, then a butterfly sum (every wave computes it)
+__device__ __forceinline__ uint64_t rect_offset(const TileDesc* __restrict__ tiles, uint32_t first, uint32_t t,
+                                                const uint32_t* R) {
+    uint32_t acc = 0;  // < W * H < 2^32
+    for (uint32_t u = first + (threadIdx.x & 63); u < t; u += 64) {
+        uint32_t a, b, c, d;
+        acc += tile_rect(tiles[u], R, a, b, c, d);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    return acc;
+}
+// grid x: the rank's tiles, z: the frame of the batch
+__global__ __launch_bounds__(256) void k_pack_rect(const TileDesc* __restrict__ tiles, uint32_t ntiles, RectJobs jobs) {
+    const uint32_t f = blockIdx.z;
+    const uint32_t* R = jobs.rect[f];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t tt = __builtin_amdgcn_readfirstlane(t);
+        const TileDesc td = tiles[tt];
+        uint32_t cx0, cy0, cw, ch;
+        const uint32_t n = tile_rect(td, R, cx0, cy0, cw, ch);
+        if (n == 0) continue;
+        const uint64_t off = rect_offset(tiles, 0, tt, R);
+        const uint32_t* __restrict__ src = jobs.src[f] + td.out_off;
+        uint32_t* __restrict__ dst = jobs.dst[f] + off;
+        for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) {
+            const uint32_t lx = p / ch, ly = p - lx * ch;
+            dst[p] = src[(uint64_t)(cx0 - td.x + lx) * td.h + (cy0 - td.y + ly)];
+        }
     }
 }
-hipError_t launch_pack24(const PackJobs& jobs, uint32_t nframes, uint64_t npix, uint64_t cap, hipStream_t s) {
-    const uint64_t n8 = (npix + 7) / 8;
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n8 + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_pack24, dim3(grid, nframes), dim3(256), 0, s, jobs, n8, cap);
+hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_pack_rect, dim3(ntiles ? ntiles : 1u, 1, nframes), dim3(256), 0, s, tiles, ntiles, jobs);
     return hipGetLastError();
 }
 
-// The transfer form -> framebuffer planes (rgb8 is a straight copy of the colour bytes).
-// Grid as k_unpack: x over tiles, y over 1024-pixel chunks.
-__global__ __launch_bounds__(256) void k_unpack24(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t H,
-                                                  UnpackJobs jobs, uint64_t cap) {
-    const uint8_t* __restrict__ regions = jobs.src[blockIdx.z];  // frame blockIdx.z of the batch
-    const OutPlanes dst = jobs.dst[blockIdx.z];
-    const uint64_t rbytes = rgb24_region_bytes(cap), voff = rgb24_valid_offset(cap);
+// Gathered regions (rank r at word r * cap) -> framebuffer planes; pixels outside the hit
+// rectangle are misses.  Grid as k_unpack (x: tile, y: 1024-pixel chunk), z: frame.
+__global__ __launch_bounds__(256) void k_unpack_rect(const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t H,
+                                                     uint64_t cap, RectJobs jobs) {
+    const uint32_t f = blockIdx.z;
+    const uint32_t* R = jobs.rect[f];
+    const OutPlanes dst = jobs.out[f];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const TileDesc td = tiles[__builtin_amdgcn_readfirstlane(t)];
-        const uint8_t* rgb = regions + (uint64_t)td.region * rbytes;
-        const uint8_t* vb = rgb + voff;
+        const uint32_t tt = __builtin_amdgcn_readfirstlane(t);
+        const TileDesc td = tiles[tt];
+        uint32_t cx0, cy0, cw, ch;
+        tile_rect(td, R, cx0, cy0, cw, ch);
+        const uint64_t off = rect_offset(tiles, td.pad, tt, R);  // pad: the region's first tile
+        const uint32_t* __restrict__ src = jobs.src[f] + (uint64_t)td.region * cap + off;
         const uint32_t n = td.w * td.h;
-        const bool fast = (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0 && (td.out_off & 3u) == 0;
+        const bool fast = (td.h & 3u) == 0 && (td.y & 3u) == 0 && (H & 3u) == 0;
         for (uint32_t c0 = blockIdx.y * kUnpackChunk; c0 < n; c0 += gridDim.y * kUnpackChunk) {
-            if (fast) {
+            if (fast) {  // 4 pixels of one column per thread: 16-byte / 4-byte aligned stores
                 const uint32_t local = c0 + threadIdx.x * 4;
                 if (local >= n) continue;
                 const uint32_t lx = local / td.h, ly = local - lx * td.h;
-                const uint64_t p = td.out_off + local;  // multiple of 4
-                const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
-                const uint32_t* c = (const uint32_t*)(rgb + 3 * p);
-                const uint32_t c0w = c[0], c1w = c[1], c2w = c[2];
-                const uint32_t v4 = (vb[p >> 3] >> (p & 7u)) & 0xfu;
-                if (dst.rgb8) {
-                    uint32_t* o = (uint32_t*)(dst.rgb8 + 3 * q);
-                    o[0] = c0w;
-                    o[1] = c1w;
-                    o[2] = c2w;
+                const uint32_t X = td.x + lx, Y = td.y + ly;
+                const bool xin = X >= cx0 && X < cx0 + cw;
+                uint32_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t y = Y + k;
+                    v[k] = xin && y >= cy0 && y < cy0 + ch ? src[(uint64_t)(X - cx0) * ch + (y - cy0)] : 0u;
                 }
+                const uint64_t q = (uint64_t)X * H + Y;  // multiple of 4
+                if (dst.rgbv) *(uint4*)(dst.rgbv + q) = make_uint4(v[0], v[1], v[2], v[3]);
                 if (dst.valid)
-                    *(uint32_t*)(dst.valid + q) = (v4 & 1u) | (((v4 >> 1) & 1u) << 8) | (((v4 >> 2) & 1u) << 16) |
-                                                  (((v4 >> 3) & 1u) << 24);
-                if (dst.rgbv) {
-                    uint4 w;
-                    w.x = (c0w & 0xffffffu) | ((v4 & 1u) << 24);
-                    w.y = (c0w >> 24) | ((c1w & 0xffffu) << 8) | (((v4 >> 1) & 1u) << 24);
-                    w.z = (c1w >> 16) | ((c2w & 0xffu) << 16) | (((v4 >> 2) & 1u) << 24);
-                    w.w = (c2w >> 8) | (((v4 >> 3) & 1u) << 24);
-                    *(uint4*)(dst.rgbv + q) = w;
+                    *(uint32_t*)(dst.valid + q) = (v[0] >> 24) | ((v[1] >> 24) << 8) | ((v[2] >> 24) << 16) |
+                                                  ((v[3] >> 24) << 24);
+                if (dst.rgb8) {  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+                    uint32_t* o = (uint32_t*)(dst.rgb8 + 3 * q);
+                    o[0] = (v[0] & 0xffffffu) | (v[1] << 24);
+                    o[1] = ((v[1] >> 8) & 0xffffu) | (v[2] << 16);
+                    o[2] = ((v[2] >> 16) & 0xffu) | ((v[3] & 0xffffffu) << 8);
                 }
-            } else {
-                const uint32_t end = min(n, c0 + kUnpackChunk);
-                for (uint32_t local = c0 + threadIdx.x; local < end; local += blockDim.x) {
-                    const uint32_t lx = local / td.h, ly = local - lx * td.h;
-                    const uint64_t p = td.out_off + local;
-                    const uint64_t q = (uint64_t)(td.x + lx) * H + (td.y + ly);
-                    const uint8_t r = rgb[3 * p], g = rgb[3 * p + 1], b = rgb[3 * p + 2];
-                    const uint32_t v = (vb[p >> 3] >> (p & 7u)) & 1u;
-                    if (dst.rgb8) {
-                        dst.rgb8[3 * q] = r;
-                        dst.rgb8[3 * q + 1] = g;
-                        dst.rgb8[3 * q + 2] = b;
-                    }
-                    if (dst.valid) dst.valid[q] = (uint8_t)v;
-                    if (dst.rgbv) dst.rgbv[q] = r | ((uint32_t)g << 8) | ((uint32_t)b << 16) | (v << 24);
+                continue;
+            }
+            const uint32_t end = min(n, c0 + kUnpackChunk);
+            for (uint32_t local = c0 + threadIdx.x; local < end; local += blockDim.x) {
+                const uint32_t lx = local / td.h, ly = local - lx * td.h;
+                const uint32_t X = td.x + lx, Y = td.y + ly;
+                const bool in = X >= cx0 && X < cx0 + cw && Y >= cy0 && Y < cy0 + ch;
+                const uint32_t v = in ? src[(uint64_t)(X - cx0) * ch + (Y - cy0)] : 0u;
+                const uint64_t q = (uint64_t)X * H + Y;
+                if (dst.rgbv) dst.rgbv[q] = v;
+                if (dst.valid) dst.valid[q] = (uint8_t)(v >> 24);
+                if (dst.rgb8) {
+                    dst.rgb8[3 * q] = (uint8_t)v;
+                    dst.rgb8[3 * q + 1] = (uint8_t)(v >> 8);
+                    dst.rgb8[3 * q + 2] = (uint8_t)(v >> 16);
                 }
             }
         }
     }
 }
-hipError_t launch_unpack24(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H,
-                           const UnpackJobs& jobs, uint32_t nframes, uint64_t cap, hipStream_t s) {
+hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, uint64_t cap,
+                              const RectJobs& jobs, uint32_t nframes, hipStream_t s) {
     const uint32_t gx = ntiles < 8192u ? (ntiles ? ntiles : 1u) : 8192u;
     const uint64_t chunks = (max_tile_px + kUnpackChunk - 1) / kUnpackChunk;
     const uint32_t gy = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunks, std::max<uint64_t>(1, 16384 / gx)));
-    hipLaunchKernelGGL(k_unpack24, dim3(gx, gy, nframes), dim3(256), 0, s, tiles, ntiles, H, jobs, cap);
+    hipLaunchKernelGGL(k_unpack_rect, dim3(gx, gy, nframes), dim3(256), 0, s, tiles, ntiles, H, cap, jobs);
     return hipGetLastError();
 }
 

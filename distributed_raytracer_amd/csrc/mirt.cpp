@@ -1298,9 +1298,10 @@ struct mirt_group {
     std::vector<mirt_tile> mine;
     uint64_t cap = 0;                   // largest rank share (pixels): every rank's gather size
     std::vector<uint32_t*> packed;      // tiled: my tiles' rgbv plane per frame slot (the trace's output)
-    std::vector<uint8_t*> send24;       // non-root: its transfer form (rgb24_region_bytes(cap)) per frame slot
-    std::vector<uint8_t*> gathered;     // root: world regions in the transfer form per frame slot
-    uint64_t rbytes = 0;                // bytes of one region
+    std::vector<uint32_t*> sendbuf;     // non-root: its transfer form (k_pack_rect) per frame slot
+    std::vector<uint32_t*> gathered;    // root: world regions of cap words in the transfer form per frame slot
+    std::vector<std::vector<mirt_tile>> plans;  // every rank's tiles (the transfer sizes)
+    TileDesc* d_mine = nullptr;         // my tiles with their offsets in my rgbv plane (k_pack_rect)
     std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
     TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
     uint32_t n_unpack = 0;
@@ -1359,10 +1360,11 @@ void mirt_group_destroy(mirt_group* g) {
     for (auto& sl : g->slots) slot_free(sl.get());
     for (uint32_t* p : g->packed)
         if (p) (void)hipFree(p);
-    for (uint8_t* p : g->gathered)
+    for (uint32_t* p : g->gathered)
         if (p) (void)hipFree(p);
-    for (uint8_t* p : g->send24)
+    for (uint32_t* p : g->sendbuf)
         if (p) (void)hipFree(p);
+    if (g->d_mine) (void)hipFree(g->d_mine);
     if (g->d_unpack) (void)hipFree(g->d_unpack);
     for (auto* v : {&g->ev_traced, &g->ev_gathered, &g->ev_done})
         for (hipEvent_t e : *v)
@@ -1409,8 +1411,9 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             g->cap = std::max(g->cap, tiles_pixels(t));
         }
         if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
-        g->cap = (g->cap + 31) & ~31ull;  // k_pack24 packs 8 pixels per thread
-        g->rbytes = rgb24_region_bytes(g->cap);
+        g->plans.resize((size_t)plan_world);
+        for (int r = 0; r < plan_world; ++r)
+            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, g->plans[(size_t)r]);
     } else {
         g->mine.push_back(mirt_tile{0, 0, W, H});
         g->cap = (uint64_t)W * H;
@@ -1437,17 +1440,26 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     if (g->tiled) {
         g->packed.assign(inflight, nullptr);
         for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->packed[j], g->cap * 4));
+        {
+            std::vector<TileDesc> md;
+            uint64_t o = 0;
+            for (const mirt_tile& x : g->mine) {
+                md.push_back(TileDesc{x.x, x.y, x.w, x.h, o, 0, 0});
+                o += (uint64_t)x.w * x.h;
+            }
+            HIP_TRY(hipMalloc((void**)&g->d_mine, md.size() * sizeof(TileDesc)));
+            HIP_TRY(hipMemcpy(g->d_mine, md.data(), md.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+        }
         if (is_root) {
             g->gathered.assign(inflight, nullptr);
             for (uint32_t j = 0; j < inflight; ++j)
-                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->rbytes));
+                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->cap * 4));
             std::vector<TileDesc> td;
             for (int r = 0; r < plan_world; ++r) {
-                std::vector<mirt_tile> t;
-                plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t);
+                const uint32_t first = (uint32_t)td.size();
                 uint64_t o = 0;  // within region r
-                for (const mirt_tile& x : t) {
-                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, (uint32_t)r, 0});
+                for (const mirt_tile& x : g->plans[(size_t)r]) {
+                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, (uint32_t)r, first});
                     o += (uint64_t)x.w * x.h;
                     g->max_tile_px = std::max<uint64_t>(g->max_tile_px, (uint64_t)x.w * x.h);
                 }
@@ -1456,8 +1468,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             HIP_TRY(hipMalloc((void**)&g->d_unpack, td.size() * sizeof(TileDesc)));
             HIP_TRY(hipMemcpy(g->d_unpack, td.data(), td.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
         } else {
-            g->send24.assign(inflight, nullptr);
-            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->send24[j], g->rbytes));
+            g->sendbuf.assign(inflight, nullptr);
+            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->sendbuf[j], g->cap * 4));
         }
     }
     if (world > 1) {
@@ -1469,6 +1481,77 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     }
     *out = g.release();
     return MIRT_OK;
+}
+
+// The frame's hit rectangle [x0, x1) x [y0, y1): the pixels whose ray can meet the object.
+// A ray that meets a triangle passes through a root child's box, so its (s, t) lies in that
+// child's frustum rectangle (frustum_args: conservative, the block pre-test relies on it);
+// pixel i's s is (float)(sB - sA i), non-increasing in i, and likewise t in j.  Frames
+// without the pre-test (several objects, culling off) use the whole screen.
+static void hit_rect(const FrameRec& rec, uint32_t W, uint32_t H, uint32_t out[4]) {
+    out[0] = 0;
+    out[1] = 0;
+    out[2] = W;
+    out[3] = H;
+    const FrustumArgs& fr = rec.fr;
+    if (!fr.on) return;
+    float slo = INFINITY, shi = -INFINITY, tlo = INFINITY, thi = -INFINITY;
+    for (int c = 0; c < 8; ++c) {
+        if (!(fr.rect[c][0] <= fr.rect[c][1]) || !(fr.rect[c][2] <= fr.rect[c][3])) continue;  // empty
+        slo = std::min(slo, fr.rect[c][0]);
+        shi = std::max(shi, fr.rect[c][1]);
+        tlo = std::min(tlo, fr.rect[c][2]);
+        thi = std::max(thi, fr.rect[c][3]);
+    }
+    if (!(slo <= shi)) {  // no child can be met: nothing to send
+        out[2] = out[0];
+        out[3] = out[1];
+        return;
+    }
+    // first and last index whose value v(i) = (float)(B - A i) lies in [lo, hi] (v non-increasing)
+    auto span = [](double A, double B, float lo, float hi, uint32_t n, uint32_t& a, uint32_t& b) {
+        auto v = [&](int64_t i) { return (float)(B - A * (double)i); };
+        int64_t i0 = 0, i1 = (int64_t)n - 1;
+        if (std::isfinite(hi) && A > 0) {  // smallest i with v(i) <= hi
+            int64_t k = (int64_t)std::max(0.0, std::min((double)n, std::floor((B - (double)hi) / A))) - 2;
+            k = std::max<int64_t>(k, 0);
+            while (k < (int64_t)n && v(k) > hi) ++k;
+            while (k > 0 && v(k - 1) <= hi) --k;
+            i0 = k;
+        }
+        if (std::isfinite(lo) && A > 0) {  // largest i with v(i) >= lo
+            int64_t k = (int64_t)std::max(-1.0, std::min((double)n - 1, std::ceil((B - (double)lo) / A))) + 2;
+            k = std::min<int64_t>(k, (int64_t)n - 1);
+            while (k >= 0 && v(k) < lo) --k;
+            while (k + 1 < (int64_t)n && v(k + 1) >= lo) ++k;
+            i1 = k;
+        }
+        if (i1 < i0) {
+            a = b = 0;
+            return;
+        }
+        a = (uint32_t)i0;
+        b = (uint32_t)(i1 + 1);
+    };
+    uint32_t x0, x1, y0, y1;
+    span(fr.sA, fr.sB, slo, shi, W, x0, x1);
+    span(fr.tA, fr.tB, tlo, thi, H, y0, y1);
+    if (x0 >= x1 || y0 >= y1) x0 = x1 = y0 = y1 = 0;
+    out[0] = x0;
+    out[1] = y0;
+    out[2] = x1;
+    out[3] = y1;
+}
+
+// Pixels of a tile list inside a hit rectangle (k_pack_rect's transfer size in words).
+static uint64_t rect_pixels(const std::vector<mirt_tile>& tiles, const uint32_t R[4]) {
+    uint64_t n = 0;
+    for (const mirt_tile& t : tiles) {
+        const uint32_t x0 = std::max(t.x, R[0]), x1 = std::min(t.x + t.w, R[2]);
+        const uint32_t y0 = std::max(t.y, R[1]), y1 = std::min(t.y + t.h, R[3]);
+        if (x1 > x0 && y1 > y0) n += (uint64_t)(x1 - x0) * (y1 - y0);
+    }
+    return n;
 }
 
 // Launch the open batch on its slot's stream: trace, then (tiled) the gather of every frame
@@ -1491,29 +1574,34 @@ static int group_flush(mirt_group* g) {
         return r;
     }
     if (g->tiled) {
-        // every frame's rgbv tiles -> the transfer form (the root packs into its own region)
-        PackJobs jobs{};
+        // every frame's tiles inside its hit rectangle -> the transfer buffer (the root packs
+        // into its own region); every rank derives the same rectangles, hence the same sizes
+        RectJobs jobs{};
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t j = g->bj[i];
+            hit_rect(g->slots[bs]->h_frames[i], g->W, g->H, jobs.rect[i]);
             jobs.src[i] = g->packed[j];
-            jobs.dst[i] = is_root ? g->gathered[j] + (uint64_t)g->root * g->rbytes : g->send24[j];
+            jobs.dst[i] = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->sendbuf[j];
         }
-        HIP_TRY(launch_pack24(jobs, n, tiles_pixels(g->mine), g->cap, s));
+        HIP_TRY(launch_pack_rect(g->d_mine, (uint32_t)g->mine.size(), jobs, n, s));
         if (g->world > 1) {
             const Rccl& R = rccl();
             HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
             HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
-            const size_t bytes = g->rbytes;
             RCCL_TRY(R.group_start());
             for (uint32_t i = 0; i < n; ++i) {
                 const uint32_t j = g->bj[i];
                 if (is_root) {
-                    for (int q = 0; q < g->world; ++q)
-                        if (q != g->root)
-                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->rbytes, bytes, ncclUint8, q, g->comm,
+                    for (int q = 0; q < g->world; ++q) {
+                        const uint64_t words = rect_pixels(g->plans[(size_t)q], jobs.rect[i]);
+                        if (q != g->root && words)
+                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, words * 4, ncclUint8, q, g->comm,
                                             g->comm_stream));
+                    }
                 } else {
-                    RCCL_TRY(R.send(g->send24[j], bytes, ncclUint8, g->root, g->comm, g->comm_stream));
+                    const uint64_t words = rect_pixels(g->mine, jobs.rect[i]);
+                    if (words)
+                        RCCL_TRY(R.send(g->sendbuf[j], words * 4, ncclUint8, g->root, g->comm, g->comm_stream));
                 }
             }
             RCCL_TRY(R.group_end());
@@ -1522,12 +1610,11 @@ static int group_flush(mirt_group* g) {
         }
         HT(4);
         if (is_root && !g->skip_unpack) {
-            UnpackJobs uj{};
             for (uint32_t i = 0; i < n; ++i) {
-                uj.src[i] = g->gathered[g->bj[i]];
-                uj.dst[i] = g->fb[g->bj[i]];
+                jobs.src[i] = g->gathered[g->bj[i]];
+                jobs.out[i] = g->fb[g->bj[i]];
             }
-            HIP_TRY(launch_unpack24(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, uj, n, g->cap, s));
+            HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->cap, jobs, n, s));
         }
     }
     HT(5);

@@ -95,18 +95,12 @@ struct FrameArgs {
 
 struct TileDesc {
     uint32_t x, y, w, h;
-    uint64_t out_off;      // first packed pixel of this tile (k_unpack24: within its region)
-    uint32_t region;       // k_unpack24: the rank region holding the tile
-    uint32_t pad;
+    uint64_t out_off;      // first packed pixel of this tile
+    uint32_t region;       // k_unpack_rect: the rank region holding the tile
+    uint32_t pad;          // k_unpack_rect: index of that region's first tile
 };
 
-// The transfer form of a rank's packed tiles (mirt_group, world > 1): per region of `cap`
-// pixels, 3 colour bytes per pixel (r, g, b, as the framebuffer's rgb8) and then one
-// valid bit per pixel — 3.125 B per pixel instead of the 4 B rgbv word.
-__host__ __device__ inline uint64_t rgb24_region_bytes(uint64_t cap) {
-    return ((cap * 3 + 15) & ~15ull) + (((cap + 7) / 8 + 15) & ~15ull);
-}
-__host__ __device__ inline uint64_t rgb24_valid_offset(uint64_t cap) { return (cap * 3 + 15) & ~15ull; }
+
 
 // One 8x8 pixel block of one tile: the primary kernel's work item.  Built on the host
 // per tile list (cached while the list does not change) and stored shard-major (entry
@@ -254,17 +248,16 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
-struct PackJobs {  // k_pack24: per frame of a batch, its rgbv plane and its transfer region
-    const uint32_t* src[kMaxFrames];
-    uint8_t* dst[kMaxFrames];
+struct RectJobs {  // k_pack_rect / k_unpack_rect: per frame of a batch
+    const uint32_t* src[kMaxFrames];  // pack: the rgbv plane; unpack: the gathered regions
+    uint32_t* dst[kMaxFrames];        // pack: the transfer buffer
+    OutPlanes out[kMaxFrames];        // unpack: the framebuffer
+    uint32_t rect[kMaxFrames][4];     // hit rectangle x0, y0, x1, y1 (half-open)
 };
-hipError_t launch_pack24(const PackJobs& jobs, uint32_t nframes, uint64_t npix, uint64_t cap, hipStream_t s);
-struct UnpackJobs {  // k_unpack24: per frame of a batch, its gathered regions and framebuffer
-    const uint8_t* src[kMaxFrames];
-    OutPlanes dst[kMaxFrames];
-};
-hipError_t launch_unpack24(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H,
-                           const UnpackJobs& jobs, uint32_t nframes, uint64_t cap, hipStream_t s);
+hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
+                            hipStream_t s);
+hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, uint64_t cap,
+                              const RectJobs& jobs, uint32_t nframes, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);
 

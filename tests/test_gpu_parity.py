@@ -502,11 +502,19 @@ def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight, batch
     cams = [c, rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.7, 0.3, 0.0])), c.forward, c.fov)]
     muts = [rt.EnvMutables(base.objects, base.lights, cm) for cm in cams]
     muts.append(rt.EnvMutables(base.objects, base.lights[:2], cams[1]))  # fewer lights
+    c0 = np.array([1.0, 1.0, -1.0])  # suzanne's position
+    muts.append(rt.EnvMutables(base.objects, base.lights,  # turned away: an empty hit rectangle
+                               rt.Camera.new(c.pos, tuple(-np.asarray(c.forward)), c.fov)))
+    muts.append(rt.EnvMutables(base.objects, base.lights,  # object cut by the screen edge
+                               rt.Camera.new(tuple(c0 + [3.0, 0.5, 3.0]), (-0.2, -0.1, -1.0), 0.9)))
+    muts.append(rt.EnvMutables(base.objects, base.lights,  # camera inside the bounding box
+                               rt.Camera.new(tuple(c0 + [0.0, 0.0, 0.1]), (0.0, 0.0, -1.0), 1.2)))
     frames = [m.to_frame() for m in muts]
     refs = [rt.draw(env, W, H, m) for m in muts]
+    assert refs[3].valid.sum() == 0 and 0 < refs[4].valid.sum() and 0 < refs[5].valid.sum()
     try:
         g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=inflight, tile_h=tile_h, batch=batch)
-        order = [0, 1, 1, 0, 1, 0, 0, 1, 2, 0, 1, 1, 0, 2, 1, 0]
+        order = [0, 1, 4, 0, 3, 5, 0, 1, 2, 0, 1, 4, 5, 2, 3, 0, 4, 5, 1, 4, 0, 3]
         for q in order:
             g.render(frames[q])
         g.flush()
@@ -516,6 +524,26 @@ def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight, batch
             q = order[k]
             assert np.array_equal(got.valid.cpu().numpy(), refs[q].valid), f"frame {k} valid differs"
             assert np.array_equal(got.rgb8.cpu().numpy(), refs[q].rgb8), f"frame {k} rgb8 differs"
+        g.close()
+    finally:
+        ctx.set_grid()
+
+
+def test_group_batch_arguments(ctx):
+    """mirt_group_set_batch: 1..min(8, inflight) frames per launch, before the first frame."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib as L
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    env = rt.Environment.from_file(os.path.join(GOLDEN, "example", "scene.json"), ctx)
+    try:
+        g = NativeFrameGroup(ctx, 64, 48, 0, 1, None, inflight=4)
+        lib = L.lib()
+        assert lib.mirt_group_set_batch(g._h, 0) == L.MIRT_E_INVALID
+        assert lib.mirt_group_set_batch(g._h, 5) == L.MIRT_E_INVALID  # more than in flight
+        assert lib.mirt_group_set_batch(g._h, 4) == L.MIRT_OK
+        g.render(env.mutable().to_frame())
+        assert lib.mirt_group_set_batch(g._h, 2) == L.MIRT_E_INVALID  # after the first frame
+        g.flush()
         g.close()
     finally:
         ctx.set_grid()
