@@ -132,6 +132,8 @@ SIGNATURES = {
     "mirt_group_destroy": (None, [_P]),
     "mirt_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
                                   C.c_uint32]),
+    "mirt_group_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
+                                        C.c_uint32]),
     "mirt_stream_destroy": (C.c_int, [_P, _P]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),

@@ -1259,16 +1259,40 @@ uint32_t deal_skew(uint32_t world) {
 }
 
 // tile_h == 0: full-height column strips (contiguous in the column-major framebuffer).
+// The frame group's deal weights rank 0 down: the root also unpacks every frame (~1/32 of a
+// whole frame's trace time, measured: tools/rehearsal_table.sh), so of every L = a + b (N-1)
+// consecutive deal slots it takes a = b - 1 and every other rank b = round(32 / N) (N = 8:
+// 3 and 4 of 31).  Slots are interleaved by stride scheduling (smallest (2 count + 1) /
+// weight first, ties to the lower rank).
+void deal_pattern(uint32_t world, bool weighted, std::vector<uint32_t>& P) {
+    P.clear();
+    const uint32_t b = weighted ? std::max<uint32_t>(1, (32 + world / 2) / world) : 1;
+    const uint32_t a = b >= 2 ? b - 1 : b;
+    std::vector<uint64_t> w(world, b), cnt(world, 0);
+    w[0] = a;
+    const uint64_t L = a + (uint64_t)b * (world - 1);
+    for (uint64_t p = 0; p < L; ++p) {
+        uint32_t best = 0;
+        for (uint32_t q = 1; q < world; ++q)
+            if ((2 * cnt[q] + 1) * w[best] < (2 * cnt[best] + 1) * w[q]) best = q;
+        ++cnt[best];
+        P.push_back(best);
+    }
+}
+
 void plan_rank_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
-                     std::vector<mirt_tile>& out) {
+                     std::vector<mirt_tile>& out, bool weighted = false) {
     out.clear();
     const uint32_t th = tile_h ? tile_h : H;
     const uint32_t cols = (W + tile - 1) / tile;
-    const uint32_t s = deal_skew(world);
+    std::vector<uint32_t> P;
+    deal_pattern(std::max<uint32_t>(world, 1), weighted && world > 1, P);
+    const uint64_t L = P.size();
+    const uint32_t s = deal_skew((uint32_t)L);  // == deal_skew(world) unweighted (L == world)
     uint64_t k = 0;
     for (uint32_t y = 0; y < H; y += th)
         for (uint32_t x = 0; x < W; x += tile, ++k)
-            if (world <= 1 || ((k % cols) + (uint64_t)s * (k / cols)) % world == rank)
+            if (world <= 1 || P[((k % cols) + (uint64_t)s * (k / cols)) % L] == rank)
                 out.push_back(mirt_tile{x, y, std::min(tile, W - x), std::min(th, H - y)});
 }
 
@@ -1330,6 +1354,18 @@ int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint
     if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
     std::vector<mirt_tile> t;
     plan_rank_tiles(W, H, tile, tile_h, world, rank, t);
+    if (out) {
+        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
+        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
+    }
+    return (int)t.size();
+}
+
+int mirt_group_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                          mirt_tile* out, uint32_t cap) {
+    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
+    std::vector<mirt_tile> t;
+    plan_rank_tiles(W, H, tile, tile_h, world, rank, t, true);
     if (out) {
         if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
         memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
@@ -1404,16 +1440,19 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->plan_world = plan_world;
     g->skip_unpack = plan_world != world && getenv("MIRT_GROUP_REHEARSE_NO_UNPACK");
     if (g->tiled) {
-        plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)rank, g->mine);
+        // rehearsal diagnostic: MIRT_GROUP_REHEARSE_RANK=q traces rank q's share instead
+        const char* rr = plan_world != world ? getenv("MIRT_GROUP_REHEARSE_RANK") : nullptr;
+        const uint32_t share = rr ? (uint32_t)std::min(std::max(atoi(rr), 0), plan_world - 1) : (uint32_t)rank;
+        plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, share, g->mine, true);
         for (int r = 0; r < plan_world; ++r) {
             std::vector<mirt_tile> t;
-            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t);
+            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t, true);
             g->cap = std::max(g->cap, tiles_pixels(t));
         }
         if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
         g->plans.resize((size_t)plan_world);
         for (int r = 0; r < plan_world; ++r)
-            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, g->plans[(size_t)r]);
+            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, g->plans[(size_t)r], true);
     } else {
         g->mine.push_back(mirt_tile{0, 0, W, H});
         g->cap = (uint64_t)W * H;

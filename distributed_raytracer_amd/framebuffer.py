@@ -369,6 +369,17 @@ class FrameSharder:
         return self.bufs[(self._k - 1) % self._nb] if self.world > 1 else None
 
 
+def plan_group_tiles(W: int, H: int, tile: int, world: int, rank: int, tile_h: Optional[int] = None) -> List[TileT]:
+    """The deal mirt_group uses (mirt_group_plan_tiles): rank 0, which also unpacks every
+    frame, is weighted down (N = 8: 3 of every 31 deal slots, the others 4)."""
+    th = tile if tile_h is None else tile_h
+    n = L.lib().mirt_group_plan_tiles(W, H, tile, th, world, rank, None, 0)
+    L.check(min(n, 0))
+    arr = (L.Tile * max(n, 1))()
+    L.check(min(L.lib().mirt_group_plan_tiles(W, H, tile, th, world, rank, C.cast(arr, C.c_void_p), n), 0))
+    return [(t.x, t.y, t.w, t.h) for t in arr[:n]]
+
+
 def plan_rank_tiles_native(W: int, H: int, tile: int, world: int, rank: int, tile_h: Optional[int] = None) -> List[TileT]:
     """The C++ tile deal of mirt_group (mirt_plan_tiles); equals assign(plan_tiles(...))."""
     th = tile if tile_h is None else tile_h
@@ -402,7 +413,7 @@ class NativeFrameGroup:
         tile = (tile or 0) if world == 1 else int(tile or 8)
         th = tile if tile_h is None else int(tile_h)  # 0: full-height strips
         self.tiles_all = [(0, 0, W, H)] if tile == 0 else plan_tiles(W, H, tile, th)
-        self.mine = [(0, 0, W, H)] if tile == 0 else plan_rank_tiles_native(W, H, tile, world, rank, th)
+        self.mine = [(0, 0, W, H)] if tile == 0 else plan_group_tiles(W, H, tile, world, rank, th)
         if self.F > 1:
             # frames in flight share the chip: at most wg_factor * CUs / F workgroups per frame
             # (2 per CU can be resident; factor 4 = twice what fits)

@@ -303,6 +303,11 @@ int mirt_group_set_batch(mirt_group *g, uint32_t frames_per_launch);
 int mirt_trace_frame(mirt_group *group, const mirt_frame *frame, uint64_t *index);
 int mirt_group_wait(mirt_group *group, void *stream);
 void mirt_group_destroy(mirt_group *group);
+/* The deal mirt_group uses (world > 1): as mirt_plan_tiles, with rank 0 (which also unpacks
+ * every frame) taking b - 1 of every L = b N - 1 deal slots and the other ranks b each,
+ * b = round(32 / N) (N = 8: 3 and 4 of 31). */
+int mirt_group_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                          mirt_tile *out, uint32_t cap);
 int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
                     mirt_tile *out, uint32_t cap);
 

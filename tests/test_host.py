@@ -212,3 +212,20 @@ def test_native_tile_deal_equals_python():
         for world in (1, 2, 3, 4, 6, 8):
             for r in range(world):
                 assert plan_rank_tiles_native(W, H, t, world, r, th) == assign(tiles, world, r), (W, H, t, th, world, r)
+
+
+def test_group_deal_weights_the_root_down():
+    """mirt_group_plan_tiles: every tile exactly once over the ranks; rank 0 (which also
+    unpacks every frame) holds (b - 1) / (b N - 1) of the deal slots, the others b / (b N - 1),
+    b = round(32 / N); world 1 is the whole tile list."""
+    from distributed_raytracer_amd.framebuffer import plan_group_tiles, plan_tiles
+    for W, H, t, th in ((1920, 1080, 8, 0), (1920, 1080, 32, 32), (320, 240, 16, 0), (7, 5, 3, 3)):
+        tiles = plan_tiles(W, H, t, th)
+        assert plan_group_tiles(W, H, t, 1, 0, th) == tiles
+        for world in (2, 3, 4, 8):
+            parts = [plan_group_tiles(W, H, t, world, r, th) for r in range(world)]
+            assert sorted(x for p in parts for x in p) == sorted(tiles), (W, H, t, th, world)
+    b = 4  # N = 8
+    strips = [plan_group_tiles(1920, 1080, 8, 8, r, 0) for r in range(8)]
+    n = [len(p) for p in strips]  # 240 strips, 31-slot pattern
+    assert abs(n[0] / 240 - (b - 1) / 31) < 0.02 and all(abs(k / 240 - b / 31) < 0.02 for k in n[1:])
