@@ -80,7 +80,13 @@ def parse():
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes / fp64 flops of the dominant kernel from rocprofv3 --pmc passes (profiles/)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    # a short run (--steps K) keeps the pipeline shallow: the timed region ends with a drain
+    # of up to F frames, so F stays within K / 8 unless set explicitly
+    if "--inflight" not in sys.argv and "MIRT_INFLIGHT" not in os.environ:
+        a.inflight = max(2, min(a.inflight, a.steps // 8))
+    a.batch = max(1, min(a.batch, a.inflight))
+    return a
 
 
 def workload_name(a, W: int, H: int, tris: int, nl: int) -> str:
