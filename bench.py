@@ -3,21 +3,27 @@
 A "step" is one full frame of tracer.Trace semantics over example/scene.json
 (BASELINE.json configs[1]): primary ray per pixel, one shadow ray per light per hit
 (3 lights), Phong, uint8 packing — everything worker/sequential's draw loop does per
-frame.  Inputs (mesh, frame params) are resident on the GPU before timing; outputs stay
-in HBM.  With N GPUs (torchrun, one process per GPU) the same frame is split into
-interleaved 32x32 tiles and the packed tiles are gathered to rank 0 over RCCL and
-unpacked into the framebuffer inside the timed region (strong scaling: total work is
-one frame whatever N is).
+frame — and, as BASELINE.md §3 defines ms/frame, the D2H copy of the assembled rgb8 +
+valid framebuffer into pinned host memory (mirt_group_set_host_output; --no-d2h leaves
+outputs in HBM).  Inputs (mesh, frame params) are resident on the GPU before timing.
+With N GPUs (torchrun, one process per GPU) the same frame is split into interleaved
+8-px strips; every rank's strips inside the frame's hit rectangle are gathered to rank 0
+over RCCL and unpacked into the framebuffer inside the timed region (strong scaling:
+total work is one frame whatever N is).
 
-Frames are pipelined (--inflight F, default 4): frame k runs on stream k % F with its own
-buffers, so frame k+1's kernel starts while frame k's last workgroups finish, as the
-reference master keeps several frames in flight.  ms_per_step is therefore the frame
-INTERVAL at steady state (throughput); frame_latency_ms is one frame rendered alone
-(render, gather, unpack, host sync) with the same launch shape.
+Frames are pipelined (--inflight F frames in flight, --batch B frames per k_trace
+launch): frame k+1's kernel starts while frame k's last workgroups finish, as the
+reference master keeps several frames in flight (master/main.go:264-266).  ms_per_step is
+the wall time of the K timed frames / K (from an empty pipeline to the last frame in host
+memory); device_ms_per_frame the same frames without the D2H; frame_latency_ms one frame
+rendered alone (render, [gather, unpack,] D2H, host sync), median of up to 20.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).  Fields beyond the
-contract: frames_in_flight, frame_latency_ms, primary_mrays_s, rays_per_frame, hits,
-ms_kernels, parity, roofline_fp64_valu, cpu_baseline.
+contract: frames_in_flight, frames_per_launch, device_ms_per_frame, frame_latency_ms,
+primary_mrays_s, rays_per_frame, ms_kernels, launches (k_trace launches per region, in
+order: warmup, timed, device-only, profiled, latency — the key to the committed rocprofv3
+trace), parity, roofs (physical roofs from the committed PMC passes of this command),
+cpu_baseline.
 """
 from __future__ import annotations
 
@@ -37,6 +43,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"] if os.pa
 BYTES_PER_TRI_TEST = 72  # fp64 P1, E1, E2 read per ray-triangle test
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec, vector FP64 (FMA = 2 flops)
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions per second: 1024 SIMDs, 4 cycles each
 HOST_CORES = 16  # the GPU box's CPU share for one GPU (os.cpu_count() shows the whole machine)
 
 
@@ -53,21 +60,17 @@ def parse():
     ap.add_argument("--scene", default=SCENE)
     ap.add_argument("--bounces", type=int, default=0,
                     help="configs[4] reflection EXTENSION: bounces per primary hit (0 = the reference)")
-    # defaults measured on one MI355X (tools/batch_sweep.sh): the whole 1080p frame runs
-    # best as 8 in flight, 2 per launch; a rank's 1/N share needs more frames per launch
-    # (each workgroup then owns enough blocks to hide its heaviest block's chain)
-    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIRT_BATCH", "4" if multi else "2")),
-                    help="frames per k_trace launch (native sharder; 1..min(8, inflight))")
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "8")),
-                    help="frames in flight (one stream and one set of buffers each; frame k+1's kernel "
-                         "starts while frame k's last workgroups finish)")
+    # None = the measured default for the run (see resolve_shape)
+    ap.add_argument("--batch", type=int, default=None, help="frames per k_trace launch (1..min(8, inflight))")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="frames in flight (one stream and one set of buffers each)")
     ap.add_argument("--grid", default="",
                     help="frame-kernel launch shape 'MIN_BLOCKS_PER_WG,MAX_WORKGROUPS' (mirt_set_grid; "
-                         "default: FrameSharder's choice for the frames in flight)")
+                         "default: NativeFrameGroup's choice for the frames in flight)")
     ap.add_argument("--sharder", choices=("native", "torch"), default="native",
                     help="per-frame driver: native (libmirt mirt_trace_frame, RCCL called from C) or torch "
                          "(framebuffer.FrameSharder over torch.distributed)")
+    ap.add_argument("--no-d2h", action="store_true", help="leave the assembled frames in HBM (no host output)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
@@ -78,15 +81,30 @@ def parse():
                     help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
-                    help="per-launch HBM bytes / fp64 flops of the dominant kernel from rocprofv3 --pmc passes (profiles/)")
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02_roofline.json"),
+                    help="per-launch counters of the dominant kernel from rocprofv3 passes of this command "
+                         "(tools/roofline.py writes it; used only when its launch shape equals this run's)")
     a = ap.parse_args()
-    # a short run (--steps K) keeps the pipeline shallow: the timed region ends with a drain
-    # of up to F frames, so F stays within K / 8 unless set explicitly
-    if "--inflight" not in sys.argv and "MIRT_INFLIGHT" not in os.environ:
-        a.inflight = max(2, min(a.inflight, a.steps // 8))
-    a.batch = max(1, min(a.batch, a.inflight))
+    resolve_shape(a)
     return a
+
+
+def resolve_shape(a) -> None:
+    """Frames in flight F and frames per launch B.  Measured on one MI355X (profiles/
+    r02_shape_sweep.txt): the whole 1080p frame runs best as 8 in flight x 2 per launch
+    over long runs; a rank's 1/N share needs more frames per launch (each workgroup then
+    owns enough blocks to hide its heaviest block's chain).  A short run keeps at least two
+    launches' worth of batch slots so launches overlap."""
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "8"))
+    B = a.batch if a.batch is not None else int(os.environ.get("MIRT_BATCH", "4" if multi else "2"))
+    F = max(1, min(F, 16))
+    if a.split_kernels or a.bounces:
+        B = 1  # one frame per launch on those paths
+    B = max(1, min(B, F, 8))
+    if a.batch is None and F // B < 2 and F >= 2:
+        B = max(1, F // 2)
+    a.inflight, a.batch = F, B
 
 
 def workload_name(a, W: int, H: int, tris: int, nl: int) -> str:
@@ -101,16 +119,32 @@ def workload_name(a, W: int, H: int, tris: int, nl: int) -> str:
     return name
 
 
+def host_threads() -> int:
+    """CPUs this process may run on (the box's share; os.cpu_count() shows the machine)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
-    """SURVEY.md §8(d) CPU baselines, timed on this host: (i) the oracle's faithful variant
-    (rtreego-style R-tree, 1 thread, fp64, worker/sequential's serial i/j loop) over one
-    full frame — the reported value; (ii) the same code on the box's host cores
-    (column-interleaved threads)."""
+    """SURVEY.md §8(d) / BASELINE.md §2 CPU baselines, timed on this host:
+    (i) the oracle's faithful variant (rtreego-style R-tree, 1 thread, fp64,
+        worker/sequential's serial i/j loop) over one full frame — the reported value;
+    (ii) the same code on all the host cores this process is allotted (the box's share for
+        one GPU, 16; column-interleaved threads) — os.cpu_count() (`nproc`) shows the whole,
+        shared machine and is reported, not used;
+    (iii) brute force (every triangle, no culling), 1 thread, on every 64th column of the
+        frame (a bounded sample), scaled to the full frame."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
-    orc = Oracle(load_scene(scene_path), use_rtree=True)
+    sc = load_scene(scene_path)
+    orc = Oracle(sc, use_rtree=True)
     out = None
-    for threads in (1, HOST_CORES):
+    # the box allots HOST_CORES CPUs per GPU; os.cpu_count() shows the whole, shared machine,
+    # so the all-cores variant runs on the allotted cores (sched_getaffinity if smaller)
+    allc = max(1, min(host_threads(), HOST_CORES))
+    for threads in sorted({1, allc}):
         t0 = time.perf_counter()
         r = orc.frame(W, H, nthreads=threads)
         dt = time.perf_counter() - t0
@@ -122,24 +156,48 @@ def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
         if out is None:
             out = v
         else:
-            out["all_cores"] = {k: v[k] for k in ("value", "cores", "ms_per_frame")}
+            out[f"threads_{threads}"] = {k: v[k] for k in ("value", "cores", "ms_per_frame")}
+    cols = list(range(0, W, 64))
+    brute = Oracle(sc, use_rtree=False)
+    t0 = time.perf_counter()
+    r = brute.trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=1)
+    dt = time.perf_counter() - t0
+    rays = r["stats"]["primary_rays"] + r["stats"]["shadow_rays"]
+    out["brute_force_1_thread"] = {
+        "value": round(rays / dt / 1e6, 4), "cores": 1,
+        "ms_per_frame": round(dt * 1e3 * W / len(cols), 1),
+        "sample": f"every 64th column ({len(cols)} x {H} px, {rays} rays) in {dt:.2f} s, scaled x{W / len(cols):.0f}"}
     out["nproc"] = os.cpu_count()
+    out["affinity_cpus"] = host_threads()
     return out
 
 
 def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int,
                  bounces: int = 0) -> dict:
-    """Parity gate of the timed frame: a 1/16 subsample — every 16th
-    column — against the oracle, valid mask and rgb8 bit-exact."""
+    """Parity gate of the timed frames: EVERY pixel of the last timed
+    frame against the oracle (R-tree restatement, 16 threads), valid mask and rgb8
+    bit-exact; with the D2H on, the frame checked is the host copy."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
-    cols = list(range(5, W, 16))
     orc = Oracle(load_scene(scene_path), use_rtree=True)
     orc.set_bounces(bounces)
-    ref = orc.trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=HOST_CORES)
-    sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
-    ok = bool(np.array_equal(fb_valid[sub], ref["valid"]) and np.array_equal(fb_rgb8[sub], ref["rgb8"]))
-    return {"columns_checked": len(cols), "bit_exact": ok, "hits": int(fb_valid.sum())}
+    ref = orc.frame(W, H, nthreads=HOST_CORES)
+    ok = bool(np.array_equal(fb_valid, ref["valid"]) and np.array_equal(fb_rgb8, ref["rgb8"]))
+    return {"pixels_checked": W * H, "bit_exact": ok, "hits": int(fb_valid.sum())}
+
+
+def load_profile(path: str, shape: dict):
+    """The committed rocprofv3 summary of THIS command (tools/roofline.py), if its launch
+    shape matches; counters from another shape are never mixed in."""
+    if not os.path.exists(path):
+        return None
+    try:
+        pj = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if any(pj.get("shape", {}).get(k) != v for k, v in shape.items()):
+        return None
+    return pj
 
 
 def main():
@@ -178,59 +236,102 @@ def main():
     frame = dataclasses.replace(env.mutable(), max_bounces=a.bounces).to_frame()
     tris = sum(len(m.face_v) for m in env.meshes)
     nl = len(env.mutable().lights)
-    # native: the per-frame trace + RCCL gather + unpack in libmirt (mirt_trace_frame), one C
-    # call per frame; torch: the same sequence through torch.distributed (FrameSharder), used
-    # for the gloo rehearsal (RCCL cannot put two ranks on one GPU) and as a fallback
-    sharder = a.sharder if not (world > 1 and backend != "nccl") else "torch"
-    sh = None
-    if sharder == "native":
-        try:
-            sh = NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
-                                  tile_h=a.tile_h, batch=a.batch)
-        except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
-            print(f"native frame group unavailable ({e}); using the torch.distributed sharder", file=sys.stderr)
-            sharder = f"torch (native failed: {e})"
-    if sh is None:
-        # the torch.distributed path was tuned at 4 in flight (one frame per launch)
-        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=min(a.inflight, 4), tile_h=a.tile_h)
-    if a.grid:
-        ctx.set_grid(*(int(x) for x in a.grid.split(",")))
     dev = torch.device("cuda", local)
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[local]) if backend == "nccl" else dist.barrier()
 
-    # One stream for every frame: frames are serialised on the GPU (no two frames in
-    # flight writing the same framebuffer); the host still enqueues ahead of the GPU.
-    # The throughput region runs without profiling (its HIP events between the kernels cost
-    # ~10 % of a frame); the same frames are then traced again with profiling on, and the
-    # per-kernel HIP-event times and device counters (rays, tests) come from that region.
+    # native: the per-frame trace + RCCL gather + unpack (+ D2H) in libmirt (mirt_trace_frame),
+    # one C call per frame; torch: the same sequence through torch.distributed (FrameSharder),
+    # used for the gloo rehearsal (RCCL cannot put two ranks on one GPU).  The choice is
+    # collective: if any rank cannot create the native group, every rank uses torch.
+    sharder = a.sharder if not (world > 1 and backend != "nccl") else "torch"
+    d2h = not a.no_d2h and sharder == "native"
+
+    def native_group(host_output: bool):
+        return NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
+                                tile_h=a.tile_h, batch=a.batch, host_output=host_output and rank == 0)
+
+    sh = sh_dev = None
+    err = ""
+    if sharder == "native":
+        try:
+            sh = native_group(d2h)
+            sh_dev = native_group(False) if d2h else None
+        except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
+            err = str(e)
+    if world > 1 and sharder == "native":
+        ok = torch.tensor([0.0 if sh is None else 1.0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() < 1.0:
+            sh = sh_dev = None
+            err = err or "another rank could not create its native group"
+    if sharder == "native" and sh is None:
+        print(f"native frame group unavailable ({err}); using the torch.distributed sharder", file=sys.stderr)
+        sharder, d2h = f"torch (native failed: {err})", False
+    if sh is None:
+        # the torch.distributed path was tuned at 4 in flight (one frame per launch)
+        sh = FrameSharder(ctx, W, H, rank, world, a.tile, inflight=min(a.inflight, 4), tile_h=a.tile_h)
+    if a.grid:
+        ctx.set_grid(*(int(x) for x in a.grid.split(",")))
+
+    # launches per region (the key that partitions the rocprofv3 kernel trace of this command)
+    launches = {}
+
+    def count(region, n_frames, batched=True):
+        per = a.batch if (batched and hasattr(sh, "B")) else 1
+        launches[region] = launches.get(region, 0) + (n_frames + per - 1) // per
+
     stream = torch.cuda.Stream(dev)
+    host_last = None
     with torch.cuda.stream(stream):
-        for _ in range(a.warmup):
-            sh.render(frame)
-        sh.flush()
+        for g in ([sh] + ([sh_dev] if sh_dev is not None else [])):
+            for _ in range(a.warmup):
+                g.render(frame)
+            g.flush()
+            count("warmup", a.warmup)
         torch.cuda.synchronize(dev)
 
+        # timed region: K frames from an empty pipeline to the last one in host memory
         barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
+        last = None
         for _ in range(a.steps):
-            sh.render(frame)  # N > 1: frame k's gather overlaps frame k+1's tracing
-        sh.flush()            # the last frame's gather + unpack are inside the timed region
+            last = sh.render(frame)  # N > 1: frame k's gather overlaps frame k+1's tracing
+        sh.flush()                   # the last frame's gather + unpack (+ D2H) are inside the timed region
         torch.cuda.synchronize(dev)
         barrier()
         t1 = time.perf_counter()
+        count("timed", a.steps)
+        if d2h and rank == 0:
+            host_last = sh.host_frame(last)  # the D2H'd frame (checked against the oracle below)
 
+        # the same frames without the D2H (device-resident outputs)
+        dev_elapsed = None
+        if sh_dev is not None:
+            barrier()
+            torch.cuda.synchronize(dev)
+            d0 = time.perf_counter()
+            for _ in range(a.steps):
+                sh_dev.render(frame)
+            sh_dev.flush()
+            torch.cuda.synchronize(dev)
+            barrier()
+            dev_elapsed = time.perf_counter() - d0
+            count("device_only", a.steps)
+
+        # profiled region: HIP events around every k_trace launch + device counters
         ctx.profile_enable(True)
         for _ in range(a.steps):
             sh.render(frame)
         sh.flush()
         torch.cuda.synchronize(dev)
         ctx.profile_enable(False)
+        count("profiled", a.steps)
 
-        # single-frame latency: one frame alone (render, gather + unpack, host sync), median
+        # single-frame latency: one frame alone (render, gather + unpack, D2H, host sync), median
         lat = []
         for _ in range(min(a.steps, 20)):
             barrier()
@@ -240,45 +341,42 @@ def main():
             sh.flush()
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - l0)
+        count("latency", min(a.steps, 20), batched=False)
         latency = float(np.median(lat)) if lat else 0.0
     prof = ctx.profile_read()
 
     elapsed = t1 - t0
     pl = max(prof["frames"], 1)  # per-frame device counters (a launch may trace several frames)
-    counts = torch.tensor([elapsed, latency, prof["primary_rays"] / pl, prof["shadow_rays"] / pl, prof["hits"] / pl,
-                           prof["reflection_rays"] / pl], dtype=torch.float64,
+    counts = torch.tensor([elapsed, latency, dev_elapsed or 0.0, prof["primary_rays"] / pl, prof["shadow_rays"] / pl,
+                           prof["hits"] / pl, prof["reflection_rays"] / pl], dtype=torch.float64,
                           device=dev if backend == "nccl" else "cpu")
     if world > 1:
-        tmax = counts[:2].clone()
+        tmax = counts[:3].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        sums = counts[2:].clone()
+        sums = counts[3:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed, latency = (float(x) for x in tmax.tolist())
+        elapsed, latency, dev_elapsed_max = (float(x) for x in tmax.tolist())
+        dev_elapsed = dev_elapsed_max if dev_elapsed is not None else None
         primary, shadow, hits, refl = (float(x) for x in sums.tolist())
     else:
-        primary, shadow, hits, refl = (float(x) for x in counts[2:].tolist())
+        primary, shadow, hits, refl = (float(x) for x in counts[3:].tolist())
 
     if rank == 0:
         steps = a.steps
         ms = elapsed / steps * 1e3
         rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
-        launches = max(prof["launches"], 1)
-        prim_ms = prof["primary_ms_sum"] / launches
+        nlaunch = max(prof["launches"], 1)
+        prim_ms = prof["primary_ms_sum"] / nlaunch
         # the dominant kernel: k_trace (the whole frame, one launch) or, split, k_primary;
         # reflection frames always run split (k_primary, k_shadow, k_reflect)
         one = not a.split_kernels and not a.bounces
         kname = "k_trace" if one else "k_primary"
-        k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / launches
+        k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
         achieved = k_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
-        traffic = fp64_flops = None
-        if os.path.exists(a.traffic_json):
-            try:
-                tj = json.load(open(a.traffic_json))
-                if tj.get("width") == W and tj.get("height") == H and tj.get("gpus", 1) == world:
-                    traffic = tj.get(f"{kname}_hbm_bytes_per_launch")
-                    fp64_flops = tj.get(f"{kname}_fp64_flops_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        shape = {"width": W, "height": H, "gpus": world, "inflight": a.inflight, "batch": a.batch,
+                 "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname}
+        pj = load_profile(a.profile_json, shape)
+        frames_per_launch = pl / nlaunch
         line = {
             "metric": METRIC,
             "value": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
@@ -297,10 +395,12 @@ def main():
             "config": {"workload": workload_name(a, W, H, tris, nl), "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
-                       "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)"},
-            "frames_in_flight": sh.F,
+                       "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)",
+                       "d2h": "rgb8 + valid to pinned host memory inside the timed region" if d2h else "none (HBM)"},
+            "frames_in_flight": getattr(sh, "F", a.inflight),
             "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,
+            "device_ms_per_frame": round(dev_elapsed / steps * 1e3, 4) if dev_elapsed else round(ms, 4),
             "frame_latency_ms": round(latency * 1e3, 4),
             "primary_mrays_s": round(primary / (ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
@@ -309,32 +409,44 @@ def main():
             "bvh_visits_per_frame": {k: int(prof[k] / pl) for k in (
                 "primary_node_visits", "primary_leaf_visits", "shadow_node_visits", "shadow_leaf_visits")},
             "ms_kernels": {("frame_kernel" if one else "primary"): round(prim_ms, 4),
-                           "shadow": round(prof["shadow_ms_sum"] / launches, 4),
-                           "reflect": round(prof["reflect_ms_sum"] / launches, 4),
-                           "frame_device": round(prof["frame_ms_sum"] / launches, 4)},
+                           "shadow": round(prof["shadow_ms_sum"] / nlaunch, 4),
+                           "reflect": round(prof["reflect_ms_sum"] / nlaunch, 4),
+                           "frame_device": round(prof["frame_ms_sum"] / nlaunch, 4)},
+            "launches": launches,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST,
-                         "units_per_launch": int(k_tests),
-                         # with frames in flight a launch shares the chip with its neighbours,
-                         # so per-launch time overstates the cost: the same bytes per frame
-                         # over the steady-state frame interval
-                         "chip_rate_gbs": round(k_tests * launches / pl * BYTES_PER_TRI_TEST / (ms / 1e3) / 1e9, 1),
-                         "note": "algorithmic bytes = 72 B fp64 triangle record x ray-triangle tests actually "
-                                 "performed (device counter); the mesh is LDS-resident so the real bound is fp64 "
-                                 "VALU, see DESIGN.md; kernel time = HIP events on the trace stream over a second "
-                                 "region of the same frames (the throughput region runs without events)"},
-            "roofline_fp64_valu": None if fp64_flops is None else {
-                "bound": "fp64-valu", "kernel": kname, "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFLOPS,
-                "achieved": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12, 3),
-                "frac": round(64 * fp64_flops / (prim_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
-                "flops_per_launch": int(64 * fp64_flops),
-                "note": "SQ_INSTS_VALU_FLOPS_FP64 (counts per wave instruction, FMA = 2) x 64 lanes per launch, "
-                        "from the committed rocprofv3 pass (profiles/), over this run's HIP-event time of the kernel"},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pj["hbm_bytes_per_launch"] if pj else None,
+                         "kind": "algorithmic (north star): 72 B fp64 triangle record x ray-triangle tests performed "
+                                 "(device counter) per launch / mean HIP-event duration of the launch; the mesh is "
+                                 "LDS-resident, so these bytes never touch HBM (physical roofs: `roofs`)",
+                         "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
+                         "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(prim_ms, 4)},
         }
-        if not a.no_parity:
-            fr = sh.frame
-            line["parity"] = parity_check(fr.valid.cpu().numpy(), fr.rgb8.cpu().numpy(), a.scene, W, H, a.bounces)
+        if pj:
+            # physical roofs over the frame interval (counters of this exact command, profiles/)
+            per_frame = lambda x: x / pj["frames_per_launch"]  # noqa: E731
+            iv = ms / 1e3
+            valu = per_frame(pj["sq_insts_valu_per_launch"])
+            line["roofs"] = {
+                "source": os.path.relpath(a.profile_json, ROOT),
+                "frame_interval_ms": round(ms, 4),
+                "valu_issue_frac": round(valu / iv / VALU_ISSUE_PER_S, 4),
+                "valu_insts_per_frame": int(valu),
+                "salu_insts_per_frame": int(per_frame(pj["sq_insts_salu_per_launch"])),
+                "fp64_tflops": round(64 * per_frame(pj["fp64_flops_per_launch"]) / iv / 1e12, 3),
+                "fp64_frac": round(64 * per_frame(pj["fp64_flops_per_launch"]) / iv / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
+                "hbm_bytes_per_frame": int(per_frame(pj["hbm_bytes_per_launch"])),
+                "hbm_frac": round(per_frame(pj["hbm_bytes_per_launch"]) / iv / 1e9 / HBM_PEAK_GBS, 4),
+                "output_bytes_per_frame": W * H * 4,
+            }
+        if not a.no_parity and rank == 0:
+            if host_last is not None:
+                rgb8, valid = host_last
+            else:
+                fr = sh.frame
+                rgb8, valid = fr.rgb8.cpu().numpy(), fr.valid.cpu().numpy()
+            line["parity"] = parity_check(valid, rgb8, a.scene, W, H, a.bounces)
+            line["parity"]["frame"] = "host copy (D2H)" if host_last is not None else "device framebuffer"
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.scene, W, H)
         print(json.dumps(line), flush=True)

@@ -20,6 +20,8 @@ MIRT_E_NOMEM = -4
 MIRT_E_CAMERA = -5
 MIRT_E_CANCELLED = -6
 MIRT_E_IO = -7
+MIRT_E_TIMEOUT = -8
+MIRT_E_PEER = -9
 MIRT_MAX_OBJECTS = 16
 MIRT_MAX_LIGHTS = 16
 MIRT_OPT_NO_PREFILTER = 1
@@ -135,6 +137,13 @@ SIGNATURES = {
     "mirt_group_plan_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
                                         C.c_uint32]),
     "mirt_stream_destroy": (C.c_int, [_P, _P]),
+    "mirt_group_set_timeout": (C.c_int, [_P, C.c_uint32]),
+    "mirt_group_failed_ranks": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "mirt_group_exclude": (C.c_int, [_P, C.c_uint64, _P]),
+    "mirt_group_emulate": (C.c_int, [_P, C.c_uint32]),
+    "mirt_group_emulate_drop": (C.c_int, [_P, C.c_uint64]),
+    "mirt_group_set_host_output": (C.c_int, [_P, C.c_int]),
+    "mirt_group_frame_host": (C.c_int, [_P, C.c_uint64, C.POINTER(Outputs)]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_unpack_tiles_at_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),

@@ -1887,6 +1887,35 @@ __global__ __launch_bounds__(256) void k_pack_rect(const TileDesc* __restrict__ 
             dst[p] = src[(uint64_t)(cx0 - td.x + lx) * td.h + (cy0 - td.y + ly)];
         }
     }
+    // the trailer right after the data: {frame tag, words} (mirt_internal.hpp kTrailerWords)
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const uint64_t total = rect_offset(tiles, 0, ntiles, R);
+        if (threadIdx.x == 0) {
+            jobs.dst[f][total] = jobs.tag[f];
+            jobs.dst[f][total + 1] = (uint32_t)total;
+        }
+    }
+}
+
+// Root, before the unpack: region r of the gathered plane must end with the trailer of
+// this frame at the word count its tiles give inside the hit rectangle.  One wave per
+// (region, frame); writes bad[f][r] (host-visible) for every region.
+__global__ __launch_bounds__(64) void k_check_regions(const TileDesc* __restrict__ tiles,
+                                                      const RegionDesc* __restrict__ regions, uint64_t stride,
+                                                      RectJobs jobs) {
+    const uint32_t r = blockIdx.x, f = blockIdx.z;
+    const RegionDesc rd = regions[r];
+    const uint64_t total = rect_offset(tiles, rd.first, rd.first + rd.count, jobs.rect[f]);
+    if (threadIdx.x == 0) {
+        const uint32_t* t = jobs.src[f] + (uint64_t)r * stride + total;
+        const bool ok = total + kTrailerWords <= stride && t[0] == jobs.tag[f] && t[1] == (uint32_t)total;
+        jobs.bad[f][r] = ok ? 0 : 1;
+    }
+}
+hipError_t launch_check_regions(const TileDesc* tiles, const RegionDesc* regions, uint32_t nregions, uint64_t stride,
+                                const RectJobs& jobs, uint32_t nframes, hipStream_t s) {
+    hipLaunchKernelGGL(k_check_regions, dim3(nregions, 1, nframes), dim3(64), 0, s, tiles, regions, stride, jobs);
+    return hipGetLastError();
 }
 hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
                             hipStream_t s) {

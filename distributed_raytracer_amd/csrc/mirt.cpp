@@ -14,7 +14,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <memory>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -1199,6 +1201,8 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;    // optional (peer exclusion)
+    decltype(&ncclCommShrink) comm_shrink = nullptr;  // optional (peer exclusion without a new id)
 };
 
 Rccl load_rccl() {
@@ -1226,6 +1230,8 @@ Rccl load_rccl() {
     MIRT_RCCL_SYM(group_end, "ncclGroupEnd")
     MIRT_RCCL_SYM(error_string, "ncclGetErrorString")
 #undef MIRT_RCCL_SYM
+    R.comm_abort = (decltype(R.comm_abort))dlsym(h, "ncclCommAbort");
+    R.comm_shrink = (decltype(R.comm_shrink))dlsym(h, "ncclCommShrink");
     R.ok = true;
     return R;
 }
@@ -1308,226 +1314,12 @@ hipError_t stream_with_queue(int cus, hipStream_t* s) {
     return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
 }
 
-}  // namespace
-
-struct mirt_group {
-    mirt_ctx* c = nullptr;
-    int rank = 0, world = 1, root = 0;
-    uint32_t W = 0, H = 0, F = 1;
-    bool tiled = false;               // packed rgbv tiles + unpack (world > 1, or a tiled rehearsal)
-    ncclComm_t comm = nullptr;
-    hipStream_t comm_stream = nullptr;  // every RCCL call, in issue order (the same on every rank)
-    std::vector<hipStream_t> streams;   // frame k runs on streams[k % F]
-    std::vector<hipEvent_t> ev_traced, ev_gathered, ev_done;
-    std::vector<mirt_tile> mine;
-    uint64_t cap = 0;                   // largest rank share (pixels): every rank's gather size
-    std::vector<uint32_t*> packed;      // tiled: my tiles' rgbv plane per frame slot (the trace's output)
-    std::vector<uint32_t*> sendbuf;     // non-root: its transfer form (k_pack_rect) per frame slot
-    std::vector<uint32_t*> gathered;    // root: world regions of cap words in the transfer form per frame slot
-    std::vector<std::vector<mirt_tile>> plans;  // every rank's tiles (the transfer sizes)
-    TileDesc* d_mine = nullptr;         // my tiles with their offsets in my rgbv plane (k_pack_rect)
-    std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
-    TileDesc* d_unpack = nullptr;       // root: every rank's tiles at their gathered offsets
-    uint32_t n_unpack = 0;
-    uint64_t max_tile_px = 0;           // root: largest tile (unpack grid)
-    // one workspace per frame slot: frame k reuses slot k % F after frame k - F on the same
-    // stream, so no slot pool, event query or host wait is on the per-frame path
-    std::vector<std::unique_ptr<Slot>> slots;
-    uint64_t k = 0;                     // frames enqueued
-    int plan_world = 1;                 // ranks of the tile deal (== world except in a rehearsal)
-    bool skip_unpack = false;           // rehearsal diagnostic: a non-root rank's work (trace only)
-    // frames per k_trace launch (mirt_group_set_batch): frames accumulate in the open batch,
-    // which launches when full, when an incompatible frame arrives, or at mirt_group_wait.
-    // Batch b uses batch slot b % FB (its workspace, stream and events), FB = F / B, so the
-    // F framebuffers (frame k: k % F) are never reused before their frame completed.
-    uint32_t B = 1, FB = 1;
-    uint64_t nb = 0;                    // batches launched
-    uint32_t bn = 0;                    // frames in the open batch
-    uint32_t bj[kMaxFrames] = {};       // their frame slots (k % F)
-    uint32_t bbounces = 0;
-};
-
-extern "C" {
-
-int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
-                    mirt_tile* out, uint32_t cap) {
-    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
-    std::vector<mirt_tile> t;
-    plan_rank_tiles(W, H, tile, tile_h, world, rank, t);
-    if (out) {
-        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
-        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
-    }
-    return (int)t.size();
-}
-
-int mirt_group_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
-                          mirt_tile* out, uint32_t cap) {
-    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
-    std::vector<mirt_tile> t;
-    plan_rank_tiles(W, H, tile, tile_h, world, rank, t, true);
-    if (out) {
-        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
-        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
-    }
-    return (int)t.size();
-}
-
-int mirt_group_unique_id(uint8_t* id) {
-    if (!id) return fail(MIRT_E_INVALID, "id is NULL");
-    if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
-    ncclUniqueId u;
-    RCCL_TRY(rccl().get_unique_id(&u));
-    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
-    return MIRT_OK;
-}
-
-void mirt_group_destroy(mirt_group* g) {
-    if (!g) return;
-#ifdef MIRT_HOST_TIMERS
-    fprintf(stderr, "host_timers_us_per_frame wait %.2f record %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
-            g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k);
-#endif
-    (void)hipSetDevice(g->c->device);
-    for (hipStream_t s : g->streams)
-        if (s) (void)hipStreamSynchronize(s);
-    if (g->comm_stream) (void)hipStreamSynchronize(g->comm_stream);
-    if (g->comm) (void)rccl().comm_destroy(g->comm);
-    for (auto& sl : g->slots) slot_free(sl.get());
-    for (uint32_t* p : g->packed)
-        if (p) (void)hipFree(p);
-    for (uint32_t* p : g->gathered)
-        if (p) (void)hipFree(p);
-    for (uint32_t* p : g->sendbuf)
-        if (p) (void)hipFree(p);
-    if (g->d_mine) (void)hipFree(g->d_mine);
-    if (g->d_unpack) (void)hipFree(g->d_unpack);
-    for (auto* v : {&g->ev_traced, &g->ev_gathered, &g->ev_done})
-        for (hipEvent_t e : *v)
-            if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : g->streams)
-        if (s) (void)hipStreamDestroy(s);
-    if (g->comm_stream) (void)hipStreamDestroy(g->comm_stream);
-    delete g;
-}
-
-int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world, uint32_t W, uint32_t H,
-                      uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
-    if (!c || !out) return fail(MIRT_E_INVALID, "NULL context or out");
-    *out = nullptr;
-    if (world < 1 || rank < 0 || rank >= world) return fail(MIRT_E_INVALID, "bad rank / world");
-    if (!W || !H || W > 65535 || H > 65535) return fail(MIRT_E_INVALID, "bad screen size");
-    if (inflight < 1 || inflight > 16) return fail(MIRT_E_INVALID, "inflight must be 1..16");
-    if (world > 1 && !unique_id) return fail(MIRT_E_INVALID, "world > 1 needs the root's unique id");
-    if (world > 1 && tile == 0) return fail(MIRT_E_INVALID, "world > 1 needs a tile size");
-    const bool is_root = rank == 0;
-    if (is_root && !fbs) return fail(MIRT_E_INVALID, "the root needs its framebuffers");
-    HIP_TRY(hipSetDevice(c->device));
-    std::unique_ptr<mirt_group, void (*)(mirt_group*)> g(new mirt_group(), mirt_group_destroy);
-    g->c = c;
-    g->rank = rank;
-    g->world = world;
-    g->W = W;
-    g->H = H;
-    g->F = inflight;
-    g->FB = inflight;  // one frame per launch until mirt_group_set_batch
-    g->tiled = tile > 0;
-    // MIRT_GROUP_REHEARSE=N (diagnostic, world == 1 only): trace rank 0's share of an N-way
-    // deal and unpack all N shares' regions (the others hold stale words), i.e. the root's
-    // per-frame work at N GPUs without the RCCL transfers (tools/native_host_probe.py)
-    const char* reh = getenv("MIRT_GROUP_REHEARSE");
-    const int plan_world = (world == 1 && g->tiled && reh && atoi(reh) > 1) ? atoi(reh) : world;
-    g->plan_world = plan_world;
-    g->skip_unpack = plan_world != world && getenv("MIRT_GROUP_REHEARSE_NO_UNPACK");
-    if (g->tiled) {
-        // rehearsal diagnostic: MIRT_GROUP_REHEARSE_RANK=q traces rank q's share instead
-        const char* rr = plan_world != world ? getenv("MIRT_GROUP_REHEARSE_RANK") : nullptr;
-        const uint32_t share = rr ? (uint32_t)std::min(std::max(atoi(rr), 0), plan_world - 1) : (uint32_t)rank;
-        plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, share, g->mine, true);
-        for (int r = 0; r < plan_world; ++r) {
-            std::vector<mirt_tile> t;
-            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, t, true);
-            g->cap = std::max(g->cap, tiles_pixels(t));
-        }
-        if (g->mine.empty()) return fail(MIRT_E_INVALID, "this rank has no tiles (tile too large for the world size)");
-        g->plans.resize((size_t)plan_world);
-        for (int r = 0; r < plan_world; ++r)
-            plan_rank_tiles(W, H, tile, tile_h, (uint32_t)plan_world, (uint32_t)r, g->plans[(size_t)r], true);
-    } else {
-        g->mine.push_back(mirt_tile{0, 0, W, H});
-        g->cap = (uint64_t)W * H;
-    }
-    for (uint32_t j = 0; j < inflight; ++j) {
-        g->slots.emplace_back(new Slot());
-        g->slots.back()->dedicated = true;
-        int r = slot_init(g->slots.back().get());
-        if (r != MIRT_OK) return r;
-    }
-    g->streams.assign(inflight, nullptr);
-    g->ev_traced.assign(inflight, nullptr);
-    g->ev_gathered.assign(inflight, nullptr);
-    g->ev_done.assign(inflight, nullptr);
-    for (uint32_t j = 0; j < inflight; ++j) {
-        HIP_TRY(stream_with_queue(c->cus, &g->streams[j]));
-        HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
-    }
-    if (is_root)
-        for (uint32_t j = 0; j < inflight; ++j)
-            g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
-    if (g->tiled) {
-        g->packed.assign(inflight, nullptr);
-        for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->packed[j], g->cap * 4));
-        {
-            std::vector<TileDesc> md;
-            uint64_t o = 0;
-            for (const mirt_tile& x : g->mine) {
-                md.push_back(TileDesc{x.x, x.y, x.w, x.h, o, 0, 0});
-                o += (uint64_t)x.w * x.h;
-            }
-            HIP_TRY(hipMalloc((void**)&g->d_mine, md.size() * sizeof(TileDesc)));
-            HIP_TRY(hipMemcpy(g->d_mine, md.data(), md.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
-        }
-        if (is_root) {
-            g->gathered.assign(inflight, nullptr);
-            for (uint32_t j = 0; j < inflight; ++j)
-                HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)plan_world * g->cap * 4));
-            std::vector<TileDesc> td;
-            for (int r = 0; r < plan_world; ++r) {
-                const uint32_t first = (uint32_t)td.size();
-                uint64_t o = 0;  // within region r
-                for (const mirt_tile& x : g->plans[(size_t)r]) {
-                    td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, (uint32_t)r, first});
-                    o += (uint64_t)x.w * x.h;
-                    g->max_tile_px = std::max<uint64_t>(g->max_tile_px, (uint64_t)x.w * x.h);
-                }
-            }
-            g->n_unpack = (uint32_t)td.size();
-            HIP_TRY(hipMalloc((void**)&g->d_unpack, td.size() * sizeof(TileDesc)));
-            HIP_TRY(hipMemcpy(g->d_unpack, td.data(), td.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
-        } else {
-            g->sendbuf.assign(inflight, nullptr);
-            for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(hipMalloc((void**)&g->sendbuf[j], g->cap * 4));
-        }
-    }
-    if (world > 1) {
-        if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
-        HIP_TRY(stream_with_queue(c->cus, &g->comm_stream));
-        ncclUniqueId u;
-        memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
-        RCCL_TRY(rccl().comm_init_rank(&g->comm, world, u, rank));
-    }
-    *out = g.release();
-    return MIRT_OK;
-}
-
 // The frame's hit rectangle [x0, x1) x [y0, y1): the pixels whose ray can meet the object.
 // A ray that meets a triangle passes through a root child's box, so its (s, t) lies in that
 // child's frustum rectangle (frustum_args: conservative, the block pre-test relies on it);
 // pixel i's s is (float)(sB - sA i), non-increasing in i, and likewise t in j.  Frames
 // without the pre-test (several objects, culling off) use the whole screen.
-static void hit_rect(const FrameRec& rec, uint32_t W, uint32_t H, uint32_t out[4]) {
+void hit_rect(const FrameRec& rec, uint32_t W, uint32_t H, uint32_t out[4]) {
     out[0] = 0;
     out[1] = 0;
     out[2] = W;
@@ -1583,7 +1375,7 @@ static void hit_rect(const FrameRec& rec, uint32_t W, uint32_t H, uint32_t out[4
 }
 
 // Pixels of a tile list inside a hit rectangle (k_pack_rect's transfer size in words).
-static uint64_t rect_pixels(const std::vector<mirt_tile>& tiles, const uint32_t R[4]) {
+uint64_t rect_pixels(const std::vector<mirt_tile>& tiles, const uint32_t R[4]) {
     uint64_t n = 0;
     for (const mirt_tile& t : tiles) {
         const uint32_t x0 = std::max(t.x, R[0]), x1 = std::min(t.x + t.w, R[2]);
@@ -1593,69 +1385,788 @@ static uint64_t rect_pixels(const std::vector<mirt_tile>& tiles, const uint32_t 
     return n;
 }
 
-// Launch the open batch on its slot's stream: trace, then (tiled) the gather of every frame
-// of the batch as ONE RCCL group and, on the root, one unpack per frame.
+// One rank's share of the deal, traced by this process: normally this rank's own; in the
+// emulated world (mirt_group_emulate) every rank's, so one GPU runs the whole N-rank
+// pack -> transfer -> check -> unpack chain.
+struct Share {
+    uint32_t q = 0;                            // deal index (0: the root's share)
+    std::vector<mirt_tile> tiles;
+    TileDesc* d_tiles = nullptr;               // tiles at their offsets in the share's rgbv plane
+    std::vector<uint32_t*> packed;             // tiled, per frame slot: the share's rgbv plane
+    std::vector<uint32_t*> sendbuf;            // tiled non-root share, per frame slot: transfer form
+    std::vector<std::unique_ptr<Slot>> slots;  // per batch slot: trace workspace
+};
+
+// A launched batch (per batch slot): its frames, their slots and hit rectangles.
+struct BatchRec {
+    uint32_t n = 0;
+    uint64_t first = 0;                        // frames first .. first + n - 1
+    uint32_t j[kMaxFrames] = {};               // their frame slots
+    uint32_t rect[kMaxFrames][4] = {};
+    bool checked = true;                       // trailer results folded into the frame states
+};
+
+// Host copy of one frame slot's framebuffer (mirt_group_set_host_output).
+struct HostFrame {
+    uint8_t* rgb8 = nullptr;
+    uint8_t* valid = nullptr;
+    uint32_t rect[4] = {0, 0, 0, 0};           // the region last copied (the rest is zero)
+};
+
+}  // namespace
+
+struct mirt_group {
+    mirt_ctx* c = nullptr;
+    int rank = 0, world = 1;
+    uint32_t W = 0, H = 0, F = 1, tile = 0, tile_h = 0;
+    bool tiled = false;                 // packed rgbv tiles + unpack (world > 1, or a tiled rehearsal)
+    ncclComm_t comm = nullptr;          // ranks of the communicator == deal indices
+    hipStream_t comm_stream = nullptr;  // every RCCL call, in issue order (the same on every rank)
+    hipEvent_t ev_comm = nullptr;
+    std::vector<hipStream_t> streams;   // batch slot b runs on streams[b]
+    std::vector<hipEvent_t> ev_traced, ev_gathered, ev_done;
+    // the deal: deal index i is rank members[i] (members[0] = 0, the root)
+    std::vector<uint32_t> members;
+    std::vector<std::vector<mirt_tile>> plans;  // every deal index's tiles (the transfer sizes)
+    uint64_t cap = 0;                   // largest share (pixels)
+    uint64_t stride = 0;                // words per gathered region / transfer buffer (cap + trailer)
+    int my_index = 0;
+    std::vector<Share> shares;
+    std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
+    std::vector<uint32_t*> gathered;    // root, per frame slot: plan regions of `stride` words
+    TileDesc* d_unpack = nullptr;       // root: every share's tiles at their region offsets
+    uint32_t n_unpack = 0;
+    RegionDesc* d_regions = nullptr;
+    uint64_t max_tile_px = 0;
+    uint8_t* h_bad = nullptr;           // root, pinned: [frame slot][region] trailer verdicts
+    size_t h_bad_cap = 0;
+    // modes
+    uint32_t emulate = 0;               // > 1: the emulated world (mirt_group_emulate)
+    uint64_t emu_drop = 0;              // emulated deal indices whose transfer is dropped (fault injection)
+    bool rehearse = false;              // MIRT_GROUP_REHEARSE diagnostic (timing only: no checks)
+    bool skip_unpack = false;
+    bool host_out = false;
+    std::vector<HostFrame> hfb;
+    // frames and batches
+    uint32_t B = 1, FB = 1;
+    uint64_t nb = 0;                    // batches launched
+    uint64_t k = 0;                     // frames enqueued
+    uint32_t bn = 0;                    // frames in the open batch
+    uint32_t bj[kMaxFrames] = {};
+    FrameRec stage[kMaxFrames];         // the open batch's records (copied per share at launch)
+    uint32_t bbounces = 0;
+    std::vector<BatchRec> binfo;        // per batch slot
+    std::vector<uint64_t> slot_frame;   // per frame slot: the frame it holds (~0: none)
+    std::vector<uint64_t> slot_bad;     // per frame slot: deal indices whose transfer failed
+    // fault handling (master/pool/pool.go:224-260, master/main.go:111-161)
+    uint32_t timeout_ms = 0;
+    uint64_t failed_mask = 0;           // ranks (not deal indices) named by the last failure
+    uint64_t pending_bad = 0;           // deal indices failed since the last mirt_group_wait
+    uint64_t pending_bad_frame = ~0ull;
+    bool broken = false;                // a wait timed out: only mirt_group_exclude / destroy
+    hipStream_t probe_stream = nullptr;
+};
+
+namespace {
+
+uint64_t now_us() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Wait for a group event, within the group's deadline (0: no deadline).
+int group_wait_event(mirt_group* g, hipEvent_t ev, const char* what) {
+    if (!g->timeout_ms) {
+        HIP_TRY(hipEventSynchronize(ev));
+        return MIRT_OK;
+    }
+    const uint64_t deadline = now_us() + (uint64_t)g->timeout_ms * 1000;
+    for (uint32_t spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return MIRT_OK;
+        if (e != hipErrorNotReady) return hip_fail(e, what);
+        if (now_us() > deadline)
+            return fail(MIRT_E_TIMEOUT, std::string(what) + ": no completion within " + std::to_string(g->timeout_ms) +
+                                            " ms");
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// Transfer words of deal index q for a frame with hit rectangle R (data + trailer).
+uint64_t transfer_words(const mirt_group* g, uint32_t q, const uint32_t R[4]) {
+    return rect_pixels(g->plans[q], R) + kTrailerWords;
+}
+
+uint64_t mask_of_ranks(const mirt_group* g, uint64_t deal_mask) {
+    uint64_t m = 0;
+    for (size_t i = 0; i < g->members.size() && i < 64; ++i)
+        if ((deal_mask >> i) & 1u) m |= 1ull << (g->members[i] & 63u);
+    return m;
+}
+
+// A batch known to be complete: fold its frames' trailer verdicts into the frame states.
+void batch_fold(mirt_group* g, uint32_t bs) {
+    BatchRec& br = g->binfo[bs];
+    if (br.checked) return;
+    br.checked = true;
+    if (!g->tiled || g->rank != 0 || g->rehearse || g->skip_unpack) return;
+    const size_t P = g->members.size();
+    for (uint32_t i = 0; i < br.n; ++i) {
+        const uint32_t j = br.j[i];
+        uint64_t bad = 0;
+        for (size_t q = 0; q < P && q < 64; ++q)
+            if (g->h_bad[(size_t)j * P + q]) bad |= 1ull << q;
+        g->slot_bad[j] = bad;
+        if (bad) {
+            g->pending_bad |= bad;
+            if (g->pending_bad_frame == ~0ull) g->pending_bad_frame = br.first + i;
+        }
+    }
+}
+
+std::string ranks_text(uint64_t m) {
+    std::string s;
+    for (int r = 0; r < 64; ++r)
+        if ((m >> r) & 1u) s += (s.empty() ? "" : ",") + std::to_string(r);
+    return s;
+}
+
+// After a timeout on the root: which transfers of the stuck batch never arrived intact?
+// The trailers are read straight from the gathered regions on a stream of their own.
+uint64_t probe_failed(mirt_group* g, uint32_t bs) {
+    const BatchRec& br = g->binfo[bs];
+    const size_t P = g->members.size();
+    if (g->rank != 0 || !g->tiled) return 1;  // a sender only talks to the root
+    uint64_t bad = 0;
+    if (!g->probe_stream && hipStreamCreateWithFlags(&g->probe_stream, hipStreamNonBlocking) != hipSuccess)
+        return ~0ull;
+    uint32_t* h = nullptr;
+    if (hipHostMalloc((void**)&h, sizeof(uint32_t) * 2 * P * kMaxFrames) != hipSuccess) return ~0ull;
+    for (uint32_t i = 0; i < br.n; ++i)
+        for (size_t q = 1; q < P; ++q) {
+            const uint64_t words = rect_pixels(g->plans[q], br.rect[i]);
+            (void)hipMemcpyAsync(h + 2 * (i * P + q), g->gathered[br.j[i]] + q * g->stride + words, 8,
+                                 hipMemcpyDeviceToHost, g->probe_stream);
+        }
+    hipEvent_t ev = nullptr;
+    bool done = false;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+        hipEventRecord(ev, g->probe_stream) == hipSuccess) {
+        const uint64_t deadline = now_us() + 1000000;
+        while (!(done = hipEventQuery(ev) == hipSuccess) && now_us() < deadline)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    if (ev) (void)hipEventDestroy(ev);
+    if (!done) {
+        bad = ~1ull;  // the device does not answer: every peer is suspect
+    } else {
+        for (uint32_t i = 0; i < br.n; ++i)
+            for (size_t q = 1; q < P && q < 64; ++q) {
+                const uint64_t words = rect_pixels(g->plans[q], br.rect[i]);
+                const uint32_t* t = h + 2 * (i * P + q);
+                if (t[0] != transfer_tag(br.first + i) || t[1] != (uint32_t)words) bad |= 1ull << q;
+            }
+    }
+    (void)hipHostFree(h);
+    return bad;
+}
+
+int group_timed_out(mirt_group* g, uint32_t bs, int r) {
+    if (r != MIRT_E_TIMEOUT) return r;
+    const uint64_t bad = probe_failed(g, bs);
+    g->failed_mask = mask_of_ranks(g, bad) & ~(g->rank == 0 ? 1ull : 0ull);
+    if (g->rank != 0) g->failed_mask = 1;  // a sender waits on the root only
+    g->broken = true;
+    const BatchRec& br = g->binfo[bs];
+    return fail(MIRT_E_TIMEOUT, "frames " + std::to_string(br.first) + ".." + std::to_string(br.first + br.n - 1) +
+                                    " did not complete within " + std::to_string(g->timeout_ms) +
+                                    " ms; transfers missing from rank(s) " +
+                                    (g->failed_mask ? ranks_text(g->failed_mask) : std::string("none (local)")) +
+                                    " (mirt_group_failed_ranks; mirt_group_exclude re-deals)");
+}
+
+// (Re)build the deal over g->members: plans, shares, buffers, the root's unpack tables.
+int group_plan(mirt_group* g) {
+    const uint32_t P = (uint32_t)g->members.size();
+    g->plans.assign(P, {});
+    uint64_t cap = 0;
+    if (g->tiled) {
+        for (uint32_t q = 0; q < P; ++q) {
+            plan_rank_tiles(g->W, g->H, g->tile, g->tile_h, P, q, g->plans[q], true);
+            if (g->plans[q].empty())
+                return fail(MIRT_E_INVALID, "deal index " + std::to_string(q) + " has no tiles (tile too large for " +
+                                                std::to_string(P) + " ranks)");
+            cap = std::max(cap, tiles_pixels(g->plans[q]));
+        }
+    } else {
+        g->plans[0].push_back(mirt_tile{0, 0, g->W, g->H});
+        cap = (uint64_t)g->W * g->H;
+    }
+    const uint64_t stride = (cap + kTrailerWords + 3) & ~3ull;
+    const bool grow = stride > g->stride;
+    g->cap = cap;
+    g->stride = std::max(g->stride, stride);
+    // the shares this process traces
+    std::vector<uint32_t> want;
+    if (g->emulate > 1) {
+        for (uint32_t q = 0; q < P; ++q) want.push_back(q);
+    } else if (g->rehearse) {
+        const char* rr = getenv("MIRT_GROUP_REHEARSE_RANK");
+        want.push_back(rr ? (uint32_t)std::min<int>(std::max(atoi(rr), 0), (int)P - 1) : 0u);
+    } else {
+        want.push_back((uint32_t)g->my_index);
+    }
+    // keep existing shares' workspaces (slots), rebuild their tile lists and planes
+    while (g->shares.size() > want.size()) {
+        Share& sh = g->shares.back();
+        for (auto& sl : sh.slots) slot_free(sl.get());
+        for (uint32_t* p : sh.packed) (void)hipFree(p);
+        for (uint32_t* p : sh.sendbuf) (void)hipFree(p);
+        if (sh.d_tiles) (void)hipFree(sh.d_tiles);
+        g->shares.pop_back();
+    }
+    g->shares.resize(want.size());
+    for (size_t si = 0; si < want.size(); ++si) {
+        Share& sh = g->shares[si];
+        sh.q = want[si];
+        sh.tiles = g->plans[sh.q];
+        while (sh.slots.size() < g->F) {
+            sh.slots.emplace_back(new Slot());
+            sh.slots.back()->dedicated = true;
+            int r = slot_init(sh.slots.back().get());
+            if (r != MIRT_OK) return r;
+        }
+        if (!g->tiled) continue;
+        if (grow || sh.packed.empty()) {
+            for (uint32_t* p : sh.packed) (void)hipFree(p);
+            for (uint32_t* p : sh.sendbuf) (void)hipFree(p);
+            sh.packed.assign(g->F, nullptr);
+            sh.sendbuf.assign(g->F, nullptr);
+            for (uint32_t j = 0; j < g->F; ++j) {
+                HIP_TRY(hipMalloc((void**)&sh.packed[j], g->stride * 4));
+                HIP_TRY(hipMalloc((void**)&sh.sendbuf[j], g->stride * 4));
+            }
+        }
+        std::vector<TileDesc> md;
+        uint64_t o = 0;
+        for (const mirt_tile& x : sh.tiles) {
+            md.push_back(TileDesc{x.x, x.y, x.w, x.h, o, 0, 0});
+            o += (uint64_t)x.w * x.h;
+        }
+        if (sh.d_tiles) (void)hipFree(sh.d_tiles);
+        sh.d_tiles = nullptr;
+        HIP_TRY(hipMalloc((void**)&sh.d_tiles, md.size() * sizeof(TileDesc)));
+        HIP_TRY(hipMemcpy(sh.d_tiles, md.data(), md.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+    }
+    if (g->tiled && g->rank == 0) {
+        if (grow || g->gathered.empty() || g->h_bad_cap < (size_t)g->F * P) {
+            for (uint32_t* p : g->gathered) (void)hipFree(p);
+            g->gathered.assign(g->F, nullptr);
+        }
+        // sized for the largest deal this group can hold (a deal never grows after creation)
+        for (uint32_t j = 0; j < g->F; ++j)
+            if (!g->gathered[j]) HIP_TRY(hipMalloc((void**)&g->gathered[j], (size_t)P * g->stride * 4));
+        std::vector<TileDesc> td;
+        std::vector<RegionDesc> rd;
+        g->max_tile_px = 0;
+        for (uint32_t q = 0; q < P; ++q) {
+            const uint32_t first = (uint32_t)td.size();
+            uint64_t o = 0;  // within region q
+            for (const mirt_tile& x : g->plans[q]) {
+                td.push_back(TileDesc{x.x, x.y, x.w, x.h, o, q, first});
+                o += (uint64_t)x.w * x.h;
+                g->max_tile_px = std::max<uint64_t>(g->max_tile_px, (uint64_t)x.w * x.h);
+            }
+            rd.push_back(RegionDesc{first, (uint32_t)(td.size() - first)});
+        }
+        g->n_unpack = (uint32_t)td.size();
+        if (g->d_unpack) (void)hipFree(g->d_unpack);
+        if (g->d_regions) (void)hipFree(g->d_regions);
+        g->d_unpack = nullptr;
+        g->d_regions = nullptr;
+        HIP_TRY(hipMalloc((void**)&g->d_unpack, td.size() * sizeof(TileDesc)));
+        HIP_TRY(hipMemcpy(g->d_unpack, td.data(), td.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc((void**)&g->d_regions, rd.size() * sizeof(RegionDesc)));
+        HIP_TRY(hipMemcpy(g->d_regions, rd.data(), rd.size() * sizeof(RegionDesc), hipMemcpyHostToDevice));
+        if (g->h_bad_cap < (size_t)g->F * P) {
+            if (g->h_bad) (void)hipHostFree(g->h_bad);
+            g->h_bad = nullptr;
+            g->h_bad_cap = 0;
+            HIP_TRY(hipHostMalloc((void**)&g->h_bad, (size_t)g->F * P));
+            g->h_bad_cap = (size_t)g->F * P;
+        }
+        memset(g->h_bad, 0, g->h_bad_cap);
+    }
+    return MIRT_OK;
+}
+
+// Creation-time agreement of the ranks (world > 1): every sender's view of the group
+// {W, H, tile, tile_h, world, inflight, stride, deal checksum} must equal the root's, or
+// every rank fails here instead of hanging or corrupting frames later.
+uint32_t group_signature(const mirt_group* g) {
+    uint32_t h = 2166136261u;
+    auto mix = [&](uint32_t v) {
+        for (int b = 0; b < 4; ++b) h = (h ^ ((v >> (8 * b)) & 0xffu)) * 16777619u;
+    };
+    mix(g->W), mix(g->H), mix(g->tile), mix(g->tile_h), mix((uint32_t)g->members.size()), mix(g->F);
+    mix((uint32_t)g->stride);
+    for (const auto& p : g->plans)
+        for (const mirt_tile& t : p) mix(t.x), mix(t.y), mix(t.w), mix(t.h);
+    return h;
+}
+
+int group_handshake(mirt_group* g) {
+    const Rccl& R = rccl();
+    const uint32_t P = (uint32_t)g->members.size();
+    uint32_t* d = nullptr;  // [P][4] words: root receives, then sends its verdicts
+    HIP_TRY(hipMalloc((void**)&d, (size_t)P * 16));
+    std::vector<uint32_t> h((size_t)P * 4, 0);
+    const uint32_t sig[4] = {0x6d697274u, group_signature(g), (uint32_t)g->my_index, (uint32_t)P};
+    int r = MIRT_OK;
+    auto step = [&](bool send_phase) -> int {
+        RCCL_TRY(R.group_start());
+        for (uint32_t q = 1; q < P; ++q) {
+            if (g->my_index == 0) {
+                if (send_phase) RCCL_TRY(R.send(d + 4 * q, 16, ncclUint8, (int)q, g->comm, g->comm_stream));
+                else RCCL_TRY(R.recv(d + 4 * q, 16, ncclUint8, (int)q, g->comm, g->comm_stream));
+            } else if ((uint32_t)g->my_index == q) {
+                if (send_phase) RCCL_TRY(R.recv(d + 4 * q, 16, ncclUint8, 0, g->comm, g->comm_stream));
+                else RCCL_TRY(R.send(d + 4 * q, 16, ncclUint8, 0, g->comm, g->comm_stream));
+            }
+        }
+        RCCL_TRY(R.group_end());
+        HIP_TRY(hipEventRecord(g->ev_comm, g->comm_stream));
+        return group_wait_event(g, g->ev_comm, "group handshake");
+    };
+    if (g->my_index != 0) HIP_TRY(hipMemcpy(d + 4 * g->my_index, sig, 16, hipMemcpyHostToDevice));
+    if ((r = step(false)) == MIRT_OK) {
+        if (g->my_index == 0) {
+            HIP_TRY(hipMemcpy(h.data(), d, (size_t)P * 16, hipMemcpyDeviceToHost));
+            uint64_t bad = 0;
+            for (uint32_t q = 1; q < P; ++q) {
+                const uint32_t* s = &h[(size_t)q * 4];
+                const bool ok = s[0] == sig[0] && s[1] == sig[1] && s[2] == q && s[3] == P;
+                h[(size_t)q * 4] = ok ? 1u : 0u;
+                if (!ok) bad |= 1ull << (q & 63u);
+            }
+            HIP_TRY(hipMemcpy(d, h.data(), (size_t)P * 16, hipMemcpyHostToDevice));
+            r = step(true);
+            if (r == MIRT_OK && bad) {
+                g->failed_mask = mask_of_ranks(g, bad);
+                r = fail(MIRT_E_PEER, "group handshake: rank(s) " + ranks_text(g->failed_mask) +
+                                          " disagree with the root on W/H/tile/world/inflight or the deal");
+            }
+        } else {
+            r = step(true);
+            if (r == MIRT_OK) {
+                uint32_t v[4];
+                HIP_TRY(hipMemcpy(v, d + 4 * g->my_index, 16, hipMemcpyDeviceToHost));
+                if (v[0] != 1u) {
+                    g->failed_mask = 1;
+                    r = fail(MIRT_E_PEER, "group handshake: the root rejected this rank's view of the group");
+                }
+            }
+        }
+    }
+    (void)hipFree(d);
+    return r;
+}
+
+// Device -> host copy of a frame's framebuffer: the union of this frame's hit rectangle
+// and the one last copied into that host slot (outside the rectangle every pixel is a
+// miss, i.e. zero, so the host planes stay exact).
+int host_copy(mirt_group* g, uint32_t j, const uint32_t R[4], hipStream_t s) {
+    HostFrame& hf = g->hfb[j];
+    const OutPlanes& d = g->fb[j];
+    uint32_t u[4] = {R[0], R[1], R[2], R[3]};
+    const bool r_empty = R[0] >= R[2] || R[1] >= R[3], p_empty = hf.rect[0] >= hf.rect[2] || hf.rect[1] >= hf.rect[3];
+    if (r_empty) memcpy(u, hf.rect, sizeof(u));
+    else if (!p_empty) {
+        u[0] = std::min(u[0], hf.rect[0]);
+        u[1] = std::min(u[1], hf.rect[1]);
+        u[2] = std::max(u[2], hf.rect[2]);
+        u[3] = std::max(u[3], hf.rect[3]);
+    }
+    memcpy(hf.rect, R, sizeof(hf.rect));
+    if (u[0] >= u[2] || u[1] >= u[3]) return MIRT_OK;
+    const size_t off = (size_t)u[0] * g->H + u[1], rows = u[3] - u[1], cols = u[2] - u[0];
+    if (d.rgb8)
+        HIP_TRY(hipMemcpy2DAsync(hf.rgb8 + 3 * off, (size_t)g->H * 3, d.rgb8 + 3 * off, (size_t)g->H * 3, rows * 3, cols,
+                                 hipMemcpyDeviceToHost, s));
+    if (d.valid)
+        HIP_TRY(hipMemcpy2DAsync(hf.valid + off, g->H, d.valid + off, g->H, rows, cols, hipMemcpyDeviceToHost, s));
+    return MIRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                    mirt_tile* out, uint32_t cap) {
+    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
+    std::vector<mirt_tile> t;
+    plan_rank_tiles(W, H, tile, tile_h, world, rank, t);
+    if (out) {
+        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
+        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
+    }
+    return (int)t.size();
+}
+
+int mirt_group_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
+                          mirt_tile* out, uint32_t cap) {
+    if (!W || !H || !tile || !world || rank >= world) return fail(MIRT_E_INVALID, "bad tile plan arguments");
+    std::vector<mirt_tile> t;
+    plan_rank_tiles(W, H, tile, tile_h, world, rank, t, true);
+    if (out) {
+        if (t.size() > cap) return fail(MIRT_E_LIMIT, "tile buffer too small");
+        memcpy(out, t.data(), t.size() * sizeof(mirt_tile));
+    }
+    return (int)t.size();
+}
+
+int mirt_group_unique_id(uint8_t* id) {
+    if (!id) return fail(MIRT_E_INVALID, "id is NULL");
+    if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
+    ncclUniqueId u;
+    RCCL_TRY(rccl().get_unique_id(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return MIRT_OK;
+}
+
+void mirt_group_destroy(mirt_group* g) {
+    if (!g) return;
+#ifdef MIRT_HOST_TIMERS
+    fprintf(stderr, "host_timers_us_per_frame wait %.2f record %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
+            g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k);
+#endif
+    (void)hipSetDevice(g->c->device);
+    if (g->comm) {
+        // a broken group (a peer stopped answering) may have RCCL work that never ends
+        if (g->broken && rccl().comm_abort) (void)rccl().comm_abort(g->comm);
+        else (void)rccl().comm_destroy(g->comm);
+    }
+    if (!g->broken) {
+        for (hipStream_t s : g->streams)
+            if (s) (void)hipStreamSynchronize(s);
+        if (g->comm_stream) (void)hipStreamSynchronize(g->comm_stream);
+    }
+    for (Share& sh : g->shares) {
+        for (auto& sl : sh.slots) slot_free(sl.get());
+        for (uint32_t* p : sh.packed) (void)hipFree(p);
+        for (uint32_t* p : sh.sendbuf) (void)hipFree(p);
+        if (sh.d_tiles) (void)hipFree(sh.d_tiles);
+    }
+    for (uint32_t* p : g->gathered)
+        if (p) (void)hipFree(p);
+    if (g->d_unpack) (void)hipFree(g->d_unpack);
+    if (g->d_regions) (void)hipFree(g->d_regions);
+    if (g->h_bad) (void)hipHostFree(g->h_bad);
+    for (HostFrame& hf : g->hfb) {
+        if (hf.rgb8) (void)hipHostFree(hf.rgb8);
+        if (hf.valid) (void)hipHostFree(hf.valid);
+    }
+    for (auto* v : {&g->ev_traced, &g->ev_gathered, &g->ev_done})
+        for (hipEvent_t e : *v)
+            if (e) (void)hipEventDestroy(e);
+    if (g->ev_comm) (void)hipEventDestroy(g->ev_comm);
+    for (hipStream_t s : g->streams)
+        if (s) (void)hipStreamDestroy(s);
+    if (g->comm_stream) (void)hipStreamDestroy(g->comm_stream);
+    if (g->probe_stream) (void)hipStreamDestroy(g->probe_stream);
+    delete g;
+}
+
+int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world, uint32_t W, uint32_t H,
+                      uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL context or out");
+    *out = nullptr;
+    if (world < 1 || world > 64 || rank < 0 || rank >= world) return fail(MIRT_E_INVALID, "bad rank / world (1..64)");
+    if (!W || !H || W > 65535 || H > 65535) return fail(MIRT_E_INVALID, "bad screen size");
+    if (inflight < 1 || inflight > 16) return fail(MIRT_E_INVALID, "inflight must be 1..16");
+    if (world > 1 && !unique_id) return fail(MIRT_E_INVALID, "world > 1 needs the root's unique id");
+    if (world > 1 && tile == 0) return fail(MIRT_E_INVALID, "world > 1 needs a tile size");
+    const bool is_root = rank == 0;
+    if (is_root && !fbs) return fail(MIRT_E_INVALID, "the root needs its framebuffers");
+    // the tiled path gathers packed rgbv words (uint8 colour + valid): it cannot produce
+    // the fp64 colour or the diagnostic face/object planes
+    if (is_root && tile > 0)
+        for (uint32_t j = 0; j < inflight; ++j)
+            if (fbs[j].rgb || fbs[j].face || fbs[j].object)
+                return fail(MIRT_E_INVALID, "tiled frame groups produce rgb8 / valid / rgbv only (rgb, face and "
+                                            "object planes need tile == 0)");
+    HIP_TRY(hipSetDevice(c->device));
+    std::unique_ptr<mirt_group, void (*)(mirt_group*)> g(new mirt_group(), mirt_group_destroy);
+    g->c = c;
+    g->rank = rank;
+    g->world = world;
+    g->W = W;
+    g->H = H;
+    g->F = inflight;
+    g->FB = inflight;  // one frame per launch until mirt_group_set_batch
+    g->tile = tile;
+    g->tile_h = tile_h;
+    g->tiled = tile > 0;
+    // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
+    // N-way deal (MIRT_GROUP_REHEARSE_RANK, default 0) and unpack all N regions, the others
+    // stale: the root's per-frame GPU work at N GPUs without the transfers.  Results are
+    // not checked; mirt_group_emulate is the correctness mode.
+    const char* reh = getenv("MIRT_GROUP_REHEARSE");
+    const int plan_world = (world == 1 && g->tiled && reh && atoi(reh) > 1) ? std::min(atoi(reh), 64) : world;
+    g->rehearse = plan_world != world;
+    g->skip_unpack = g->rehearse && getenv("MIRT_GROUP_REHEARSE_NO_UNPACK");
+    for (int q = 0; q < plan_world; ++q) g->members.push_back((uint32_t)q);
+    g->my_index = rank;
+    g->streams.assign(inflight, nullptr);
+    g->ev_traced.assign(inflight, nullptr);
+    g->ev_gathered.assign(inflight, nullptr);
+    g->ev_done.assign(inflight, nullptr);
+    for (uint32_t j = 0; j < inflight; ++j) {
+        HIP_TRY(stream_with_queue(c->cus, &g->streams[j]));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&g->ev_comm, hipEventDisableTiming));
+    g->binfo.assign(inflight, BatchRec());
+    g->slot_frame.assign(inflight, ~0ull);
+    g->slot_bad.assign(inflight, 0);
+    if (is_root)
+        for (uint32_t j = 0; j < inflight; ++j)
+            g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
+    int r = group_plan(g.get());
+    if (r != MIRT_OK) return r;
+    if (world > 1) {
+        if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
+        HIP_TRY(stream_with_queue(c->cus, &g->comm_stream));
+        ncclUniqueId u;
+        memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
+        RCCL_TRY(rccl().comm_init_rank(&g->comm, world, u, rank));
+        g->timeout_ms = 120000;  // the handshake never waits forever
+        r = group_handshake(g.get());
+        g->timeout_ms = 0;
+        if (r != MIRT_OK) {
+            if (r == MIRT_E_TIMEOUT) g->broken = true;
+            return r;
+        }
+    }
+    *out = g.release();
+    return MIRT_OK;
+}
+
+int mirt_group_emulate(mirt_group* g, uint32_t world) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (g->k != 0) return fail(MIRT_E_INVALID, "emulate before the first frame");
+    if (g->world != 1 || !g->tiled || g->rehearse)
+        return fail(MIRT_E_INVALID, "emulation needs a tiled world == 1 group (not a rehearsal)");
+    if (world < 1 || world > 64) return fail(MIRT_E_INVALID, "emulated world must be 1..64");
+    HIP_TRY(hipSetDevice(g->c->device));
+    g->emulate = world;
+    g->members.clear();
+    for (uint32_t q = 0; q < world; ++q) g->members.push_back(q);
+    g->my_index = 0;
+    return group_plan(g);
+}
+
+int mirt_group_emulate_drop(mirt_group* g, uint64_t ranks) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (g->emulate < 2) return fail(MIRT_E_INVALID, "fault injection needs an emulated world");
+    if (ranks & 1u) return fail(MIRT_E_INVALID, "the root (rank 0) cannot be dropped");
+    uint64_t deal = 0;  // ranks -> deal indices
+    for (size_t i = 0; i < g->members.size() && i < 64; ++i)
+        if ((ranks >> (g->members[i] & 63u)) & 1u) deal |= 1ull << i;
+    g->emu_drop = deal;
+    return MIRT_OK;
+}
+
+int mirt_group_set_timeout(mirt_group* g, uint32_t ms) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    g->timeout_ms = ms;
+    return MIRT_OK;
+}
+
+int mirt_group_failed_ranks(const mirt_group* g, uint64_t* mask) {
+    if (!g || !mask) return fail(MIRT_E_INVALID, "NULL argument");
+    *mask = g->failed_mask;
+    return __builtin_popcountll(g->failed_mask);
+}
+
+int mirt_group_set_host_output(mirt_group* g, int enable) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (g->k != 0) return fail(MIRT_E_INVALID, "set the host output before the first frame");
+    if (g->rank != 0) return fail(MIRT_E_INVALID, "only the root holds framebuffers");
+    HIP_TRY(hipSetDevice(g->c->device));
+    g->host_out = enable != 0;
+    if (g->host_out && g->hfb.empty()) {
+        g->hfb.assign(g->F, HostFrame());
+        const size_t n = (size_t)g->W * g->H;
+        for (HostFrame& hf : g->hfb) {
+            HIP_TRY(hipHostMalloc((void**)&hf.rgb8, 3 * n));
+            HIP_TRY(hipHostMalloc((void**)&hf.valid, n));
+            memset(hf.rgb8, 0, 3 * n);
+            memset(hf.valid, 0, n);
+        }
+    }
+    return MIRT_OK;
+}
+
+int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_id) {
+    if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (!(alive & 1u)) return fail(MIRT_E_INVALID, "the root (rank 0) must stay in the group");
+    const uint32_t world = g->emulate > 1 ? g->emulate : (uint32_t)g->world;
+    if (world < 64 && (alive >> world)) return fail(MIRT_E_INVALID, "alive names ranks outside the group");
+    if (g->emulate <= 1 && !((alive >> g->rank) & 1u))
+        return fail(MIRT_E_INVALID, "this rank is excluded: destroy its group instead");
+    HIP_TRY(hipSetDevice(g->c->device));
+    std::vector<uint32_t> keep;
+    for (uint32_t q = 0; q < g->members.size(); ++q)
+        if ((alive >> (g->members[q] & 63u)) & 1u) keep.push_back(q);  // deal indices that stay
+    if (g->world > 1) {
+        const Rccl& R = rccl();
+        std::vector<int> excl;
+        for (uint32_t q = 0; q < g->members.size(); ++q)
+            if (!((alive >> (g->members[q] & 63u)) & 1u)) excl.push_back((int)q);
+        ncclComm_t nc = nullptr;
+        if (new_unique_id) {
+            if (R.comm_abort) (void)R.comm_abort(g->comm);
+            else (void)R.comm_destroy(g->comm);
+            g->comm = nullptr;
+            ncclUniqueId u;
+            memcpy(u.internal, new_unique_id, NCCL_UNIQUE_ID_BYTES);
+            int me = 0;
+            for (uint32_t i = 0; i < keep.size(); ++i)
+                if (keep[i] == (uint32_t)g->my_index) me = (int)i;
+            RCCL_TRY(R.comm_init_rank(&nc, (int)keep.size(), u, me));
+        } else {
+            if (!R.comm_shrink) return fail(MIRT_E_DEVICE, "librccl has no ncclCommShrink: pass a new unique id");
+            RCCL_TRY(R.comm_shrink(g->comm, excl.data(), (int)excl.size(), &nc, nullptr, NCCL_SHRINK_ABORT));
+            if (R.comm_abort) (void)R.comm_abort(g->comm);
+        }
+        g->comm = nc;
+    }
+    // drain what the group still runs (the aborted communicator's kernels have ended)
+    const uint32_t saved = g->timeout_ms;
+    if (!g->timeout_ms) g->timeout_ms = 10000;
+    for (uint32_t b = 0; b < g->F; ++b) {
+        HIP_TRY(hipEventRecord(g->ev_done[b], g->streams[b]));
+        int r = group_wait_event(g, g->ev_done[b], "draining the group");
+        if (r != MIRT_OK) {
+            g->timeout_ms = saved;
+            return r;
+        }
+    }
+    g->timeout_ms = saved;
+    std::vector<uint32_t> members;
+    for (uint32_t q : keep) members.push_back(g->members[q]);
+    for (uint32_t i = 0; i < keep.size(); ++i)
+        if (keep[i] == (uint32_t)g->my_index) g->my_index = (int)i;
+    g->members = members;
+    g->emu_drop = 0;
+    g->bn = 0;
+    g->nb = 0;
+    for (BatchRec& br : g->binfo) br = BatchRec();
+    for (uint64_t& f : g->slot_frame) f = ~0ull;
+    for (uint64_t& b : g->slot_bad) b = 0;
+    g->pending_bad = 0;
+    g->pending_bad_frame = ~0ull;
+    g->failed_mask = 0;
+    g->broken = false;
+    return group_plan(g);
+}
+
+// Launch the open batch on its slot's stream: every share's trace, then (tiled) the pack
+// into the transfer form, the gather of the batch as ONE RCCL group (emulated: the same
+// bytes copied on the device), and on the root the trailer check and one unpack launch.
 static int group_flush(mirt_group* g) {
     if (g->bn == 0) return MIRT_OK;
     mirt_ctx* c = g->c;
     const uint32_t bs = (uint32_t)(g->nb % g->FB);
     hipStream_t s = g->streams[bs];
-    const bool is_root = g->rank == g->root;
+    const bool is_root = g->rank == 0;
     const uint32_t n = g->bn;
     g->bn = 0;
+    BatchRec& br = g->binfo[bs];
+    br.n = n;
+    br.first = g->k - n;
+    br.checked = false;
+    RectJobs jobs{};
+    for (uint32_t i = 0; i < n; ++i) {
+        br.j[i] = g->bj[i];
+        hit_rect(g->stage[i], g->W, g->H, br.rect[i]);
+        memcpy(jobs.rect[i], br.rect[i], sizeof(jobs.rect[i]));
+        jobs.tag[i] = transfer_tag(br.first + i);
+    }
     // a sender reuses its packed planes only after their previous batch's sends are done (the
     // root's stream already waited for that gather before its unpacks)
     if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
-    int r = launch_frames(c, g->slots[bs].get(), n, g->W, g->H, g->mine.data(), (uint32_t)g->mine.size(), g->bbounces,
-                          s, nullptr);
-    if (r != MIRT_OK) {
-        (void)hipStreamSynchronize(s);
-        return r;
-    }
-    if (g->tiled) {
-        // every frame's tiles inside its hit rectangle -> the transfer buffer (the root packs
-        // into its own region); every rank derives the same rectangles, hence the same sizes
-        RectJobs jobs{};
+    for (Share& sh : g->shares) {
+        Slot* sl = sh.slots[bs].get();
+        for (uint32_t i = 0; i < n; ++i) {
+            sl->h_frames[i] = g->stage[i];
+            sl->h_frames[i].out = g->tiled ? OutPlanes{nullptr, nullptr, nullptr, nullptr, nullptr, sh.packed[g->bj[i]]}
+                                           : g->fb[g->bj[i]];
+        }
+        int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr);
+        if (r != MIRT_OK) {
+            (void)hipStreamSynchronize(s);
+            return r;
+        }
+        if (!g->tiled) continue;
+        // the share's tiles inside each frame's hit rectangle -> its transfer form (the root's
+        // share straight into region 0 of the gathered plane)
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t j = g->bj[i];
-            hit_rect(g->slots[bs]->h_frames[i], g->W, g->H, jobs.rect[i]);
-            jobs.src[i] = g->packed[j];
-            jobs.dst[i] = is_root ? g->gathered[j] + (uint64_t)g->root * g->cap : g->sendbuf[j];
+            jobs.src[i] = sh.packed[j];
+            jobs.dst[i] = (is_root && sh.q == 0) ? g->gathered[j] : sh.sendbuf[j];
         }
-        HIP_TRY(launch_pack_rect(g->d_mine, (uint32_t)g->mine.size(), jobs, n, s));
-        if (g->world > 1) {
-            const Rccl& R = rccl();
-            HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
-            HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
-            RCCL_TRY(R.group_start());
-            for (uint32_t i = 0; i < n; ++i) {
+        HIP_TRY(launch_pack_rect(sh.d_tiles, (uint32_t)sh.tiles.size(), jobs, n, s));
+        if (g->emulate > 1 && sh.q != 0 && !((g->emu_drop >> sh.q) & 1u))
+            for (uint32_t i = 0; i < n; ++i) {  // exactly the bytes an RCCL send would carry
                 const uint32_t j = g->bj[i];
-                if (is_root) {
-                    for (int q = 0; q < g->world; ++q) {
-                        const uint64_t words = rect_pixels(g->plans[(size_t)q], jobs.rect[i]);
-                        if (q != g->root && words)
-                            RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->cap, words * 4, ncclUint8, q, g->comm,
-                                            g->comm_stream));
-                    }
-                } else {
-                    const uint64_t words = rect_pixels(g->mine, jobs.rect[i]);
-                    if (words)
-                        RCCL_TRY(R.send(g->sendbuf[j], words * 4, ncclUint8, g->root, g->comm, g->comm_stream));
-                }
+                HIP_TRY(hipMemcpyAsync(g->gathered[j] + (uint64_t)sh.q * g->stride, sh.sendbuf[j],
+                                       transfer_words(g, sh.q, br.rect[i]) * 4, hipMemcpyDeviceToDevice, s));
             }
-            RCCL_TRY(R.group_end());
-            HIP_TRY(hipEventRecord(g->ev_gathered[bs], g->comm_stream));
-            if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
-        }
-        HT(4);
-        if (is_root && !g->skip_unpack) {
-            for (uint32_t i = 0; i < n; ++i) {
-                jobs.src[i] = g->gathered[g->bj[i]];
-                jobs.out[i] = g->fb[g->bj[i]];
-            }
-            HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->cap, jobs, n, s));
-        }
     }
+    if (g->tiled && g->world > 1) {
+        const Rccl& R = rccl();
+        const uint32_t P = (uint32_t)g->members.size();
+        HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
+        HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
+        RCCL_TRY(R.group_start());
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t j = g->bj[i];
+            if (is_root) {
+                for (uint32_t q = 1; q < P; ++q)
+                    RCCL_TRY(R.recv(g->gathered[j] + (uint64_t)q * g->stride, transfer_words(g, q, br.rect[i]) * 4,
+                                    ncclUint8, (int)q, g->comm, g->comm_stream));
+            } else {
+                RCCL_TRY(R.send(g->shares[0].sendbuf[j], transfer_words(g, (uint32_t)g->my_index, br.rect[i]) * 4,
+                                ncclUint8, 0, g->comm, g->comm_stream));
+            }
+        }
+        RCCL_TRY(R.group_end());
+        HIP_TRY(hipEventRecord(g->ev_gathered[bs], g->comm_stream));
+        if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
+    }
+    HT(4);
+    if (g->tiled && is_root && !g->skip_unpack) {
+        const uint32_t P = (uint32_t)g->members.size();
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t j = g->bj[i];
+            jobs.src[i] = g->gathered[j];
+            jobs.out[i] = g->fb[j];
+            jobs.bad[i] = g->h_bad + (size_t)j * P;
+        }
+        if (!g->rehearse) HIP_TRY(launch_check_regions(g->d_unpack, g->d_regions, P, g->stride, jobs, n, s));
+        HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->stride, jobs, n, s));
+    }
+    if (g->host_out && is_root)
+        for (uint32_t i = 0; i < n; ++i) {
+            int r = host_copy(g, g->bj[i], br.rect[i], s);
+            if (r != MIRT_OK) return r;
+        }
     HT(5);
     HIP_TRY(hipEventRecord(g->ev_done[bs], s));
     HT(6);
@@ -1668,6 +2179,8 @@ int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
     if (g->k != 0) return fail(MIRT_E_INVALID, "set the batch before the first frame");
     if (frames_per_launch < 1 || frames_per_launch > kMaxFrames || frames_per_launch > g->F)
         return fail(MIRT_E_INVALID, "frames per launch must be 1..min(8, inflight)");
+    if (frames_per_launch > 1 && (g->c->flags & MIRT_OPT_SPLIT_KERNELS))
+        return fail(MIRT_E_INVALID, "several frames per launch need the single-kernel path (not MIRT_OPT_SPLIT_KERNELS)");
     g->B = frames_per_launch;
     g->FB = g->F / g->B;
     return MIRT_OK;
@@ -1675,52 +2188,107 @@ int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
 
 int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
+    if (g->broken) {  // the caller must exclude the failed ranks first
+        return fail(MIRT_E_PEER, "the group lost rank(s) " + ranks_text(g->failed_mask) +
+                                     ": call mirt_group_exclude before tracing more frames");
+    }
     mirt_ctx* c = g->c;
     HT_START();
     HIP_TRY(hipSetDevice(c->device));
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
     const uint32_t j = (uint32_t)(g->k % g->F);
-    OutPlanes out{};
-    if (!g->tiled) {
-        out = g->fb[j];
-    } else {
-        out.rgbv = g->packed[j];
-    }
     FrameRec rec{};
     uint64_t tris = 0;
-    frame_record(c, f, g->W, g->H, out, rec, tris);
+    frame_record(c, f, g->W, g->H, OutPlanes{}, rec, tris);
     HT(1);
-    if (g->bn > 0 && (g->bbounces || f->max_bounces || !frames_batchable(g->slots[g->nb % g->FB]->h_frames[0], rec)))
+    // split kernels and reflection frames run one frame per launch
+    if (g->bn > 0 && (g->bbounces || f->max_bounces || (c->flags & MIRT_OPT_SPLIT_KERNELS) ||
+                      !frames_batchable(g->stage[0], rec)))
         if ((r = group_flush(g)) != MIRT_OK) return r;
     const uint32_t bs = (uint32_t)(g->nb % g->FB);
     // back-pressure when a batch opens: batch nb - FB (the last user of this slot, and of
     // every framebuffer this batch can touch) must have finished
-    if (g->bn == 0 && g->nb >= g->FB) HIP_TRY(hipEventSynchronize(g->ev_done[bs]));
+    if (g->bn == 0 && g->nb >= g->FB) {
+        if ((r = group_wait_event(g, g->ev_done[bs], "mirt_trace_frame back-pressure")) != MIRT_OK)
+            return group_timed_out(g, bs, r);
+        batch_fold(g, bs);
+    }
     HT(0);
-    g->slots[bs]->h_frames[g->bn] = rec;
+    g->stage[g->bn] = rec;
     g->bj[g->bn++] = j;
+    g->slot_frame[j] = g->k;
+    g->slot_bad[j] = 0;
     g->bbounces = f->max_bounces;
     if (index) *index = g->k;
     ++g->k;
-    if (g->bn == g->B || g->bbounces) return group_flush(g);
+    if (g->bn == g->B || g->bbounces || (c->flags & MIRT_OPT_SPLIT_KERNELS)) return group_flush(g);
     return MIRT_OK;
 }
 
 int mirt_group_wait(mirt_group* g, void* stream) {
     if (!g) return fail(MIRT_E_INVALID, "NULL group");
+    if (g->broken) return fail(MIRT_E_PEER, "the group lost rank(s) " + ranks_text(g->failed_mask));
     HIP_TRY(hipSetDevice(g->c->device));
     int r = group_flush(g);
     if (r != MIRT_OK) return r;
     const uint64_t used = std::min<uint64_t>(g->nb, g->FB);
-    for (uint64_t j = 0; j < used; ++j) {
+    for (uint64_t b = 0; b < used; ++b) {
         if (stream) {
-            HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[j], 0));
+            HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[b], 0));
         } else {
-            HIP_TRY(hipEventSynchronize(g->ev_done[j]));
+            if ((r = group_wait_event(g, g->ev_done[b], "mirt_group_wait")) != MIRT_OK)
+                return group_timed_out(g, (uint32_t)b, r);
+            batch_fold(g, (uint32_t)b);
         }
     }
-    if (!stream && g->comm_stream) HIP_TRY(hipStreamSynchronize(g->comm_stream));
+    if (!stream && g->comm_stream) {
+        HIP_TRY(hipEventRecord(g->ev_comm, g->comm_stream));
+        if ((r = group_wait_event(g, g->ev_comm, "mirt_group_wait (gathers)")) != MIRT_OK) {
+            g->broken = true;
+            g->failed_mask = g->rank == 0 ? 0 : 1;
+            return r;
+        }
+    }
+    if (!stream && g->pending_bad) {
+        g->failed_mask = mask_of_ranks(g, g->pending_bad);
+        const uint64_t fr = g->pending_bad_frame;
+        g->pending_bad = 0;
+        g->pending_bad_frame = ~0ull;
+        return fail(MIRT_E_PEER, "frame " + std::to_string(fr) + ": the transfer of rank(s) " +
+                                     ranks_text(g->failed_mask) + " is missing or inconsistent (frame skipped)");
+    }
+    return MIRT_OK;
+}
+
+int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
+    if (!g || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    if (!g->host_out) return fail(MIRT_E_INVALID, "host output is off (mirt_group_set_host_output)");
+    HIP_TRY(hipSetDevice(g->c->device));
+    const uint32_t j = (uint32_t)(index % g->F);
+    if (index >= g->k || g->slot_frame[j] != index)
+        return fail(MIRT_E_INVALID, "frame " + std::to_string(index) + " is not held (enqueued frames keep their " +
+                                        "slot until frame index + inflight)");
+    int r;
+    if (g->bn && index >= g->k - g->bn && (r = group_flush(g)) != MIRT_OK) return r;
+    // the batch holding the frame: the latest launched batch whose slot lists j
+    for (uint32_t b = 0; b < g->FB; ++b) {
+        const BatchRec& br = g->binfo[b];
+        if (br.n && index >= br.first && index < br.first + br.n) {
+            if ((r = group_wait_event(g, g->ev_done[b], "mirt_group_frame_host")) != MIRT_OK)
+                return group_timed_out(g, b, r);
+            batch_fold(g, b);
+            break;
+        }
+    }
+    if (g->slot_bad[j]) {
+        g->failed_mask = mask_of_ranks(g, g->slot_bad[j]);
+        return fail(MIRT_E_PEER, "frame " + std::to_string(index) + ": the transfer of rank(s) " +
+                                     ranks_text(g->failed_mask) + " is missing or inconsistent (frame skipped)");
+    }
+    memset(out, 0, sizeof(*out));
+    out->rgb8 = g->hfb[j].rgb8;
+    out->valid = g->hfb[j].valid;
     return MIRT_OK;
 }
 

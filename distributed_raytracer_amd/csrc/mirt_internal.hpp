@@ -248,16 +248,33 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
-struct RectJobs {  // k_pack_rect / k_unpack_rect: per frame of a batch
-    const uint32_t* src[kMaxFrames];  // pack: the rgbv plane; unpack: the gathered regions
+struct RectJobs {  // k_pack_rect / k_unpack_rect / k_check_regions: per frame of a batch
+    const uint32_t* src[kMaxFrames];  // pack: the rgbv plane; unpack/check: the gathered regions
     uint32_t* dst[kMaxFrames];        // pack: the transfer buffer
     OutPlanes out[kMaxFrames];        // unpack: the framebuffer
     uint32_t rect[kMaxFrames][4];     // hit rectangle x0, y0, x1, y1 (half-open)
+    uint32_t tag[kMaxFrames];         // the frame's trailer tag (transfer_tag of its index)
+    uint8_t* bad[kMaxFrames];         // check: one byte per region, 1 = trailer missing or wrong
+};
+// Every transfer buffer ends with a two-word trailer written by k_pack_rect right after
+// the data: {tag of the frame, words of data}.  The root checks it in every gathered
+// region before the unpack, so a transfer of the wrong size, a stale one or one that never
+// arrived fails loudly (mirt_group: MIRT_E_PEER naming the rank) instead of corrupting the
+// frame.
+constexpr uint32_t kTrailerWords = 2;
+__host__ __device__ constexpr uint32_t transfer_tag(uint64_t frame) {
+    return 0x6d697274u ^ (uint32_t)(frame * 0x9e3779b1u) ^ (uint32_t)(frame >> 32);
+}
+// One rank's region of the gathered plane: its tiles are d_unpack[first, first + count).
+struct RegionDesc {
+    uint32_t first, count;
 };
 hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
                             hipStream_t s);
 hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, uint64_t cap,
                               const RectJobs& jobs, uint32_t nframes, hipStream_t s);
+hipError_t launch_check_regions(const TileDesc* tiles, const RegionDesc* regions, uint32_t nregions, uint64_t stride,
+                                const RectJobs& jobs, uint32_t nframes, hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);
 

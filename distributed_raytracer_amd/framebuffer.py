@@ -404,7 +404,7 @@ class NativeFrameGroup:
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 8,
                  inflight: int = 4, group=None, with_rgb: bool = False, tile_h: Optional[int] = 0,
-                 batch: int = 1):
+                 batch: int = 1, emulate: int = 0, host_output: bool = False, timeout_ms: int = 0):
         import torch
         self.ctx, self.W, self.H, self.rank, self.world = ctx, W, H, rank, world
         self.F = max(1, int(inflight))
@@ -438,14 +438,54 @@ class NativeFrameGroup:
                                           C.byref(self._h)))
         if self.B > 1:
             L.check(L.lib().mirt_group_set_batch(self._h, self.B))
+        if emulate and emulate > 1:
+            # one GPU traces every rank's share of an `emulate`-way deal and runs the whole
+            # pack -> transfer -> trailer check -> unpack chain (mirt_group_emulate)
+            L.check(L.lib().mirt_group_emulate(self._h, int(emulate)))
+        self.emulated = int(emulate or 0)
+        if host_output:
+            L.check(L.lib().mirt_group_set_host_output(self._h, 1))
+        if timeout_ms:
+            L.check(L.lib().mirt_group_set_timeout(self._h, int(timeout_ms)))
         self._k = 0
         self._idx = C.c_uint64()
 
-    def render(self, frame_and_keep) -> None:
-        """Enqueue the next frame (no host sync, no Python collective)."""
+    def render(self, frame_and_keep) -> int:
+        """Enqueue the next frame (no host sync, no Python collective); returns its index."""
         fr, _keep = frame_and_keep
         L.check(L.lib().mirt_trace_frame(self._h, C.byref(fr), C.byref(self._idx)))
         self._k += 1
+        return int(self._idx.value)
+
+    def wait(self) -> None:
+        """Host wait for every enqueued frame (deadline-bounded with timeout_ms); raises
+        MirtError MIRT_E_PEER / MIRT_E_TIMEOUT naming the failed frame and ranks."""
+        L.check(L.lib().mirt_group_wait(self._h, None))
+
+    def host_frame(self, index: int):
+        """(rgb8 (W*H, 3), valid (W*H,)) numpy copies of frame `index` from the group's
+        pinned host planes (host_output=True): the frame after its D2H."""
+        out = L.Outputs()
+        L.check(L.lib().mirt_group_frame_host(self._h, int(index), C.byref(out)))
+        n = self.W * self.H
+        rgb8 = np.ctypeslib.as_array(C.cast(out.rgb8, C.POINTER(C.c_uint8)), shape=(n * 3,)).reshape(n, 3).copy()
+        valid = np.ctypeslib.as_array(C.cast(out.valid, C.POINTER(C.c_uint8)), shape=(n,)).copy()
+        return rgb8, valid
+
+    def failed_ranks(self) -> List[int]:
+        m = C.c_uint64()
+        L.lib().mirt_group_failed_ranks(self._h, C.byref(m))
+        return [r for r in range(64) if (m.value >> r) & 1]
+
+    def drop(self, ranks: Sequence[int]) -> None:
+        """Fault injection (emulated world): these ranks' transfers stop arriving."""
+        L.check(L.lib().mirt_group_emulate_drop(self._h, sum(1 << r for r in ranks)))
+
+    def exclude(self, alive: Sequence[int], new_unique_id: Optional[bytes] = None) -> None:
+        """Re-deal over the ranks in `alive` (rank 0 included) after a failure."""
+        uid = (C.c_uint8 * 128)(*new_unique_id) if new_unique_id else None
+        L.check(L.lib().mirt_group_exclude(self._h, sum(1 << r for r in alive),
+                                           C.cast(uid, C.c_void_p) if uid is not None else None))
 
     def flush(self) -> None:
         """torch's current stream waits for every enqueued frame (gathers and unpacks included)."""

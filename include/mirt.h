@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 3
+#define MIRT_ABI_VERSION 4
 
 /* error codes */
 #define MIRT_OK 0
@@ -43,6 +43,8 @@ extern "C" {
 #define MIRT_E_CAMERA (-5)    /* camera dir parallel to the global up vector (camera.go:37) */
 #define MIRT_E_CANCELLED (-6) /* *cancel became non-zero (worker/distributed/main.go:73) */
 #define MIRT_E_IO (-7)        /* scene / OBJ / MTL file could not be read or parsed */
+#define MIRT_E_TIMEOUT (-8)   /* a frame group wait passed its deadline (mirt_group_set_timeout) */
+#define MIRT_E_PEER (-9)      /* a rank's transfer is missing or inconsistent (mirt_group_failed_ranks) */
 
 #define MIRT_MAX_OBJECTS 16
 #define MIRT_MAX_LIGHTS 16
@@ -283,7 +285,8 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
  * of its own, frames in issue order) gathers the planes to rank 0, and rank 0 unpacks them
  * into the frame's framebuffer.  `inflight` frames overlap, frame k on stream k % inflight
  * with framebuffer fbs[k % inflight] (rank 0 only; device planes of W x H pixels; the
- * planes a caller leaves NULL are not produced).  world == 1 with tile == 0 traces the
+ * planes a caller leaves NULL are not produced; with tile > 0 only rgb8, valid and rgbv can
+ * be produced — rgb, face or object planes are rejected).  world <= 64.  world == 1 with tile == 0 traces the
  * whole screen straight into the framebuffer (no tiles, no RCCL); world == 1 with tile > 0
  * rehearses the tiled path on one GPU.
  *   mirt_group_unique_id: rank 0 makes the RCCL id (128 bytes) every rank passes in.
@@ -303,6 +306,53 @@ int mirt_group_set_batch(mirt_group *g, uint32_t frames_per_launch);
 int mirt_trace_frame(mirt_group *group, const mirt_frame *frame, uint64_t *index);
 int mirt_group_wait(mirt_group *group, void *stream);
 void mirt_group_destroy(mirt_group *group);
+
+/*
+ * Transfer integrity.  Every rank's transfer ends with a two-word trailer {frame tag, words};
+ * the root checks it in every gathered region before the unpack.  A region whose trailer is
+ * missing, stale or at the wrong place (a rank that did not send, sent another frame or
+ * computed another size) makes the frame fail: mirt_group_wait / mirt_group_frame_host
+ * return MIRT_E_PEER naming the frame and the rank(s) — the reference master skips such a
+ * frame (master/main.go:153-161).  At creation (world > 1) every rank's view of the group
+ * (W, H, tile, tile_h, world, inflight, the deal) is compared with the root's over RCCL;
+ * a disagreement fails mirt_group_create on every rank with MIRT_E_PEER.
+ */
+/* Deadline of every host wait of the group, in ms (0: none, the default).  A wait past it
+ * returns MIRT_E_TIMEOUT; the root then reads the trailers of the stuck frames to name the
+ * ranks whose transfers never arrived (mirt_group_failed_ranks), and the group accepts no
+ * frame until mirt_group_exclude.  Stream waits (mirt_group_wait with a stream) have none. */
+int mirt_group_set_timeout(mirt_group *g, uint32_t ms);
+/* Bit r of *mask: rank r failed the last failing call.  Returns the number of such ranks. */
+int mirt_group_failed_ranks(const mirt_group *g, uint64_t *mask);
+/* Re-deal over the ranks still alive (bit r of alive = rank r stays; rank 0 must): the
+ * analogue of the pool removing a worker whose heartbeat failed (master/pool/pool.go:224-260)
+ * and the next frame being partitioned over the remaining workers (master/main.go:96-101).
+ * Every surviving rank calls it with the same mask.  The communicator is shrunk
+ * (ncclCommShrink with abort) or, if new_unique_id is non-NULL, rebuilt from that id (rank 0
+ * makes it with mirt_group_unique_id and the caller distributes it).  Frames not yet waited
+ * for are dropped; frame indices continue. */
+int mirt_group_exclude(mirt_group *g, uint64_t alive, const uint8_t *new_unique_id);
+/* Correctness mode of the tiled path on ONE GPU (world == 1, tile > 0, before the first
+ * frame): the group traces every rank's share of a `world`-way deal into that rank's own
+ * rgbv plane, packs it into that rank's transfer buffer exactly as a peer does, copies the
+ * bytes an RCCL send would carry into the root's gathered region, checks the trailers and
+ * unpacks every region: the N-GPU frame assembly, bit for bit, without RCCL. */
+int mirt_group_emulate(mirt_group *g, uint32_t world);
+/* Fault injection in an emulated world: the transfers of these ranks (bit r = rank r, never
+ * rank 0) are not copied, as if those ranks stopped answering. */
+int mirt_group_emulate_drop(mirt_group *g, uint64_t ranks);
+
+/*
+ * Host output (root): after each frame the assembled rgb8 + valid framebuffer is copied to
+ * pinned host memory on the frame's stream (the region the frame's hit rectangle and the
+ * slot's previous one cover; every other pixel is a miss, i.e. zero), so a frame completes
+ * only once it is in host memory (ms/frame includes the D2H).
+ * mirt_group_frame_host waits for frame `index` (within the deadline) and returns its host
+ * planes (rgb8 and valid, column-major x*H + y, owned by the group, valid until frame
+ * index + inflight is enqueued); MIRT_E_PEER if the frame failed.
+ */
+int mirt_group_set_host_output(mirt_group *g, int enable);
+int mirt_group_frame_host(mirt_group *g, uint64_t index, mirt_outputs *out);
 /* The deal mirt_group uses (world > 1): as mirt_plan_tiles, with rank 0 (which also unpacks
  * every frame) taking b - 1 of every L = b N - 1 deal slots and the other ranks b each,
  * b = round(32 / N) (N = 8: 3 and 4 of 31). */

@@ -102,3 +102,14 @@ def gpu_env(ctx, sc: PyScene):
     mut = rt.EnvMutables([rt.SceneObject(ids[mi], pos) for mi, pos in sc.objects],
                          [rt.Light(tuple(p), tuple(c)) for p, c in sc.lights], cam)
     return rt.Environment(ctx, ids, mut, [])
+
+
+def with_camera(scene: PyScene, pos, direction, fov=None) -> PyScene:
+    """A shallow copy of `scene` seen from another camera (the oracle takes the camera from
+    the scene; the GPU side from rt.Camera.new with the same values)."""
+    import copy
+    sc = copy.copy(scene)
+    sc.cam_pos, sc.cam_dir = tuple(float(x) for x in pos), tuple(float(x) for x in direction)
+    if fov is not None:
+        sc.fov = float(fov)
+    return sc

@@ -1,0 +1,182 @@
+"""configs[2] frame assembly, bit for bit, on one GPU (the reference's
+master gathers BulkTrace rectangles and draws them, master/main.go:130-176).
+
+mirt_group_emulate makes a world == 1 frame group trace EVERY rank's share of an N-way
+deal (mirt_group_plan_tiles, the root weighted down), pack each share into that rank's
+transfer buffer with the same k_pack_rect offsets a peer uses, copy exactly the bytes an
+RCCL send would carry into the root's gathered region, check every region's trailer and
+unpack all N regions.  Every pixel of every 1920x1080 frame is compared with the oracle
+(rtreego-style R-tree restatement, oracle/rt_oracle.c).  Also: the bench's own whole-screen
+path (2 frames per launch) on full frames, the host output (D2H) of assembled frames, and
+the fault path (a rank stops answering -> MIRT_E_PEER naming it -> re-deal over the
+survivors -> exact frames again)."""
+import numpy as np
+import pytest
+
+from conftest import SCENE
+
+W, H = 1920, 1080
+C0 = np.array([1.0, 1.0, -1.0])  # suzanne's position in example/scene.json
+
+
+def _cameras(base):
+    c = base.cam
+    return {
+        "default": (tuple(c.pos), tuple(c.forward), c.fov),
+        "away": (tuple(c.pos), tuple(-np.asarray(c.forward)), c.fov),  # empty hit rectangle
+        "edge": (tuple(C0 + [3.0, 0.5, 3.0]), (-0.2, -0.1, -1.0), 0.9),  # object cut by the screen edge
+        "inside": (tuple(C0 + [0.0, 0.0, 0.1]), (0.0, 0.0, -1.0), 1.2),  # camera inside the bounding box
+    }
+
+
+@pytest.fixture(scope="module")
+def views(env, py_scene):
+    """name -> (frame for the GPU, oracle frame) for the four cameras."""
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from scenes import with_camera
+    base = env.mutable()
+    out = {}
+    for name, (pos, d, fov) in _cameras(base).items():
+        mut = rt.EnvMutables(base.objects, base.lights, rt.Camera.new(pos, d, fov))
+        ref = Oracle(with_camera(py_scene, pos, d, fov), use_rtree=True).frame(W, H, nthreads=16)
+        out[name] = (mut.to_frame(), ref)
+    assert out["away"][1]["valid"].sum() == 0 and out["edge"][1]["valid"].sum() > 0
+    assert out["default"][1]["valid"].sum() == 209584
+    return out
+
+
+def _check(got_valid, got_rgb8, ref, what):
+    assert np.array_equal(got_valid, ref["valid"]), f"{what}: valid differs in {(got_valid != ref['valid']).sum()} px"
+    assert np.array_equal(got_rgb8, ref["rgb8"]), f"{what}: rgb8 differs in {(got_rgb8 != ref['rgb8']).any(1).sum()} px"
+
+
+ORDER = ["default", "edge", "away", "inside", "default", "inside", "edge", "default"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,tile,tile_h,batch", [
+    (2, 8, 0, 1), (4, 8, 0, 1), (8, 8, 0, 1), (2, 8, 0, 4), (4, 8, 0, 4), (8, 8, 0, 4), (4, 32, 32, 2)])
+def test_emulated_world_full_frames(ctx, views, world, tile, tile_h, batch):
+    """N = 2, 4, 8 ranks (8-px strips, the bench's deal; and 32x32 tiles), one or several
+    frames per launch, cameras alternating between the default view, an edge cut, a turned
+    away camera (empty transfers) and one inside the box: every framebuffer equals the
+    oracle on every pixel."""
+    import torch
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    F = 4
+    g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=F, tile_h=tile_h, batch=batch, emulate=world)
+    try:
+        for name in ORDER:
+            g.render(views[name][0])
+        g.wait()
+        torch.cuda.synchronize()
+        for k in range(len(ORDER) - F, len(ORDER)):
+            got = g.frames[k % F]
+            _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[ORDER[k]][1],
+                   f"world {world} frame {k} ({ORDER[k]})")
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
+def test_bench_path_full_frame(ctx, views):
+    """The bench's own configuration (whole screen, 8 frames in flight, 2 frames per
+    k_trace launch, frame records staged per launch): every pixel of each frame, valid,
+    rgb8, and the fp64 colour of tracer.Trace (with_rgb)."""
+    import torch
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    for with_rgb in (False, True):
+        g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=8, batch=2, with_rgb=with_rgb)
+        try:
+            for name in ORDER:
+                g.render(views[name][0])
+            g.wait()
+            torch.cuda.synchronize()
+            for k, name in enumerate(ORDER):
+                got, ref = g.frames[k % 8], views[name][1]
+                _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), ref, f"frame {k} ({name})")
+                if with_rgb:
+                    assert np.array_equal(got.rgb.cpu().numpy(), ref["rgb"]), f"frame {k} ({name}): rgb differs"
+        finally:
+            g.close()
+            ctx.set_grid()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile,emulate", [(None, 0), (8, 8)])
+def test_host_output_frames(ctx, views, tile, emulate):
+    """mirt_group_set_host_output: the assembled frame lands in pinned host memory (only the
+    hit rectangle and the previous one are copied); the host planes equal the oracle on
+    every pixel while the rectangle moves and empties between frames."""
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=2, batch=1, emulate=emulate, host_output=True)
+    try:
+        prev = None
+        for name in ORDER:
+            idx = g.render(views[name][0])
+            if prev is not None:
+                rgb8, valid = g.host_frame(prev[0])
+                _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+            prev = (idx, name)
+        rgb8, valid = g.host_frame(prev[0])
+        _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+        g.wait()
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
+def test_peer_failure_is_named_and_redealt(ctx, views):
+    """A rank that stops answering (emulated: its transfers are dropped) fails the frame
+    with MIRT_E_PEER naming that rank — the master skips such frames, master/main.go:153-161
+    — and after mirt_group_exclude the survivors' re-deal gives exact frames again (the pool
+    drops the worker, master/pool/pool.go:224-260)."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib as L
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    g = NativeFrameGroup(ctx, W, H, 0, 1, 8, inflight=2, batch=1, emulate=4, timeout_ms=20000)
+    try:
+        g.render(views["default"][0])
+        g.wait()
+        _check(g.frames[0].valid.cpu().numpy(), g.frames[0].rgb8.cpu().numpy(), views["default"][1], "before")
+        g.drop([2])
+        g.render(views["edge"][0])
+        with pytest.raises(rt.MirtError) as e:
+            g.wait()
+        assert e.value.code == L.MIRT_E_PEER and "rank(s) 2" in str(e.value)
+        assert g.failed_ranks() == [2]
+        g.exclude([0, 1, 3])
+        for k, name in enumerate(["edge", "default", "inside"]):
+            g.render(views[name][0])
+            g.wait()
+            torch.cuda.synchronize()
+            got = g.frames[(2 + k) % 2]
+            _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[name][1], f"after re-deal ({name})")
+        assert g.failed_ranks() == []
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
+def test_group_argument_errors(ctx):
+    """Tiled groups cannot produce the fp64 colour plane; emulation needs world == 1 and a
+    tile; the root cannot be dropped or excluded."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib as L
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    with pytest.raises(rt.MirtError):
+        NativeFrameGroup(ctx, 64, 48, 0, 1, 8, inflight=2, with_rgb=True)
+    with pytest.raises(rt.MirtError):
+        NativeFrameGroup(ctx, 64, 48, 0, 1, None, inflight=2, emulate=4)
+    g = NativeFrameGroup(ctx, 64, 48, 0, 1, 8, inflight=2, emulate=2)
+    try:
+        assert L.lib().mirt_group_emulate_drop(g._h, 1) == L.MIRT_E_INVALID
+        assert L.lib().mirt_group_exclude(g._h, 2, None) == L.MIRT_E_INVALID
+    finally:
+        g.close()
+        ctx.set_grid()

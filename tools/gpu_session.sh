@@ -1,0 +1,30 @@
+#!/bin/bash
+# One gpurun session: GPU tests, the driver's bench command, a launch-shape sweep and the
+# profile of the driver's command.  Stops at the first step that crashes, hangs or times
+# out (rc other than 0 / 1); a step whose tests merely fail lets the session go on.
+#   tools/gpu_session.sh OUTDIR [steps...]   steps: tests bench sweep profile
+set -u
+OUT=${1:-gpurun_out/session}; shift
+mkdir -p "$OUT"
+STEPS=${*:-"tests bench sweep profile"}
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -4 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
+}
+for s in $STEPS; do
+  case $s in
+    tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    bench) step bench 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench500) step bench500 300 python3 bench.py --gpus 1 --no-cpu-baseline ;;
+    sweep) step sweep 900 tools/shape_sweep.sh 20 5 ;;
+    profile) step profile 900 tools/profile_cmd.sh ${PROF_TAG:-r02} ;;
+    smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "session done"
