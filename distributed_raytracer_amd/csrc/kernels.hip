@@ -1992,6 +1992,34 @@ hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t m
     return hipGetLastError();
 }
 
+// Bytes [a, b) of src -> dst with the same alignment on both sides (same layout): head
+// bytes, 16-byte words, tail bytes; one workgroup.
+__device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t a,
+                                          uint64_t b) {
+    const uint64_t a16 = min(b, (a + 15) & ~15ull), b16 = max(a16, b & ~15ull);
+    for (uint64_t i = a + threadIdx.x; i < a16; i += blockDim.x) dst[i] = src[i];
+    for (uint64_t i = a16 + 16 * threadIdx.x; i < b16; i += 16 * blockDim.x)
+        *(uint4*)(dst + i) = *(const uint4*)(src + i);
+    for (uint64_t i = b16 + threadIdx.x; i < b; i += blockDim.x) dst[i] = src[i];
+}
+// grid x: columns of the rectangle, z: frame.  Column x holds rows [y0, y1) contiguously
+// in both planes (column-major x * H + y).
+__global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint32_t H) {
+    const uint32_t f = blockIdx.z;
+    const uint32_t* R = jobs.rect[f];
+    for (uint32_t x = R[0] + blockIdx.x; x < R[2]; x += gridDim.x) {
+        const uint64_t p0 = (uint64_t)x * H + R[1], p1 = (uint64_t)x * H + R[3];
+        if (jobs.rgb8[f]) copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1);
+        if (jobs.valid[f]) copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1);
+    }
+}
+hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
+                                 hipStream_t s) {
+    const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(max_cols, 2048));
+    hipLaunchKernelGGL(k_copy_rect_host, dim3(gx, 1, nframes), dim3(256), 0, s, jobs, H);
+    return hipGetLastError();
+}
+
 // Copy a launch's frame records from pinned host memory to the device (one workgroup; a
 // hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there).
 __global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,

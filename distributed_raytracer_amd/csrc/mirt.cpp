@@ -1775,8 +1775,9 @@ int group_handshake(mirt_group* g) {
 
 // Device -> host copy of a frame's framebuffer: the union of this frame's hit rectangle
 // and the one last copied into that host slot (outside the rectangle every pixel is a
-// miss, i.e. zero, so the host planes stay exact).
-int host_copy(mirt_group* g, uint32_t j, const uint32_t R[4], hipStream_t s) {
+// miss, i.e. zero, so the host planes stay exact).  Stages the frame's job; the batch's
+// copies run as one k_copy_rect_host launch storing straight into pinned host memory.
+void host_copy_job(mirt_group* g, uint32_t j, const uint32_t R[4], HostCopyJobs& jobs, uint32_t i, uint32_t& max_cols) {
     HostFrame& hf = g->hfb[j];
     const OutPlanes& d = g->fb[j];
     uint32_t u[4] = {R[0], R[1], R[2], R[3]};
@@ -1789,14 +1790,13 @@ int host_copy(mirt_group* g, uint32_t j, const uint32_t R[4], hipStream_t s) {
         u[3] = std::max(u[3], hf.rect[3]);
     }
     memcpy(hf.rect, R, sizeof(hf.rect));
-    if (u[0] >= u[2] || u[1] >= u[3]) return MIRT_OK;
-    const size_t off = (size_t)u[0] * g->H + u[1], rows = u[3] - u[1], cols = u[2] - u[0];
-    if (d.rgb8)
-        HIP_TRY(hipMemcpy2DAsync(hf.rgb8 + 3 * off, (size_t)g->H * 3, d.rgb8 + 3 * off, (size_t)g->H * 3, rows * 3, cols,
-                                 hipMemcpyDeviceToHost, s));
-    if (d.valid)
-        HIP_TRY(hipMemcpy2DAsync(hf.valid + off, g->H, d.valid + off, g->H, rows, cols, hipMemcpyDeviceToHost, s));
-    return MIRT_OK;
+    if (u[0] >= u[2] || u[1] >= u[3]) u[0] = u[1] = u[2] = u[3] = 0;  // nothing to copy
+    jobs.rgb8[i] = d.rgb8;
+    jobs.valid[i] = d.valid;
+    jobs.hrgb8[i] = hf.rgb8;
+    jobs.hvalid[i] = hf.valid;
+    memcpy(jobs.rect[i], u, sizeof(u));
+    max_cols = std::max(max_cols, u[2] - u[0]);
 }
 
 }  // namespace
@@ -2162,11 +2162,12 @@ static int group_flush(mirt_group* g) {
         if (!g->rehearse) HIP_TRY(launch_check_regions(g->d_unpack, g->d_regions, P, g->stride, jobs, n, s));
         HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->stride, jobs, n, s));
     }
-    if (g->host_out && is_root)
-        for (uint32_t i = 0; i < n; ++i) {
-            int r = host_copy(g, g->bj[i], br.rect[i], s);
-            if (r != MIRT_OK) return r;
-        }
+    if (g->host_out && is_root) {
+        HostCopyJobs hj{};
+        uint32_t cols = 0;
+        for (uint32_t i = 0; i < n; ++i) host_copy_job(g, g->bj[i], br.rect[i], hj, i, cols);
+        if (cols) HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, s));
+    }
     HT(5);
     HIP_TRY(hipEventRecord(g->ev_done[bs], s));
     HT(6);

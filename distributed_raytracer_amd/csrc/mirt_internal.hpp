@@ -269,6 +269,17 @@ __host__ __device__ constexpr uint32_t transfer_tag(uint64_t frame) {
 struct RegionDesc {
     uint32_t first, count;
 };
+// Device framebuffer -> pinned host framebuffer, the pixels of one rectangle per frame
+// (mirt_group_set_host_output): the kernel stores straight into host memory over PCIe.
+struct HostCopyJobs {
+    const uint8_t* rgb8[kMaxFrames];
+    const uint8_t* valid[kMaxFrames];
+    uint8_t* hrgb8[kMaxFrames];
+    uint8_t* hvalid[kMaxFrames];
+    uint32_t rect[kMaxFrames][4];  // x0, y0, x1, y1 (half-open)
+};
+hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
+                                 hipStream_t s);
 hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
                             hipStream_t s);
 hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, uint64_t cap,

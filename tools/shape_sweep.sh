@@ -2,7 +2,7 @@
 # Launch-shape sweep of the bench (frames in flight F x frames per launch B) at a given
 # run length; one JSON summary line per shape on stdout:  tools/shape_sweep.sh 20 5 [bench args]
 STEPS=${1:-20}; WARM=${2:-5}; shift 2 || true
-for fb in ${SHAPES:-"2,1 2,2 4,1 4,2 4,4 8,2 8,4 8,8 16,4 16,8"}; do
+for fb in ${SHAPES:-2,1 2,2 4,1 4,2 4,4 8,2 8,4 8,8 16,4 16,8}; do
   F=${fb%,*}; B=${fb#*,}
   LOG=/tmp/sweep_${F}_${B}.log
   timeout -k 10 120 python3 bench.py --steps "$STEPS" --warmup "$WARM" --inflight "$F" --batch "$B" \
