@@ -253,19 +253,18 @@ def main():
         return NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
                                 tile_h=a.tile_h, batch=a.batch, host_output=host_output and rank == 0)
 
-    sh = sh_dev = None
+    sh = None
     err = ""
     if sharder == "native":
         try:
             sh = native_group(d2h)
-            sh_dev = native_group(False) if d2h else None
         except Exception as e:  # noqa: BLE001 — reported in the JSON line, then the torch path runs
             err = str(e)
     if world > 1 and sharder == "native":
         ok = torch.tensor([0.0 if sh is None else 1.0], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() < 1.0:
-            sh = sh_dev = None
+            sh = None
             err = err or "another rank could not create its native group"
     if sharder == "native" and sh is None:
         print(f"native frame group unavailable ({err}); using the torch.distributed sharder", file=sys.stderr)
@@ -286,11 +285,10 @@ def main():
     stream = torch.cuda.Stream(dev)
     host_last = None
     with torch.cuda.stream(stream):
-        for g in ([sh] + ([sh_dev] if sh_dev is not None else [])):
-            for _ in range(a.warmup):
-                g.render(frame)
-            g.flush()
-            count("warmup", a.warmup)
+        for _ in range(a.warmup):
+            sh.render(frame)
+        sh.flush()
+        count("warmup", a.warmup)
         torch.cuda.synchronize(dev)
 
         # timed region: K frames from an empty pipeline to the last one in host memory
@@ -310,17 +308,21 @@ def main():
 
         # the same frames without the D2H (device-resident outputs)
         dev_elapsed = None
-        if sh_dev is not None:
+        if d2h:
+            if rank == 0:
+                sh.set_host_output(False)
             barrier()
             torch.cuda.synchronize(dev)
             d0 = time.perf_counter()
             for _ in range(a.steps):
-                sh_dev.render(frame)
-            sh_dev.flush()
+                sh.render(frame)
+            sh.flush()
             torch.cuda.synchronize(dev)
             barrier()
             dev_elapsed = time.perf_counter() - d0
             count("device_only", a.steps)
+            if rank == 0:
+                sh.set_host_output(True)
 
         # profiled region: HIP events around every k_trace launch + device counters
         ctx.profile_enable(True)

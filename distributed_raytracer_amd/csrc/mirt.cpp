@@ -1446,6 +1446,7 @@ struct mirt_group {
     bool rehearse = false;              // MIRT_GROUP_REHEARSE diagnostic (timing only: no checks)
     bool skip_unpack = false;
     bool host_out = false;
+    bool d2h_sdma = false;              // MIRT_D2H=sdma: copy-engine column ranges (default: zero-copy kernel)
     std::vector<HostFrame> hfb;
     // frames and batches
     uint32_t B = 1, FB = 1;
@@ -1909,6 +1910,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->tile = tile;
     g->tile_h = tile_h;
     g->tiled = tile > 0;
+    const char* d2h = getenv("MIRT_D2H");
+    g->d2h_sdma = d2h && !strcmp(d2h, "sdma");
     // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
     // N-way deal (MIRT_GROUP_REHEARSE_RANK, default 0) and unpack all N regions, the others
     // stale: the root's per-frame GPU work at N GPUs without the transfers.  Results are
@@ -1993,11 +1996,22 @@ int mirt_group_failed_ranks(const mirt_group* g, uint64_t* mask) {
     return __builtin_popcountll(g->failed_mask);
 }
 
+static int group_flush(mirt_group* g);
+
 int mirt_group_set_host_output(mirt_group* g, int enable) {
     if (!g) return fail(MIRT_E_INVALID, "NULL group");
-    if (g->k != 0) return fail(MIRT_E_INVALID, "set the host output before the first frame");
     if (g->rank != 0) return fail(MIRT_E_INVALID, "only the root holds framebuffers");
     HIP_TRY(hipSetDevice(g->c->device));
+    int r = group_flush(g);  // the open batch keeps the setting it was staged with
+    if (r != MIRT_OK) return r;
+    // frames traced while the output was off never reached the host planes: the next copy
+    // into each slot covers the whole screen
+    if (enable && !g->host_out)
+        for (HostFrame& hf : g->hfb) {
+            hf.rect[0] = hf.rect[1] = 0;
+            hf.rect[2] = g->W;
+            hf.rect[3] = g->H;
+        }
     g->host_out = enable != 0;
     if (g->host_out && g->hfb.empty()) {
         g->hfb.assign(g->F, HostFrame());
@@ -2166,7 +2180,20 @@ static int group_flush(mirt_group* g) {
         HostCopyJobs hj{};
         uint32_t cols = 0;
         for (uint32_t i = 0; i < n; ++i) host_copy_job(g, g->bj[i], br.rect[i], hj, i, cols);
-        if (cols) HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, s));
+        if (cols && g->d2h_sdma) {
+            // the copy engine: the whole columns of each rectangle, one contiguous range per plane
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t* u = hj.rect[i];
+                if (u[0] >= u[2]) continue;
+                const size_t p0 = (size_t)u[0] * g->H, np = (size_t)(u[2] - u[0]) * g->H;
+                if (hj.rgb8[i])
+                    HIP_TRY(hipMemcpyAsync(hj.hrgb8[i] + 3 * p0, hj.rgb8[i] + 3 * p0, 3 * np, hipMemcpyDeviceToHost, s));
+                if (hj.valid[i])
+                    HIP_TRY(hipMemcpyAsync(hj.hvalid[i] + p0, hj.valid[i] + p0, np, hipMemcpyDeviceToHost, s));
+            }
+        } else if (cols) {
+            HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, s));
+        }
     }
     HT(5);
     HIP_TRY(hipEventRecord(g->ev_done[bs], s));

@@ -472,6 +472,10 @@ class NativeFrameGroup:
         valid = np.ctypeslib.as_array(C.cast(out.valid, C.POINTER(C.c_uint8)), shape=(n,)).copy()
         return rgb8, valid
 
+    def set_host_output(self, enable: bool) -> None:
+        """Copy frames enqueued from now on to pinned host memory (or stop)."""
+        L.check(L.lib().mirt_group_set_host_output(self._h, 1 if enable else 0))
+
     def failed_ranks(self) -> List[int]:
         m = C.c_uint64()
         L.lib().mirt_group_failed_ranks(self._h, C.byref(m))

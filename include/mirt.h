@@ -349,7 +349,8 @@ int mirt_group_emulate_drop(mirt_group *g, uint64_t ranks);
  * only once it is in host memory (ms/frame includes the D2H).
  * mirt_group_frame_host waits for frame `index` (within the deadline) and returns its host
  * planes (rgb8 and valid, column-major x*H + y, owned by the group, valid until frame
- * index + inflight is enqueued); MIRT_E_PEER if the frame failed.
+ * index + inflight is enqueued); MIRT_E_PEER if the frame failed.  The setting may change
+ * between frames; it applies to frames enqueued after the call.
  */
 int mirt_group_set_host_output(mirt_group *g, int enable);
 int mirt_group_frame_host(mirt_group *g, uint64_t index, mirt_outputs *out);
