@@ -61,6 +61,7 @@ struct BNode {  // binary build node
 };
 
 struct Builder {
+    uint32_t leaf;  // max faces per leaf
     const std::vector<Box>& fbox;
     const std::vector<std::array<double, 3>>& ce;
     std::vector<uint32_t>& order;
@@ -76,7 +77,7 @@ struct Builder {
         const uint32_t cnt = end - begin;
         int idx = (int)nodes.size();
         nodes.push_back(n);
-        if (cnt <= (uint32_t)kBvhLeaf) {
+        if (cnt <= leaf) {
             nodes[idx].first = begin;
             nodes[idx].count = cnt;
             return idx;
@@ -144,7 +145,8 @@ inline float round_up(double x) {
 
 // v: nv*3 vertex array, fv: nf*3 indices.  inflate: absolute padding of every box
 // (applied in fp64, then rounded outward to fp32).
-inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, double inflate) {
+inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, double inflate,
+                          uint32_t leaf = (uint32_t)kBvhLeaf) {
     using namespace detail;
     BvhBuild out;
     out.order.resize(nf);
@@ -155,7 +157,7 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
         for (int c = 0; c < 3; ++c) fbox[f].grow(v + 3 * (size_t)fv[3 * f + c]);
         for (int k = 0; k < 3; ++k) ce[f][k] = 0.5 * (fbox[f].lo[k] + fbox[f].hi[k]);
     }
-    Builder b{fbox, ce, out.order, {}};
+    Builder b{std::max<uint32_t>(1, std::min<uint32_t>(leaf, 127)), fbox, ce, out.order, {}};
     if (nf == 0) {
         Bvh8Node root;
         for (int c = 0; c < 8; ++c) root.child[c] = kBvhEmpty;

@@ -512,7 +512,7 @@ bool frames_batchable(const FrameRec& a, const FrameRec& b) {
 }
 
 int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                  uint32_t bounces, hipStream_t s, const volatile int* cancel);
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now = 0);
 
 // Enqueue primary -> shadow -> shade for a tile list on stream s.
 int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
@@ -531,7 +531,7 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 // Launch the nf frames staged in sl->h_frames (k_trace: one launch for all of them; the
 // split kernels and reflections take one frame).
 int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                  uint32_t bounces, hipStream_t s, const volatile int* cancel) {
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now) {
     int r = MIRT_OK;
     if (nf == 0 || nf > kMaxFrames) return fail(MIRT_E_INVALID, "1..8 frames per launch");
     const bool one_launch = !(c->flags & MIRT_OPT_SPLIT_KERNELS) && !bounces;
@@ -558,6 +558,9 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         per_wg = std::max<uint32_t>(c->min_blocks_per_wg, 1);
         max_wg = c->max_workgroups ? std::min<uint64_t>(c->max_workgroups, (uint64_t)2 * c->cus) : (uint64_t)2 * c->cus;
     }
+    // a frame group that knows how many launches are still running sizes this one for the
+    // CUs they leave (a lone frame gets the whole chip)
+    if (max_wg_now) max_wg = std::min<uint64_t>(max_wg_now, (uint64_t)2 * c->cus);
     // at least min(blocks, CUs) workgroups: a small tile list (a BulkTrace order, one
     // rank's share) keeps one block per wave rather than queueing heavy blocks on few waves
     const uint64_t want = std::max<uint64_t>((total + per_wg - 1) / per_wg, std::min<uint64_t>(total, (uint64_t)c->cus));
@@ -793,7 +796,10 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     double scale = 0;
     for (size_t i = 0; i < (size_t)nv * 3; ++i) scale = std::max(scale, std::fabs(v[i]));
     scale = std::max(scale, 1e-30);
-    BvhBuild bvh = build_bvh(v, fv, nf, std::ldexp(scale, -12));
+    // MIRT_BVH_LEAF (experiments): faces per leaf, default kBvhLeaf
+    const char* leaf_env = getenv("MIRT_BVH_LEAF");
+    const uint32_t leaf = leaf_env && atoi(leaf_env) > 0 ? (uint32_t)atoi(leaf_env) : (uint32_t)kBvhLeaf;
+    BvhBuild bvh = build_bvh(v, fv, nf, std::ldexp(scale, -12), leaf);
     if (bvh.depth > (uint32_t)kBvhMaxDepth)
         return fail(MIRT_E_LIMIT, "BVH deeper than the traversal stack (" + std::to_string(bvh.depth) + " levels)");
     // P1, E1 = P2 - P1, E2 = P3 - P1 (triangle.go:38: single fp64 subtractions, so the
@@ -1447,6 +1453,7 @@ struct mirt_group {
     bool skip_unpack = false;
     bool host_out = false;
     bool d2h_sdma = false;              // MIRT_D2H=sdma: copy-engine column ranges (default: zero-copy kernel)
+    bool adaptive_grid = false;         // MIRT_ADAPTIVE_GRID=1: size each launch by the launches still running
     std::vector<HostFrame> hfb;
     // frames and batches
     uint32_t B = 1, FB = 1;
@@ -1912,6 +1919,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->tiled = tile > 0;
     const char* d2h = getenv("MIRT_D2H");
     g->d2h_sdma = d2h && !strcmp(d2h, "sdma");
+    const char* ag = getenv("MIRT_ADAPTIVE_GRID");
+    g->adaptive_grid = ag && atoi(ag) > 0;
     // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
     // N-way deal (MIRT_GROUP_REHEARSE_RANK, default 0) and unpack all N regions, the others
     // stale: the root's per-frame GPU work at N GPUs without the transfers.  Results are
@@ -2115,6 +2124,15 @@ static int group_flush(mirt_group* g) {
     // a sender reuses its packed planes only after their previous batch's sends are done (the
     // root's stream already waited for that gather before its unpacks)
     if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
+    // adaptive grid (MIRT_ADAPTIVE_GRID=1): the launches still running share the chip with
+    // this one, ~wg_factor x CUs workgroups between them
+    uint32_t max_wg_now = 0;
+    if (g->adaptive_grid) {
+        uint32_t running = 0;
+        for (uint64_t b = g->nb > g->FB ? g->nb - g->FB + 1 : 0; b < g->nb; ++b)
+            if (hipEventQuery(g->ev_done[b % g->FB]) == hipErrorNotReady) ++running;
+        max_wg_now = std::max<uint32_t>(1, (uint32_t)(4 * (uint64_t)c->cus / (running + 1)));
+    }
     for (Share& sh : g->shares) {
         Slot* sl = sh.slots[bs].get();
         for (uint32_t i = 0; i < n; ++i) {
@@ -2122,7 +2140,8 @@ static int group_flush(mirt_group* g) {
             sl->h_frames[i].out = g->tiled ? OutPlanes{nullptr, nullptr, nullptr, nullptr, nullptr, sh.packed[g->bj[i]]}
                                            : g->fb[g->bj[i]];
         }
-        int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr);
+        int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr,
+                              max_wg_now);
         if (r != MIRT_OK) {
             (void)hipStreamSynchronize(s);
             return r;
