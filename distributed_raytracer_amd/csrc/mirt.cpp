@@ -1314,9 +1314,11 @@ uint64_t tiles_pixels(const std::vector<mirt_tile>& t) {
     return n;
 }
 
-hipError_t stream_with_queue(int cus, hipStream_t* s) {
+// A stream on a hardware queue of its own whose kernels run on CUs [lo, hi) (default: all).
+hipError_t stream_with_queue(int cus, hipStream_t* s, int lo = 0, int hi = -1) {
+    if (hi < 0) hi = cus;
     std::vector<uint32_t> mask(((uint32_t)cus + 31) / 32, 0u);
-    for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    for (int i = lo; i < hi; ++i) mask[i / 32] |= 1u << (i % 32);
     return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
 }
 
@@ -1454,6 +1456,8 @@ struct mirt_group {
     bool host_out = false;
     bool d2h_sdma = false;              // MIRT_D2H=sdma: copy-engine column ranges (default: zero-copy kernel)
     bool adaptive_grid = false;         // MIRT_ADAPTIVE_GRID=1: size each launch by the launches still running
+    int d2h_cus = 0;                    // CUs reserved for the host copies (0: copies on the frame stream)
+    hipStream_t copy_stream = nullptr;
     std::vector<HostFrame> hfb;
     // frames and batches
     uint32_t B = 1, FB = 1;
@@ -1860,6 +1864,7 @@ void mirt_group_destroy(mirt_group* g) {
         for (hipStream_t s : g->streams)
             if (s) (void)hipStreamSynchronize(s);
         if (g->comm_stream) (void)hipStreamSynchronize(g->comm_stream);
+        if (g->copy_stream) (void)hipStreamSynchronize(g->copy_stream);
     }
     for (Share& sh : g->shares) {
         for (auto& sl : sh.slots) slot_free(sl.get());
@@ -1883,6 +1888,7 @@ void mirt_group_destroy(mirt_group* g) {
     for (hipStream_t s : g->streams)
         if (s) (void)hipStreamDestroy(s);
     if (g->comm_stream) (void)hipStreamDestroy(g->comm_stream);
+    if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
     if (g->probe_stream) (void)hipStreamDestroy(g->probe_stream);
     delete g;
 }
@@ -1935,13 +1941,19 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->ev_traced.assign(inflight, nullptr);
     g->ev_gathered.assign(inflight, nullptr);
     g->ev_done.assign(inflight, nullptr);
+    // host output on reserved CUs (MIRT_D2H_CUS=n): the trace kernels fill every CU's VGPR
+    // file, so a copy kernel sharing their CUs waits for a frame tail to start; n CUs kept
+    // for the copy stream let each frame's D2H run beside the next frames' traces
+    const char* dc = getenv("MIRT_D2H_CUS");
+    g->d2h_cus = dc ? std::min(std::max(atoi(dc), 0), c->cus / 2) : 0;
     for (uint32_t j = 0; j < inflight; ++j) {
-        HIP_TRY(stream_with_queue(c->cus, &g->streams[j]));
+        HIP_TRY(stream_with_queue(c->cus, &g->streams[j], 0, c->cus - g->d2h_cus));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&g->ev_comm, hipEventDisableTiming));
+    if (g->d2h_cus) HIP_TRY(stream_with_queue(c->cus, &g->copy_stream, c->cus - g->d2h_cus, c->cus));
     g->binfo.assign(inflight, BatchRec());
     g->slot_frame.assign(inflight, ~0ull);
     g->slot_bad.assign(inflight, 0);
@@ -2080,6 +2092,14 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
             return r;
         }
     }
+    if (g->copy_stream) {
+        HIP_TRY(hipEventRecord(g->ev_comm, g->copy_stream));
+        int r = group_wait_event(g, g->ev_comm, "draining the host copies");
+        if (r != MIRT_OK) {
+            g->timeout_ms = saved;
+            return r;
+        }
+    }
     g->timeout_ms = saved;
     std::vector<uint32_t> members;
     for (uint32_t q : keep) members.push_back(g->members[q]);
@@ -2210,6 +2230,15 @@ static int group_flush(mirt_group* g) {
                 if (hj.valid[i])
                     HIP_TRY(hipMemcpyAsync(hj.hvalid[i] + p0, hj.valid[i] + p0, np, hipMemcpyDeviceToHost, s));
             }
+        } else if (cols && g->copy_stream) {
+            // the batch's frames are final on stream s: copy them on the reserved CUs, and let
+            // the batch complete (ev_done) only once they are in host memory
+            HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
+            HIP_TRY(hipStreamWaitEvent(g->copy_stream, g->ev_traced[bs], 0));
+            HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, g->copy_stream));
+            HIP_TRY(hipEventRecord(g->ev_done[bs], g->copy_stream));
+            ++g->nb;
+            return MIRT_OK;
         } else if (cols) {
             HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, s));
         }
