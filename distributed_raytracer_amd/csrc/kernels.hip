@@ -2002,15 +2002,49 @@ __device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8
         *(uint4*)(dst + i) = *(const uint4*)(src + i);
     for (uint64_t i = b16 + threadIdx.x; i < b; i += blockDim.x) dst[i] = src[i];
 }
-// grid x: columns of the rectangle, z: frame.  Column x holds rows [y0, y1) contiguously
-// in both planes (column-major x * H + y).
+// grid x: columns, z: frame.  Column x holds rows contiguously in both planes (x * H + y).
+// The column's hit span is found from the valid plane inside this frame's hit rectangle;
+// the rows of its union with the span the host slot held are copied.
 __global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint32_t H) {
+    __shared__ uint32_t s_lo, s_hi;
     const uint32_t f = blockIdx.z;
     const uint32_t* R = jobs.rect[f];
+    const uint32_t* C = jobs.cur[f];
     for (uint32_t x = R[0] + blockIdx.x; x < R[2]; x += gridDim.x) {
-        const uint64_t p0 = (uint64_t)x * H + R[1], p1 = (uint64_t)x * H + R[3];
-        if (jobs.rgb8[f]) copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1);
-        if (jobs.valid[f]) copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1);
+        if (threadIdx.x == 0) {
+            s_lo = 0xffffffffu;
+            s_hi = 0;
+        }
+        __syncthreads();
+        if (x >= C[0] && x < C[2]) {
+            uint32_t lo = 0xffffffffu, hi = 0;
+            const uint8_t* v = jobs.valid[f] + (uint64_t)x * H;
+            for (uint32_t y = C[1] + threadIdx.x; y < C[3]; y += blockDim.x)
+                if (v[y]) {
+                    lo = min(lo, y);
+                    hi = max(hi, y + 1);
+                }
+            if (lo != 0xffffffffu) {
+                atomicMin(&s_lo, lo);
+                atomicMax(&s_hi, hi);
+            }
+        }
+        __syncthreads();
+        const uint32_t prev = jobs.spans[f][x];
+        const uint32_t a0 = prev & 0xffffu, b0 = prev >> 16;
+        const uint32_t a = s_lo, b = s_hi;  // empty: a > b
+        uint32_t u0 = a0, u1 = b0;
+        if (a < b) {
+            u0 = a0 < b0 ? min(a, a0) : a;
+            u1 = a0 < b0 ? max(b, b0) : b;
+        }
+        if (u0 < u1) {
+            const uint64_t p0 = (uint64_t)x * H + u0, p1 = (uint64_t)x * H + u1;
+            copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1);
+            copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1);
+        }
+        __syncthreads();  // every thread read the old span and s_lo/s_hi
+        if (threadIdx.x == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
     }
 }
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,

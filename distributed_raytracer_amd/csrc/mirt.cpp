@@ -1459,6 +1459,7 @@ struct mirt_group {
     int d2h_cus = 0;                    // CUs reserved for the host copies (0: copies on the frame stream)
     hipStream_t copy_stream = nullptr;
     std::vector<HostFrame> hfb;
+    uint32_t* d_spans = nullptr;        // host output: per frame slot and column, the hit span the host holds
     // frames and batches
     uint32_t B = 1, FB = 1;
     uint64_t nb = 0;                    // batches launched
@@ -1703,6 +1704,7 @@ int group_plan(mirt_group* g) {
         HIP_TRY(hipMemcpy(g->d_regions, rd.data(), rd.size() * sizeof(RegionDesc), hipMemcpyHostToDevice));
         if (g->h_bad_cap < (size_t)g->F * P) {
             if (g->h_bad) (void)hipHostFree(g->h_bad);
+    if (g->d_spans) (void)hipFree(g->d_spans);
             g->h_bad = nullptr;
             g->h_bad_cap = 0;
             HIP_TRY(hipHostMalloc((void**)&g->h_bad, (size_t)g->F * P));
@@ -1807,7 +1809,9 @@ void host_copy_job(mirt_group* g, uint32_t j, const uint32_t R[4], HostCopyJobs&
     jobs.valid[i] = d.valid;
     jobs.hrgb8[i] = hf.rgb8;
     jobs.hvalid[i] = hf.valid;
+    jobs.spans[i] = g->d_spans + (size_t)j * g->W;
     memcpy(jobs.rect[i], u, sizeof(u));
+    memcpy(jobs.cur[i], R, sizeof(jobs.cur[i]));
     max_cols = std::max(max_cols, u[2] - u[0]);
 }
 
@@ -1877,6 +1881,7 @@ void mirt_group_destroy(mirt_group* g) {
     if (g->d_unpack) (void)hipFree(g->d_unpack);
     if (g->d_regions) (void)hipFree(g->d_regions);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
+    if (g->d_spans) (void)hipFree(g->d_spans);
     for (HostFrame& hf : g->hfb) {
         if (hf.rgb8) (void)hipHostFree(hf.rgb8);
         if (hf.valid) (void)hipHostFree(hf.valid);
@@ -2027,15 +2032,31 @@ int mirt_group_set_host_output(mirt_group* g, int enable) {
     if (r != MIRT_OK) return r;
     // frames traced while the output was off never reached the host planes: the next copy
     // into each slot covers the whole screen
-    if (enable && !g->host_out)
+    if (enable && !g->host_out && !g->hfb.empty()) {
         for (HostFrame& hf : g->hfb) {
             hf.rect[0] = hf.rect[1] = 0;
             hf.rect[2] = g->W;
             hf.rect[3] = g->H;
         }
+        for (uint32_t b = 0; b < g->F; ++b)  // every column's span: the whole column
+            HIP_TRY(hipStreamWaitEvent(g->streams[0], g->ev_done[b], 0));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)g->d_spans, (int)(g->H << 16), (size_t)g->F * g->W, g->streams[0]));
+        for (uint32_t b = 1; b < g->F; ++b) {
+            HIP_TRY(hipEventRecord(g->ev_traced[0], g->streams[0]));
+            HIP_TRY(hipStreamWaitEvent(g->streams[b], g->ev_traced[0], 0));
+        }
+        if (g->copy_stream) {
+            HIP_TRY(hipEventRecord(g->ev_traced[0], g->streams[0]));
+            HIP_TRY(hipStreamWaitEvent(g->copy_stream, g->ev_traced[0], 0));
+        }
+    }
     g->host_out = enable != 0;
     if (g->host_out && g->hfb.empty()) {
+        if (!g->fb[0].rgb8 || !g->fb[0].valid)
+            return fail(MIRT_E_INVALID, "host output needs the rgb8 and valid framebuffer planes");
         g->hfb.assign(g->F, HostFrame());
+        HIP_TRY(hipMalloc((void**)&g->d_spans, sizeof(uint32_t) * g->F * g->W));
+        HIP_TRY(hipMemset(g->d_spans, 0, sizeof(uint32_t) * g->F * g->W));
         const size_t n = (size_t)g->W * g->H;
         for (HostFrame& hf : g->hfb) {
             HIP_TRY(hipHostMalloc((void**)&hf.rgb8, 3 * n));

@@ -271,12 +271,17 @@ struct RegionDesc {
 };
 // Device framebuffer -> pinned host framebuffer, the pixels of one rectangle per frame
 // (mirt_group_set_host_output): the kernel stores straight into host memory over PCIe.
+// Per column the kernel copies only the rows between the first and last hit of this frame
+// and of the frame the host slot held before (spans: per slot and column, first | end << 16;
+// every other pixel is a miss, i.e. zero, on both sides).
 struct HostCopyJobs {
     const uint8_t* rgb8[kMaxFrames];
     const uint8_t* valid[kMaxFrames];
     uint8_t* hrgb8[kMaxFrames];
     uint8_t* hvalid[kMaxFrames];
-    uint32_t rect[kMaxFrames][4];  // x0, y0, x1, y1 (half-open)
+    uint32_t* spans[kMaxFrames];   // the slot's W spans (device)
+    uint32_t rect[kMaxFrames][4];  // columns to visit: x0, -, x1, - (half-open)
+    uint32_t cur[kMaxFrames][4];   // this frame's hit rectangle (where to look for hits)
 };
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
                                  hipStream_t s);
