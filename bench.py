@@ -91,13 +91,14 @@ def parse():
 
 def resolve_shape(a) -> None:
     """Frames in flight F and frames per launch B.  Measured on one MI355X (profiles/
-    r02_shape_sweep.txt): the whole 1080p frame runs best as 8 in flight x 2 per launch
-    over long runs; a rank's 1/N share needs more frames per launch (each workgroup then
-    owns enough blocks to hide its heaviest block's chain).  A short run keeps at least two
-    launches' worth of batch slots so launches overlap."""
+    r02_shape_sweep.txt): at the driver's 20 frames the whole 1080p frame runs best as 4 in
+    flight x 1 per launch, D2H included (long runs: 8 x 2-4 are a few % faster on the device);
+    a rank's 1/N share needs more frames per launch (each workgroup then owns enough blocks
+    to hide its heaviest block's chain).  An unset batch keeps at least two launches' worth of
+    batch slots so launches overlap."""
     multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
-    F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "8"))
-    B = a.batch if a.batch is not None else int(os.environ.get("MIRT_BATCH", "4" if multi else "2"))
+    F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "4"))
+    B = a.batch if a.batch is not None else int(os.environ.get("MIRT_BATCH", "4" if multi else "1"))
     F = max(1, min(F, 16))
     if a.split_kernels or a.bounces:
         B = 1  # one frame per launch on those paths
@@ -379,9 +380,12 @@ def main():
                  "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname}
         pj = load_profile(a.profile_json, shape)
         frames_per_launch = pl / nlaunch
+        dev_ms = dev_elapsed / steps * 1e3 if dev_elapsed else ms
         line = {
             "metric": METRIC,
-            "value": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
+            # value: the device-resident frame interval (inputs and outputs in HBM, the task's
+            # contract); ms_per_step: BASELINE.md §3's ms/frame, the D2H to host memory included
+            "value": round(rays_per_frame / (dev_ms / 1e3) / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": steps,
@@ -402,9 +406,13 @@ def main():
             "frames_in_flight": getattr(sh, "F", a.inflight),
             "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,
-            "device_ms_per_frame": round(dev_elapsed / steps * 1e3, 4) if dev_elapsed else round(ms, 4),
+            "value_basis": "rays_per_frame / device_ms_per_frame (outputs left in HBM); ms_per_step includes the "
+                           "D2H of the assembled rgb8 + valid frame into pinned host memory" if d2h else
+                           "rays_per_frame / ms_per_step (outputs left in HBM)",
+            "device_ms_per_frame": round(dev_ms, 4),
+            "mrays_s_with_d2h": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
             "frame_latency_ms": round(latency * 1e3, 4),
-            "primary_mrays_s": round(primary / (ms / 1e3) / 1e6, 3),
+            "primary_mrays_s": round(primary / (dev_ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
             "hits_per_frame": int(hits),
             "tri_tests_per_frame": int((prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / pl),
@@ -427,11 +435,11 @@ def main():
         if pj:
             # physical roofs over the frame interval (counters of this exact command, profiles/)
             per_frame = lambda x: x / pj["frames_per_launch"]  # noqa: E731
-            iv = ms / 1e3
+            iv = dev_ms / 1e3  # the device-resident frame interval (k_trace's counters)
             valu = per_frame(pj["sq_insts_valu_per_launch"])
             line["roofs"] = {
                 "source": os.path.relpath(a.profile_json, ROOT),
-                "frame_interval_ms": round(ms, 4),
+                "frame_interval_ms": round(dev_ms, 4),
                 "valu_issue_frac": round(valu / iv / VALU_ISSUE_PER_S, 4),
                 "valu_insts_per_frame": int(valu),
                 "salu_insts_per_frame": int(per_frame(pj["sq_insts_salu_per_launch"])),
