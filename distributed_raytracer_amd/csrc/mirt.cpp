@@ -1440,7 +1440,8 @@ struct mirt_group {
     uint64_t stride = 0;                // words per gathered region / transfer buffer (cap + trailer)
     int my_index = 0;
     std::vector<Share> shares;
-    std::vector<OutPlanes> fb;          // root: the caller's framebuffers, one per frame slot
+    std::vector<OutPlanes> fb;          // root: the framebuffers, one per frame slot
+    std::vector<void*> own;             // framebuffer planes the group allocated (fbs == NULL)
     std::vector<uint32_t*> gathered;    // root, per frame slot: plan regions of `stride` words
     TileDesc* d_unpack = nullptr;       // root: every share's tiles at their region offsets
     uint32_t n_unpack = 0;
@@ -1705,6 +1706,7 @@ int group_plan(mirt_group* g) {
         if (g->h_bad_cap < (size_t)g->F * P) {
             if (g->h_bad) (void)hipHostFree(g->h_bad);
     if (g->d_spans) (void)hipFree(g->d_spans);
+    for (void* p : g->own) (void)hipFree(p);
             g->h_bad = nullptr;
             g->h_bad_cap = 0;
             HIP_TRY(hipHostMalloc((void**)&g->h_bad, (size_t)g->F * P));
@@ -1882,6 +1884,7 @@ void mirt_group_destroy(mirt_group* g) {
     if (g->d_regions) (void)hipFree(g->d_regions);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
     if (g->d_spans) (void)hipFree(g->d_spans);
+    for (void* p : g->own) (void)hipFree(p);
     for (HostFrame& hf : g->hfb) {
         if (hf.rgb8) (void)hipHostFree(hf.rgb8);
         if (hf.valid) (void)hipHostFree(hf.valid);
@@ -1908,10 +1911,9 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     if (world > 1 && !unique_id) return fail(MIRT_E_INVALID, "world > 1 needs the root's unique id");
     if (world > 1 && tile == 0) return fail(MIRT_E_INVALID, "world > 1 needs a tile size");
     const bool is_root = rank == 0;
-    if (is_root && !fbs) return fail(MIRT_E_INVALID, "the root needs its framebuffers");
     // the tiled path gathers packed rgbv words (uint8 colour + valid): it cannot produce
     // the fp64 colour or the diagnostic face/object planes
-    if (is_root && tile > 0)
+    if (is_root && tile > 0 && fbs)
         for (uint32_t j = 0; j < inflight; ++j)
             if (fbs[j].rgb || fbs[j].face || fbs[j].object)
                 return fail(MIRT_E_INVALID, "tiled frame groups produce rgb8 / valid / rgbv only (rgb, face and "
@@ -1962,9 +1964,22 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->binfo.assign(inflight, BatchRec());
     g->slot_frame.assign(inflight, ~0ull);
     g->slot_bad.assign(inflight, 0);
-    if (is_root)
+    if (is_root && fbs) {
         for (uint32_t j = 0; j < inflight; ++j)
             g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
+    } else if (is_root) {
+        // no framebuffers given (a caller without device memory of its own, e.g. a Go worker
+        // reading frames through mirt_group_frame_host): the group owns rgb8 + valid planes
+        const size_t n = (size_t)W * H;
+        for (uint32_t j = 0; j < inflight; ++j) {
+            OutPlanes o{};
+            HIP_TRY(hipMalloc((void**)&o.rgb8, 3 * n));
+            g->own.push_back(o.rgb8);
+            HIP_TRY(hipMalloc((void**)&o.valid, n));
+            g->own.push_back(o.valid);
+            g->fb.push_back(o);
+        }
+    }
     int r = group_plan(g.get());
     if (r != MIRT_OK) return r;
     if (world > 1) {

@@ -286,7 +286,9 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
  * into the frame's framebuffer.  `inflight` frames overlap, frame k on stream k % inflight
  * with framebuffer fbs[k % inflight] (rank 0 only; device planes of W x H pixels; the
  * planes a caller leaves NULL are not produced; with tile > 0 only rgb8, valid and rgbv can
- * be produced — rgb, face or object planes are rejected).  world <= 64.  world == 1 with tile == 0 traces the
+ * be produced — rgb, face or object planes are rejected; fbs == NULL on the root: the group
+ * allocates rgb8 + valid device planes itself, for callers that read frames through
+ * mirt_group_frame_host and own no device memory).  world <= 64.  world == 1 with tile == 0 traces the
  * whole screen straight into the framebuffer (no tiles, no RCCL); world == 1 with tile > 0
  * rehearses the tiled path on one GPU.
  *   mirt_group_unique_id: rank 0 makes the RCCL id (128 bytes) every rank passes in.

@@ -1,0 +1,211 @@
+/*
+ * mirt_worker.c — a non-Go, non-Python caller of libmirt.so: the call sequence of the
+ * drop-in GPU worker (worker/gpu in go/) in plain C, with no torch and no
+ * HIP calls of its own, so the HIP runtime comes in through libmirt's RUNPATH.
+ *
+ *   Register   (worker/distributed/main.go:100-129): the scene -> mirt_create -> one
+ *              mirt_mesh_upload per mesh (here mirt_scene_load stands in for the gob-decoded
+ *              Environment; shared/state/mesh.go:109-213 semantics).
+ *   BulkTrace  (worker/distributed/main.go:46-89): the master cuts the screen into one
+ *              rectangle per worker (master/main.go:54-91, restated below) and each order
+ *              is served concurrently — gRPC runs every BulkTrace in its own goroutine — by
+ *              mirt_trace_tile into host buffers; results go back as comms.TraceResults,
+ *              uint8 colours in uint32 fields, column-major i*h + j, and the master draws
+ *              them (master/main.go:164-176).
+ *   Frame group (mirt_trace_frame, world 1, library-owned framebuffers, host output):
+ *              three frames in flight; each host frame must equal the BulkTrace frame.
+ *
+ *   mirt_worker <scene.json> <W> <H> <out.bin> [workers]
+ * Writes rgb8 (W*H*3) then valid (W*H) of the assembled frame, column-major x*H + y.
+ * Exit status 0 = every check passed.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mirt.h"
+#include "mirt_scene.h"
+
+#define CHECK(call)                                                                       \
+    do {                                                                                  \
+        int rc_ = (call);                                                                 \
+        if (rc_ != MIRT_OK) {                                                             \
+            fprintf(stderr, "%s:%d %s -> %d: %s\n", __FILE__, __LINE__, #call, rc_,       \
+                    mirt_last_error());                                                   \
+            exit(2);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+typedef struct { uint32_t x, y, w, h; } rect;
+
+/* master/main.go:54-91 partition() with workerRedundancy = 1 (master/main.go:31):
+ * recursive bisection, alternating dimensions; returns the leftover workers. */
+static uint32_t partition(rect area, uint32_t workers, uint32_t dim, rect *out, int *n) {
+    const uint32_t wk = 50, hk = 50; /* widthKernel, heightKernel */
+    if (workers < 2) {
+        out[(*n)++] = area;
+        return 0;
+    }
+    if (area.w <= wk && area.h <= hk) {
+        out[(*n)++] = area;
+        return workers - 1;
+    } else if (area.w <= wk) {
+        dim = 1;
+    } else if (area.h <= hk) {
+        dim = 0;
+    }
+    rect l, r;
+    if (dim % 2 == 0) {
+        l = (rect){area.x, area.y, area.w / 2, area.h};
+        r = (rect){area.x + area.w / 2, area.y, area.w / 2 + area.w % 2, area.h};
+    } else {
+        l = (rect){area.x, area.y, area.w, area.h / 2};
+        r = (rect){area.x, area.y + area.h / 2, area.w, area.h / 2 + area.h % 2};
+    }
+    const uint32_t rem = partition(l, workers / 2 + workers % 2, (dim + 1) % 2, out, n);
+    return partition(r, workers / 2 + rem, (dim + 1) % 2, out, n);
+}
+
+typedef struct {
+    mirt_ctx *ctx;
+    const mirt_frame *frame;
+    rect order;          /* comms.WorkOrder x, y, width, height */
+    uint32_t W, H;
+    uint32_t *results;   /* comms.TraceResults: r, g, b per pixel (uint32 fields) */
+    int rc;
+} bulk_trace;
+
+/* One BulkTrace call (worker/distributed/main.go:46-89) on its own thread. */
+static void *serve(void *p) {
+    bulk_trace *b = (bulk_trace *)p;
+    const size_t n = (size_t)b->order.w * b->order.h;
+    uint8_t *rgb8 = malloc(3 * n), *valid = malloc(n);
+    mirt_outputs out;
+    memset(&out, 0, sizeof(out));
+    out.rgb8 = rgb8;
+    out.valid = valid;
+    b->rc = mirt_trace_tile(b->ctx, b->frame, b->order.x, b->order.y, b->order.w, b->order.h, b->W, b->H, &out, NULL,
+                            NULL);
+    b->results = malloc(3 * n * sizeof(uint32_t));
+    for (size_t k = 0; k < n; ++k) /* misses are (0, 0, 0) already */
+        for (int c = 0; c < 3; ++c) b->results[3 * k + c] = rgb8[3 * k + c];
+    free(rgb8);
+    free(valid);
+    return NULL;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 5) {
+        fprintf(stderr, "usage: %s scene.json W H out.bin [workers]\n", argv[0]);
+        return 2;
+    }
+    const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]);
+    uint32_t workers = argc > 5 ? (uint32_t)atoi(argv[5]) : 4;
+    if (mirt_abi_version() != MIRT_ABI_VERSION) {
+        fprintf(stderr, "ABI %d, header %d\n", mirt_abi_version(), MIRT_ABI_VERSION);
+        return 2;
+    }
+    /* Register: the scene and its meshes */
+    mirt_scene *scene = NULL;
+    if (mirt_scene_load(argv[1], &scene) != MIRT_OK) {
+        fprintf(stderr, "scene: %s\n", mirt_scene_last_error());
+        return 2;
+    }
+    mirt_ctx *ctx = NULL;
+    CHECK(mirt_create(0, &ctx));
+    const uint32_t nm = mirt_scene_mesh_count(scene), no = mirt_scene_object_count(scene),
+                   nl = mirt_scene_light_count(scene);
+    uint32_t *mesh_ids = calloc(nm ? nm : 1, sizeof(uint32_t));
+    for (uint32_t i = 0; i < nm; ++i) {
+        mirt_mesh_view v;
+        CHECK(mirt_scene_mesh(scene, i, &v));
+        CHECK(mirt_mesh_upload(ctx, v.vertices, v.n_vertices, v.normals, v.n_normals, v.face_v, v.face_n, v.face_mat,
+                               v.n_faces, v.materials, v.n_materials, &mesh_ids[i]));
+    }
+    /* WorkOrder.diff: objects (their mesh by id), lights, camera */
+    mirt_object *objs = calloc(no ? no : 1, sizeof(mirt_object));
+    mirt_light *lights = calloc(nl ? nl : 1, sizeof(mirt_light));
+    for (uint32_t i = 0; i < no; ++i) {
+        CHECK(mirt_scene_object(scene, i, &objs[i]));
+        objs[i].mesh_id = mesh_ids[objs[i].mesh_id];
+    }
+    for (uint32_t i = 0; i < nl; ++i) CHECK(mirt_scene_light(scene, i, &lights[i]));
+    mirt_frame frame;
+    memset(&frame, 0, sizeof(frame));
+    frame.objects = objs;
+    frame.n_objects = no;
+    frame.lights = lights;
+    frame.n_lights = nl;
+    CHECK(mirt_scene_camera(scene, &frame.camera));
+
+    /* BulkTrace: the master's partition, every order on its own thread */
+    rect orders[256];
+    int n = 0;
+    if (workers < 1 || workers > 256) workers = 4;
+    (void)partition((rect){0, 0, W, H}, workers, 0, orders, &n);
+    bulk_trace bt[256];
+    pthread_t th[256];
+    for (int i = 0; i < n; ++i) {
+        bt[i] = (bulk_trace){ctx, &frame, orders[i], W, H, NULL, 0};
+        pthread_create(&th[i], NULL, serve, &bt[i]);
+    }
+    uint8_t *fb_rgb8 = calloc((size_t)W * H, 3), *fb_valid = calloc((size_t)W * H, 1);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) {
+        pthread_join(th[i], NULL);
+        if (bt[i].rc != MIRT_OK) {
+            fprintf(stderr, "BulkTrace %d failed: %d\n", i, bt[i].rc);
+            bad = 1;
+            continue;
+        }
+        /* the master draws the results (master/main.go:164-176), pixel i*h + j */
+        const rect o = bt[i].order;
+        for (uint32_t a = 0; a < o.w; ++a)
+            for (uint32_t b = 0; b < o.h; ++b) {
+                const size_t src = (size_t)a * o.h + b, dst = (size_t)(o.x + a) * H + (o.y + b);
+                for (int c = 0; c < 3; ++c) fb_rgb8[3 * dst + c] = (uint8_t)bt[i].results[3 * src + c];
+            }
+        free(bt[i].results);
+    }
+    /* the valid plane of the whole screen from one more call (the wire carries colours only) */
+    {
+        mirt_outputs out;
+        memset(&out, 0, sizeof(out));
+        out.valid = fb_valid;
+        CHECK(mirt_trace_tile(ctx, &frame, 0, 0, W, H, W, H, &out, NULL, NULL));
+    }
+
+    /* the frame group: library-owned device framebuffers, frames copied to host memory */
+    mirt_group *g = NULL;
+    CHECK(mirt_group_create(ctx, NULL, 0, 1, W, H, 0, 0, 2, NULL, &g));
+    CHECK(mirt_group_set_host_output(g, 1));
+    CHECK(mirt_group_set_timeout(g, 10000));
+    uint64_t idx[3];
+    for (int k = 0; k < 3; ++k) {
+        CHECK(mirt_trace_frame(g, &frame, &idx[k]));
+        if (k > 0) {
+            mirt_outputs h;
+            CHECK(mirt_group_frame_host(g, idx[k - 1], &h));
+            if (memcmp(h.rgb8, fb_rgb8, (size_t)W * H * 3) || memcmp(h.valid, fb_valid, (size_t)W * H)) {
+                fprintf(stderr, "group frame %d differs from the BulkTrace frame\n", k - 1);
+                bad = 1;
+            }
+        }
+    }
+    CHECK(mirt_group_wait(g, NULL));
+    mirt_group_destroy(g);
+
+    FILE *f = fopen(argv[4], "wb");
+    if (!f || fwrite(fb_rgb8, 3, (size_t)W * H, f) != (size_t)W * H || fwrite(fb_valid, 1, (size_t)W * H, f) != (size_t)W * H) {
+        fprintf(stderr, "cannot write %s\n", argv[4]);
+        return 2;
+    }
+    fclose(f);
+    mirt_destroy(ctx);
+    mirt_scene_free(scene);
+    printf("mirt_worker: %ux%u, %d BulkTrace orders on %d threads, group frames equal: %s\n", W, H, n, n,
+           bad ? "NO" : "yes");
+    return bad;
+}
