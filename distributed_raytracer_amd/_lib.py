@@ -146,6 +146,7 @@ SIGNATURES = {
     "mirt_group_frame_host": (C.c_int, [_P, C.c_uint64, C.POINTER(Outputs)]),
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
+    "mirt_debug_counters": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_unpack_tiles_at_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "mirt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "mirt_scene_free": (None, [_P]),

@@ -162,7 +162,7 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
         Bvh8Node root;
         for (int c = 0; c < 8; ++c) root.child[c] = kBvhEmpty;
         for (int k = 0; k < 3; ++k)
-            for (int c = 0; c < 8; ++c) root.lo(k, c) = root.hi(k, c) = 0.0f;
+            for (int c = 0; c < 8; ++c) { root.lo(k, c) = INFINITY; root.hi(k, c) = -INFINITY; }
         out.nodes.push_back(root);
         return out;
     }
@@ -200,7 +200,7 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
         for (int c = 0; c < 8; ++c) {
             if (c >= (int)kids.size()) {
                 nd.child[c] = kBvhEmpty;
-                for (int k = 0; k < 3; ++k) { nd.lo(k, c) = 1.0f; nd.hi(k, c) = -1.0f; }
+                for (int k = 0; k < 3; ++k) { nd.lo(k, c) = INFINITY; nd.hi(k, c) = -INFINITY; }
                 continue;
             }
             const BNode& k = b.nodes[kids[c]];
@@ -218,6 +218,44 @@ inline BvhBuild build_bvh(const double* v, const uint32_t* fv, uint32_t nf, doub
             }
         }
         out.nodes[p.slot] = nd;
+    }
+    return out;
+}
+
+// The kernels' node format (mirt_internal.hpp Bvh8Dev): per sign octant, the children
+// sorted near to far along the octant's diagonal, bounds stored near plane first.
+inline std::vector<Bvh8Dev> make_dev_nodes(const std::vector<Bvh8Node>& nodes) {
+    std::vector<Bvh8Dev> out(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const Bvh8Node& n = nodes[i];
+        int nk = 0;
+        while (nk < 8 && n.child[nk] != kBvhEmpty) ++nk;
+        for (uint32_t o = 0; o < 8; ++o) {
+            Bvh8Copy& cp = out[i].oct[o];
+            int ord[8];
+            double key[8];
+            for (int c = 0; c < nk; ++c) {
+                ord[c] = c;
+                key[c] = 0;
+                for (int a = 0; a < 3; ++a) {
+                    const double ctr = 0.5 * ((double)n.lo(a, c) + (double)n.hi(a, c));
+                    key[c] += ((o >> a) & 1u) ? -ctr : ctr;
+                }
+            }
+            std::stable_sort(ord, ord + nk, [&](int x, int y) { return key[x] < key[y]; });
+            for (int slot = 0; slot < 8; ++slot) {
+                const bool full = slot < nk;
+                const int c = full ? ord[slot] : 0;
+                for (int a = 0; a < 3; ++a) {
+                    const float lo = full ? n.lo(a, c) : INFINITY, hi = full ? n.hi(a, c) : -INFINITY;
+                    const bool neg = ((o >> a) & 1u) != 0;
+                    cp.box[a][slot][0] = neg ? hi : lo;
+                    cp.box[a][slot][1] = neg ? lo : hi;
+                }
+                cp.child[slot] = full ? n.child[c] : kBvhEmpty;
+            }
+            for (uint32_t& w : cp.pad) w = 0;
+        }
     }
     return out;
 }

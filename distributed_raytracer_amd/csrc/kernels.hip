@@ -31,7 +31,7 @@ namespace mirt {
 // Wave-uniform reads of immutable device data (BVH nodes, triangles streamed from HBM)
 // go through the constant address space so hipcc emits scalar s_load into SGPRs.
 typedef const __attribute__((address_space(4))) double* cdptr;
-typedef const __attribute__((address_space(4))) Bvh8Node* cnptr;
+typedef const __attribute__((address_space(4))) Bvh8Dev* cnptr;
 typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
 typedef const __attribute__((address_space(4))) u32x16* cv16ptr;
 typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
@@ -60,23 +60,45 @@ __device__ __forceinline__ bool r2_certainly_out(double n, double d) {
     return (n * k < -__builtin_fabs(d)) | (__builtin_fabs(n) > __builtin_fabs(d) * (1.0 + 0x1p-50));
 }
 
+// MIRT_DIAG (diagnostic builds only): wave-level event counts (how many waves reach each
+// stage of the triangle test, per query kind), read with mirt_debug_counters.  Counted by
+// the wave's first active lane into 8 shards.
+#ifndef MIRT_DIAG
+#define MIRT_DIAG 0
+#endif
+constexpr int kDiagN = 32;
+__device__ unsigned long long g_diag[8 * kDiagN];
+__device__ __forceinline__ void diag(int k) {
+    if (MIRT_DIAG) {
+        const uint64_t ex = __builtin_amdgcn_read_exec();
+        if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(ex))
+            atomicAdd(&g_diag[(blockIdx.x & 7) * kDiagN + k], 1ull);
+    }
+}
+
 // Möller–Trumbore exactly as triangle.go:37-77, on (p1or = O - P1, E1, E2), returning
 // only the hit decision and the ray parameter.  neg = D * -1 (triangle.go:38).
-template <bool PREFILTER>
+//   DG: diagnostic counter base (MIRT_DIAG builds).
+template <bool PREFILTER, int DG = 0>
 __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t_out) {
+    diag(DG + 0);
     V3 c = cross(e2, neg);
     double inc = dot(e1, c);
     if (inc != 0.0) {
         double n2 = dot(p1or, c);
         if (PREFILTER && r2_certainly_out(n2, inc)) return false;
+        diag(DG + 1);
         double r2 = n2 / inc;
         if (0.0 <= r2 && r2 <= 1.0) {
+            diag(DG + 2);
             double r3 = dot(e1, cross(p1or, neg)) / inc;
             if (0.0 <= r2 + r3 && r2 + r3 <= 1.0) {
                 double r1 = 1.0 - r2 - r3;
                 if (r1 >= 0.0 && r2 >= 0.0 && r3 >= 0.0) {
+                    diag(DG + 3);
                     double t = dot(e1, cross(e2, p1or)) / inc;
                     if (t >= 0.0) {
+                        diag(DG + 4);
                         t_out = t;
                         return true;
                     }
@@ -182,7 +204,7 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
 
 // Test n triangles at positions pos0.. of the BVH-ordered arrays; `src` points at the
 // record of position pos0 (in LDS or in HBM).
-template <bool REL, bool PREFILTER, typename SrcPtr>
+template <bool REL, bool PREFILTER, int DG = 0, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
@@ -194,9 +216,11 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         V3 e1{t[3], t[4], t[5]};
         V3 e2{t[6], t[7], t[8]};
         double tt;
-        if (mt_test<PREFILTER>(p1or, e1, e2, neg, tt)) {
+        // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
+        const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
+        if (mt_test<PREFILTER, DG>(p1or, e1, e2, neg, tt)) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
-            consider(b, len(sub(ro, ip)), fidx[k], k);  // object.go:97
+            consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
         }
     }
 }
@@ -262,22 +286,36 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], in
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Wave-uniform traversal stack held in two VGPRs: entry i lives in lane i % 64 of
-// word i / 64.  Push and pop are v_writelane / v_readlane with the SGPR stack pointer:
+// Wave-uniform traversal stack in VGPR lanes: entry i lives in lane i % 64 of word i / 64
+// (DEEP: two words, 128 entries; else one word, 64 entries, for trees of depth <=
+// kBvhShallowDepth).  Push and pop are v_writelane / v_readlane with the SGPR stack pointer:
 // no memory traffic and no LDS latency on the node-to-node dependency chain.
+template <bool DEEP>
 struct WaveStack {
     int a = 0, b = 0;
     uint32_t sp = 0;
-    __device__ __forceinline__ void push(uint32_t ref) {
-        if (sp < 64)
+    __device__ __forceinline__ void put(uint32_t ref) {  // write the entry above the top
+        if (!DEEP || sp < 64)
             asm("v_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(ref), "{m0}"(sp));
         else
             asm("v_writelane_b32 %0, %1, m0" : "+v"(b) : "s"(ref), "{m0}"(sp - 64));
+    }
+    __device__ __forceinline__ void push(uint32_t ref) {
+        put(ref);
         ++sp;
+    }
+    // Child push without a branch: the ref is written above the top unconditionally and
+    // kept (sp += 1) iff some live lane's ray enters the child, i.e. (m & live) != 0:
+    // s_and_b64 sets SCC exactly then and s_addc_u32 adds it.
+    __device__ __forceinline__ void push_if(uint32_t ref, uint64_t m, uint64_t live) {
+        put(ref);
+        uint64_t t;
+        asm volatile("s_and_b64 %1, %2, %3\n\ts_addc_u32 %0, %0, 0" : "+s"(sp), "=&s"(t) : "s"(m), "s"(live) : "scc");
     }
     __device__ __forceinline__ uint32_t pop() {
         --sp;
-        return (uint32_t)(sp < 64 ? __builtin_amdgcn_readlane(a, (int)sp) : __builtin_amdgcn_readlane(b, (int)(sp - 64)));
+        return (uint32_t)(!DEEP || sp < 64 ? __builtin_amdgcn_readlane(a, (int)sp)
+                                           : __builtin_amdgcn_readlane(b, (int)(sp - 64)));
     }
 };
 
@@ -307,11 +345,11 @@ __device__ __forceinline__ Ray32 ray32(V3 ro, V3 d) {
     r.oiz = r.oz * r.iz;
     return r;
 }
-// A node in SGPRs: three s_load_dwordx16 + one s_load_dwordx8.  Words 16 a + 2 c (+1): lo (hi) of child c on
-// axis a, 48..55 child refs.
+// One copy of a node in SGPRs: three s_load_dwordx16 + one s_load_dwordx8.  Words
+// 16 a + 2 c (+1): near (far) bound of slot c on axis a (copy 0: lo, hi), 48..55 refs.
 struct NodeRegs {
     u32x16 w0, w1, w2;
-    u32x8 w3;  // the child refs (the node's last 8 words are padding, never loaded)
+    u32x8 w3;  // the child refs (the copy's last 8 words are padding, never loaded)
     __device__ __forceinline__ uint32_t word(int i) const {
         return i < 16 ? w0[i] : i < 32 ? w1[i - 16] : i < 48 ? w2[i - 32] : w3[i - 48];
     }
@@ -319,11 +357,11 @@ struct NodeRegs {
     __device__ __forceinline__ float hi(int a, int c) const { return __uint_as_float(word(a * 16 + 2 * c + 1)); }
     __device__ __forceinline__ uint32_t child(int c) const { return word(48 + c); }
 };
-// oct (packet_octant): axis a with bit a set loads the (hi, lo) copy of its bounds.
+// oct (packet_octant): the copy of that sign octant; mixed packets (kOctMixed = 8) read
+// copy 0, whose pairs are (lo, hi).
 __device__ __forceinline__ NodeRegs load_node(cnptr nd, uint32_t oct = 0) {
-    const cv16ptr p = (cv16ptr)nd;
-    const uint32_t o = oct & 7u;  // mixed packets (kOctMixed = 8) load the (lo, hi) pairs
-    return NodeRegs{p[(o & 1u) ? 4 : 0], p[(o & 2u) ? 5 : 1], p[(o & 4u) ? 6 : 2], ((cv8ptr)nd)[6]};
+    const cv16ptr p = (cv16ptr)&nd->oct[oct & 7u];
+    return NodeRegs{p[0], p[1], p[2], ((cv8ptr)p)[6]};
 }
 
 // Ray vs child c's box, t >= 0 half-line.  Boxes are inflated by 2^-12 of the mesh
@@ -434,59 +472,69 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 }
 
 // Wave-uniform walk of one object's 8-wide BVH (packet traversal).  A child is entered
-// when ANY live lane's ray hits its box; leaves are tested immediately, inner children
-// go on the wave's register stack.  Lanes whose object-space origin is beyond the cull
-// limit never cull (the inflation argument needs a bounded origin).
-//   SEG (segment query): a lane also skips boxes it enters beyond tmax, and retires once
-//   its nearest candidate is closer than `resolve` (the caller's decision is then made);
-//   the walk ends when no live lane is left.
+// when ANY live lane's ray meets its box; entered children (inner nodes and leaves alike)
+// go on the wave's register stack, the nearest one on top (node copies are sorted near
+// to far for the packet's sign octant), and the walk pops them one at a time: a leaf is
+// tested, an inner node loaded and its children tested.
+//   Nearest query (!SEG): once a lane holds a candidate at distance b.d, boxes it would
+//   enter beyond tmax = f32((b.d + M) (1 + 2^-20)), M = 2^-36 (1 + b.d + |ro|), are
+//   skipped for it: every candidate inside such a box lies farther than b.d (the argument
+//   of the segment bound below), so it can neither win nor tie.
+//   SEG (segment query): a lane also skips boxes it enters beyond its tmax, and retires
+//   once its nearest candidate is closer than `resolve` (the caller's decision is then
+//   made); the walk ends when no live lane is left.
+// Packets with a lane whose object-space origin is beyond the cull limit (the inflation
+// argument needs a bounded origin) enter every child.
 template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
                                           Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true) {
+    // LDS-resident meshes (the host guarantees depth <= kBvhShallowDepth) use a one-VGPR stack
+    constexpr bool DEEP = !__is_same(SrcPtr, const double*);
     const Ray32 r = ray32(ro, d);
     const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-    const bool force = !(far <= m.cull_limit);
+    const bool all = __ballot(lane_on && !(far <= m.cull_limit)) != 0;  // wave-uniform
     bool live = lane_on;
-    const uint64_t fmask = __ballot(force);
-    const uint32_t oct = octant ? packet_octant(r, lane_on) : kOctMixed;  // wave-uniform
-    WaveStack stk;
-    uint32_t cur = 0;
-    for (;;) {
-        cur = __builtin_amdgcn_readfirstlane(cur);
-        const NodeRegs nd = load_node((cnptr)m.nodes + cur, oct);
-        ++vis.nodes;
-        // wave-uniform: bit c = some live lane's ray hits child c (each test's compare
-        // result is the lane mask itself: no per-lane bit packing)
-        const uint64_t lmask = __ballot(live);
-        const uint32_t entered = oct == kOctMixed ? children_entered<false, SEG>(nd, r, tmax, fmask, lmask)
-                                                  : children_entered<true, SEG>(nd, r, tmax, fmask, lmask);
-        // classify the entered children (unrolled: SALU only), then test the leaves in ONE
-        // loop so the triangle test is instantiated once (code size: instruction cache)
-        uint32_t leafmask = 0;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t ref = nd.child(c);
-            if (!((entered >> c) & 1u)) continue;
-            if (ref & kBvhLeafBit)
-                leafmask |= 1u << c;
-            else
-                stk.push(ref);
-        }
-        const uint32_t r0 = nd.child(0), r1 = nd.child(1), r2 = nd.child(2), r3 = nd.child(3);
-        const uint32_t r4 = nd.child(4), r5 = nd.child(5), r6 = nd.child(6), r7 = nd.child(7);
-        while (leafmask) {
-            const uint32_t c = __builtin_ctz(leafmask);
-            leafmask &= leafmask - 1;
-            const uint32_t ref = c < 4 ? (c < 2 ? (c == 0 ? r0 : r1) : (c == 2 ? r2 : r3))
-                                       : (c < 6 ? (c == 4 ? r4 : r5) : (c == 6 ? r6 : r7));
+    const uint32_t oct = octant && !all ? packet_octant(r, lane_on) : kOctMixed;  // wave-uniform
+    float tm = SEG ? tmax : __builtin_inff();
+    const double Mbase = 0x1p-36 * (1.0 + far);
+    WaveStack<DEEP> stk;
+    stk.push(0u);  // the root
+    do {
+        const uint32_t ref = stk.pop();
+        if (ref & kBvhLeafBit) {
             const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
-            test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
-            if (SEG) live = live && !(b.has && b.d < resolve);
+            diag(SEG ? 14 : 6);
+            test_range<REL, PREFILTER, SEG ? 8 : 0>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
+                                                    vis.tests);
+            if (SEG) {
+                live = live && !(b.has && b.d < resolve);
+                if (__ballot(live) == 0) break;
+            } else if (b.has) {
+                tm = (float)(b.d + (Mbase + 0x1p-36 * b.d)) * (1.0f + 0x1p-20f);
+            }
+            continue;
         }
-        if (stk.sp == 0 || (SEG && __ballot(live) == 0)) break;
-        cur = stk.pop();
-    }
+        const NodeRegs nd = load_node((cnptr)m.nodes + ref, oct);
+        ++vis.nodes;
+        diag(SEG ? 13 : 5);
+        const uint64_t lm = __ballot(live);
+        if (oct != kOctMixed) {
+#pragma unroll
+            for (int c = 7; c >= 0; --c)  // far first: slot 0, the nearest, ends on top
+                stk.push_if(nd.child(c), slab_mask_ordered<true>(nd, c, r, tm), lm);
+        } else if (!all) {
+#pragma unroll
+            for (int c = 7; c >= 0; --c) {
+                if (nd.child(c) == kBvhEmpty) continue;
+                stk.push_if(nd.child(c), slab_mask<true>(nd, c, r, tm), lm);
+            }
+        } else {
+#pragma unroll
+            for (int c = 7; c >= 0; --c)
+                if (nd.child(c) != kBvhEmpty) stk.push(nd.child(c));
+        }
+    } while (stk.sp != 0);
 }
 
 // Occupancy target of the tracing kernels (waves per SIMD) and LDS-resident meshes.
@@ -647,7 +695,7 @@ __device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t*
         float lx = 0, ly = 0, lz = 0, hx = 0, hy = 0, hz = 0;
         uint32_t ref = kBvhEmpty;
         if (on) {
-            const float* nb = (const float*)(m.nodes + node);
+            const float* nb = (const float*)&m.nodes[node].oct[0];  // copy 0: (lo, hi) pairs
             ref = ((const uint32_t*)nb)[48 + c];
             lx = nb[2 * c];
             ly = nb[16 + 2 * c];
@@ -1787,7 +1835,8 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
     } while (0)
 
 static bool is_resident(const FrameArgs& fa) {
-    return MIRT_LDS_MESH && fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris;
+    return MIRT_LDS_MESH && fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris &&
+           fa.obj[0].m.depth <= (uint32_t)kBvhShallowDepth;
 }
 
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
@@ -2069,6 +2118,18 @@ hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_fp64, dim3((n + 255) / 256), dim3(256), 0, s, op, n, a, b, out);
     return hipGetLastError();
+}
+
+hipError_t read_diag_counters(uint64_t* out, uint32_t n) {
+    unsigned long long h[8 * kDiagN];
+    hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h), 0, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    for (uint32_t k = 0; k < n && k < (uint32_t)kDiagN; ++k) {
+        out[k] = 0;
+        for (int sh = 0; sh < 8; ++sh) out[k] += h[sh * kDiagN + k];
+    }
+    for (auto& x : h) x = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), h, sizeof(h), 0, hipMemcpyHostToDevice);
 }
 
 }  // namespace mirt

@@ -50,7 +50,7 @@ struct MeshDev {
     double* vnrm = nullptr;
     uint32_t* fmat = nullptr;
     uint32_t* fidx = nullptr;
-    Bvh8Node* nodes = nullptr;
+    Bvh8Dev* nodes = nullptr;
     double* mats = nullptr;
     uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
@@ -830,15 +830,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         }
         mt[10 * m + 9] = mats[m].ns;
     }
-    // the (hi, lo) copies of every node's bounds (kernels.hip packet_octant)
-    for (Bvh8Node& n : bvh.nodes) {
-        for (int a = 0; a < 3; ++a)
-            for (int c = 0; c < 8; ++c) {
-                n.sbox[a][c][0] = n.box[a][c][1];
-                n.sbox[a][c][1] = n.box[a][c][0];
-            }
-        for (uint32_t& w : n.pad2) w = 0;
-    }
+    const std::vector<Bvh8Dev> dev_nodes = make_dev_nodes(bvh.nodes);
     MeshDev md;
     md.ntri = nf;
     md.nmat = nm;
@@ -860,7 +852,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         (r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK ||
         (r = upload((void**)&md.fmat, fm.data(), (size_t)nf * 4)) != MIRT_OK ||
         (r = upload((void**)&md.fidx, bvh.order.data(), (size_t)nf * 4)) != MIRT_OK ||
-        (r = upload((void**)&md.nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(Bvh8Node))) != MIRT_OK ||
+        (r = upload((void**)&md.nodes, dev_nodes.data(), dev_nodes.size() * sizeof(Bvh8Dev))) != MIRT_OK ||
         (r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) {
         mesh_free(md);
         return r;
@@ -1133,6 +1125,14 @@ int mirt_debug_timeline(mirt_ctx* c, uint64_t* out, uint32_t max_records) {
         ++n;
     }
     return (int)n;
+}
+
+int mirt_debug_counters(mirt_ctx* c, uint64_t* out, uint32_t n) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(read_diag_counters(out, n));
+    return MIRT_OK;
 }
 
 int mirt_debug_fp64(mirt_ctx* c, int op, uint32_t n, const double* a, const double* b, double* out) {

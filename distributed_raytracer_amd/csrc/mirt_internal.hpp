@@ -23,23 +23,35 @@ constexpr int kTriD = 9;
 // larger meshes stream through it in batches of this size.
 constexpr int kLdsTris = 1024;
 
-// 8-wide BVH node.  Child boxes are fp32, rounded outward and inflated so that
-// a ray the fp64 Möller–Trumbore test could report as a hit always passes the fp32
-// slab test (DESIGN.md §4 "Exact culling").  child[c]: kBvhEmpty, an inner node index,
-// or kBvhLeafBit | count << kBvhCountShift | first (a contiguous triangle range).
-// Non-empty children come first.  256 B, 64-byte aligned: fetched as four
-// s_load_dwordx16 per visit.  A child's lo/hi bounds on one axis are adjacent words (an
-// aligned SGPR pair: one packed-fp32 operand of the slab test).
-struct alignas(64) Bvh8Node {
+// 8-wide BVH node as built on the host (bvh.hpp).  Child boxes are fp32, rounded outward
+// and inflated so that a ray the fp64 Möller–Trumbore test could report as a hit always
+// passes the fp32 slab test (DESIGN.md §4 "Exact culling").  child[c]: kBvhEmpty, an
+// inner node index, or kBvhLeafBit | count << kBvhCountShift | first (a contiguous
+// triangle range).  Non-empty children come first.
+struct Bvh8Node {
     float box[3][8][2];  // [axis][child][lo, hi]
     uint32_t child[8];
-    uint32_t pad[8];
-    float sbox[3][8][2];  // [axis][child][hi, lo]: the copy a packet with 1/d < 0 on that axis loads
-    uint32_t pad2[16];
     float& lo(int a, int c) { return box[a][c][0]; }
     float& hi(int a, int c) { return box[a][c][1]; }
     float lo(int a, int c) const { return box[a][c][0]; }
     float hi(int a, int c) const { return box[a][c][1]; }
+};
+// The node as the kernels read it: one 256-byte copy per sign octant of a packet's ray
+// directions (bit a set: 1/d < 0 on axis a).  In copy o the children are sorted near to
+// far along the octant's diagonal (box centres projected on (+-1, +-1, +-1)) and each
+// axis's bounds are stored near plane first ((hi, lo) on the negative axes), so a packet
+// of that octant tests a child with no min/max sorting and pushes the nearest child last
+// (it is popped first).  An empty slot is the box lo = +inf, hi = -inf stored the same way:
+// every ordered test of it fails.  Copy 0 doubles as the (lo, hi) copy that packets of
+// mixed signs test with the sorted slab test (they skip empty slots by their ref).  Read
+// with four scalar loads (three s_load_dwordx16 of bounds, one s_load_dwordx8 of refs).
+struct alignas(256) Bvh8Copy {
+    float box[3][8][2];  // [axis][slot][near, far]
+    uint32_t child[8];   // slot order
+    uint32_t pad[8];
+};
+struct Bvh8Dev {
+    Bvh8Copy oct[8];
 };
 constexpr uint32_t kBvhEmpty = 0xffffffffu;
 constexpr uint32_t kBvhLeafBit = 0x80000000u;
@@ -48,6 +60,10 @@ constexpr uint32_t kBvhFirstMask = 0x00ffffffu;
 constexpr int kBvhLeaf = 4;           // max triangles per leaf
 constexpr int kBvhStack = 128;        // per-wave traversal stack entries (two VGPRs / LDS)
 constexpr int kBvhMaxDepth = (kBvhStack - 1) / 7;
+// A traversal pushes every entered child (leaves too): at most 7 per inner level plus the
+// last node's 8, i.e. 7 depth + 1 entries.  Meshes with depth <= kBvhShallowDepth walk
+// with a one-VGPR (64-entry) stack; the LDS-resident kernels require it.
+constexpr int kBvhShallowDepth = 8;
 // Wide traversal (shared-origin packets): up to 8 nodes per pass, one lane per child box.
 // Batching is allowed only while the stack holds <= DevMesh::wide_thresh entries
 // (= kBvhStack - 64 - 7 * depth), which bounds the stack by kBvhStack.
@@ -61,7 +77,7 @@ struct DevMesh {
     const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
     const uint32_t* fmat;    // ntri     : material index
     const uint32_t* fidx;    // ntri     : original face index
-    const Bvh8Node* nodes;   // root first
+    const Bvh8Dev* nodes;    // root first
     const double* mats;      // nmat * 10: ka[3] kd[3] ks[3] ns
     uint32_t ntri;
     uint32_t has_normals;
@@ -247,6 +263,7 @@ hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
+hipError_t read_diag_counters(uint64_t* out, uint32_t n);  // MIRT_DIAG builds (zeros otherwise)
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 struct RectJobs {  // k_pack_rect / k_unpack_rect / k_check_regions: per frame of a batch
     const uint32_t* src[kMaxFrames];  // pack: the rgbv plane; unpack/check: the gathered regions

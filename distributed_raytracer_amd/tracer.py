@@ -142,6 +142,12 @@ class Context:
         L.check(min(n, 0))
         return out[:n]
 
+    def debug_counters(self) -> np.ndarray:
+        """Wave-level event counts of a -DMIRT_DIAG=1 build since the last call (mirt.h)."""
+        out = np.zeros(32, np.uint64)
+        L.check(L.lib().mirt_debug_counters(self.handle, out.ctypes.data, 32))
+        return out
+
 
 # --------------------------------------------------------------------- scene
 @dataclass

@@ -277,6 +277,16 @@ int mirt_debug_fp64(mirt_ctx *ctx, int op, uint32_t n, const double *a, const do
 int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 
 /*
+ * Diagnostic: wave-level event counts of a library built with -DMIRT_DIAG=1 (all zero in
+ * the default build), summed since the last call and reset: per query kind (base 0:
+ * primary / nearest-hit sweeps, base 8: shadow segment sweeps) [base+0] triangle tests
+ * entered, [+1] past inc != 0 and the r2 pre-reject, [+2] past the r2 range check,
+ * [+3] past the r3 / r2+r3 / r1 checks, [+4] hits (t >= 0); [5] / [13] BVH node visits,
+ * [6] / [14] leaves tested.  Synchronises the device; n <= 32.
+ */
+int mirt_debug_counters(mirt_ctx *ctx, uint64_t *out, uint32_t n);
+
+/*
  * Multi-GPU frames (one process per GPU of a box; SURVEY.md §8(b) mirt_trace_frame).  The
  * screen is cut into tile x tile_h tiles (tile_h == 0: full-height column strips, which are
  * contiguous in the column-major framebuffer) dealt to the ranks (column c of tile row r

@@ -453,18 +453,17 @@ def test_frames_in_flight_alternating_cameras(ctx, env, inflight, grid):
 
 
 def test_octant_child_test_changes_nothing(ctx, env):
-    """The sign-octant child-box test (near/far planes loaded pre-ordered, no min/max
-    sorting) must make exactly the culling decisions of the generic test: identical frames
-    AND identical traversal counters (node visits, leaf visits, ray-triangle tests) with
-    MIRT_OPT_NO_OCTANT, for views whose packets are uniform and views that mix signs."""
+    """The sign-octant walk (the node copy of the packet's octant: near/far planes loaded
+    pre-ordered, children sorted near to far) and the generic walk (copy 0 with the sorted
+    min/max test, MIRT_OPT_NO_OCTANT) must give identical frames for views whose packets
+    are uniform and views that mix signs.  Their traversal counters differ: the nearest
+    query skips boxes beyond a lane's best candidate, which depends on the visiting order."""
     import distributed_raytracer_amd as rt
     base = env.mutable()
     c = base.cam
     cams = [c,
             rt.Camera.new(tuple(np.asarray(c.pos) + np.array([0.9, 0.6, 0.2])), tuple(-np.asarray(c.pos)), c.fov),
             rt.Camera.new((0.3, 0.2, 0.1), (0.2, -0.1, -1.0), 2.0)]  # inside the mesh's box: mixed signs
-    keys = ("primary_node_visits", "primary_leaf_visits", "primary_tri_tests", "shadow_node_visits",
-            "shadow_leaf_visits", "shadow_tri_tests", "hits")
     try:
         for cam in cams:
             mut = rt.EnvMutables(base.objects, base.lights, cam)
@@ -477,8 +476,7 @@ def test_octant_child_test_changes_nothing(ctx, env):
                 res.append((fb, ctx.profile_read()))
             (a, pa), (b, pb) = res
             assert np.array_equal(a.valid, b.valid) and np.array_equal(a.rgb, b.rgb) and np.array_equal(a.face, b.face)
-            assert {k: pa[k] for k in keys} == {k: pb[k] for k in keys}
-            assert pa["primary_node_visits"] > 0
+            assert pa["hits"] == pb["hits"] and pa["primary_node_visits"] > 0 and pb["primary_node_visits"] > 0
     finally:
         ctx.set_options(0)
 

@@ -1,0 +1,35 @@
+"""Wave-level stage counts of the triangle test per frame (a -DMIRT_DIAG=1 build, MIRT_LIB):
+  MIRT_LIB=distributed_raytracer_amd/libmirt_diag.so python tools/diag_stages.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    ctx = rt.Context(0)
+    env = rt.Environment.from_file(os.path.join(ROOT, "tests", "golden", "example", "scene.json"), ctx)
+    fr = env.mutable().to_frame()
+    g = NativeFrameGroup(ctx, 1920, 1080, 0, 1, None, inflight=1)
+    g.render(fr)
+    g.wait()
+    torch.cuda.synchronize()
+    ctx.debug_counters()
+    n = 4
+    for _ in range(n):
+        g.render(fr)
+    g.wait()
+    torch.cuda.synchronize()
+    c = ctx.debug_counters() / n
+    names = ["tests", "past r2 pre-reject", "past r2 range", "past r3 checks", "hits", "node visits", "leaves"]
+    for base, kind in ((0, "primary"), (8, "shadow")):
+        print(kind, "  ".join(f"{nm}={c[base + i]:.0f}" for i, nm in enumerate(names)))
+    g.close()
+
+
+if __name__ == "__main__":
+    main()
