@@ -110,6 +110,7 @@ SIGNATURES = {
     "mirt_camera_init": (C.c_int, [_P, _P, C.c_double, C.POINTER(Camera)]),
     "mirt_go_tan": (C.c_double, [C.c_double]),
     "mirt_go_pow": (C.c_double, [C.c_double, C.c_double]),
+    "mirt_go_minmax": (C.c_double, [C.c_int, C.c_double, C.c_double]),
     "mirt_mesh_upload": (C.c_int, [_P, _P, C.c_uint32, _P, C.c_uint32, _P, _P, _P, C.c_uint32,
                                    C.POINTER(Material), C.c_uint32, C.POINTER(C.c_uint32)]),
     "mirt_mesh_release": (C.c_int, [_P, C.c_uint32]),

@@ -70,6 +70,14 @@ MIRT_HD double go_max(double x, double y) {
     return x > y ? x : y;
 }
 
+// The constant-operand forms the colour code uses, with Go's results for every input:
+//   go_min(a, 1.0):  NaN -> NaN, else the smaller (no signed-zero case: 1 is not zero)
+//   go_max(x, 0.0) and go_max(0.0, x):  NaN -> NaN, x > 0 -> x, else +0 (both zeros give
+//   +0: Go returns the operand without the sign bit)
+// (tests/test_host.py pins them against go_min / go_max over special and random values.)
+MIRT_HD double go_min1(double a) { return a >= 1.0 ? 1.0 : a; }
+MIRT_HD double go_max0(double x) { return x <= 0.0 ? 0.0 : x; }
+
 // Go math.Frexp / normalize / Ldexp (bit manipulation; exact).
 MIRT_HD double go_frexp(double f, int& e) {
     e = 0;
@@ -131,6 +139,19 @@ __host__ __device__ __attribute__((noinline)) inline double go_pow_frac(double y
 MIRT_HD double go_pow(double x, double y) {
     if (y == 0 || x == 1) return 1;
     if (y == 1) return x;
+    // Small integer exponents of a base in [2^-60, 16] (tracer.go:72's Ns): Go's repeated
+    // squaring on the Frexp mantissa only rescales every operand by powers of two, which
+    // changes no rounding while all products stay normal (here x^y lies in [2^-960, 2^64]
+    // and the squares below 2^128), so squaring x itself in the same order gives the same
+    // bits and Go's final Ldexp is exact.
+    if (y >= 2.0 && y <= 16.0 && x >= 0x1p-60 && x <= 16.0 && y == (double)(int)y) {
+        double a = 1.0, p = x;
+        for (int i = (int)y; i != 0; i >>= 1) {
+            if (i & 1) a *= p;
+            p *= p;
+        }
+        return a;
+    }
     if (d_isnan(x) || d_isnan(y)) return __builtin_nan("");
     if (x == 0) {
         if (y < 0) return (d_signbit(x) && go_is_odd_int(y)) ? -__builtin_inf() : __builtin_inf();
@@ -198,12 +219,11 @@ MIRT_HD double go_pow(double x, double y) {
 struct RGB {
     double r, g, b;
 };
-MIRT_HD RGB c_add(RGB a, RGB b) {
-    return RGB{go_min(a.r + b.r, 1.0), go_min(a.g + b.g, 1.0), go_min(a.b + b.b, 1.0)};
+MIRT_HD RGB c_add(RGB a, RGB b) {  // go_min(x, 1.0) per channel
+    return RGB{go_min1(a.r + b.r), go_min1(a.g + b.g), go_min1(a.b + b.b)};
 }
-MIRT_HD RGB c_scale(RGB a, double s) {
-    return RGB{go_max(0.0, go_min(s * a.r, 1.0)), go_max(0.0, go_min(s * a.g, 1.0)),
-               go_max(0.0, go_min(s * a.b, 1.0))};
+MIRT_HD RGB c_scale(RGB a, double s) {  // go_max(0.0, go_min(s * x, 1.0)) per channel
+    return RGB{go_max0(go_min1(s * a.r)), go_max0(go_min1(s * a.g)), go_max0(go_min1(s * a.b))};
 }
 MIRT_HD RGB c_mul(RGB a, RGB b) { return RGB{a.r * b.r, a.g * b.g, a.b * b.b}; }
 // colour.go:59-61 RGB(): uint8(255 * c), Go truncates toward zero

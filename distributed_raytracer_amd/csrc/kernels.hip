@@ -66,6 +66,12 @@ __device__ __forceinline__ bool r2_certainly_out(double n, double d) {
 #ifndef MIRT_DIAG
 #define MIRT_DIAG 0
 #endif
+#ifndef MIRT_EXP_NO_PRIMARY_TRACE  // measurement builds only: every traced primary ray misses
+#define MIRT_EXP_NO_PRIMARY_TRACE 0
+#endif
+#ifndef MIRT_EXP_NO_TRI_TESTS  // measurement builds only: leaves are entered but never tested
+#define MIRT_EXP_NO_TRI_TESTS 0
+#endif
 constexpr int kDiagN = 32;
 __device__ unsigned long long g_diag[8 * kDiagN];
 __device__ __forceinline__ void diag(int k) {
@@ -76,10 +82,20 @@ __device__ __forceinline__ void diag(int k) {
     }
 }
 
+// Sound pre-reject for t >= 0 (triangle.go:67-71): true only when fl(n / d) is certainly
+// negative (q < -2^-1000, the first half of r2_certainly_out's argument), i.e. t < 0.
+__device__ __forceinline__ bool t_certainly_negative(double n, double d) {
+    return n * __builtin_copysign(0x1p1000, d) < -__builtin_fabs(d);
+}
+
 // Möller–Trumbore exactly as triangle.go:37-77, on (p1or = O - P1, E1, E2), returning
 // only the hit decision and the ray parameter.  neg = D * -1 (triangle.go:38).
 //   DG: diagnostic counter base (MIRT_DIAG builds).
-template <bool PREFILTER, int DG = 0>
+//   TPRE (shadow segments, whose rays leave the surface: the triangles they start on and
+//   those behind them have t < 0): t's numerator is computed up front and a certainly
+//   negative t rejects before any divide.  The conditions are a conjunction of pure tests,
+//   so their order changes no result.
+template <bool PREFILTER, int DG = 0, bool TPRE = false>
 __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t_out) {
     diag(DG + 0);
     V3 c = cross(e2, neg);
@@ -87,6 +103,11 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
     if (inc != 0.0) {
         double n2 = dot(p1or, c);
         if (PREFILTER && r2_certainly_out(n2, inc)) return false;
+        double nt = 0.0;
+        if (PREFILTER && TPRE) {
+            nt = dot(e1, cross(e2, p1or));
+            if (t_certainly_negative(nt, inc)) return false;
+        }
         diag(DG + 1);
         double r2 = n2 / inc;
         if (0.0 <= r2 && r2 <= 1.0) {
@@ -96,7 +117,7 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
                 double r1 = 1.0 - r2 - r3;
                 if (r1 >= 0.0 && r2 >= 0.0 && r3 >= 0.0) {
                     diag(DG + 3);
-                    double t = dot(e1, cross(e2, p1or)) / inc;
+                    double t = (PREFILTER && TPRE ? nt : dot(e1, cross(e2, p1or))) / inc;
                     if (t >= 0.0) {
                         diag(DG + 4);
                         t_out = t;
@@ -204,10 +225,11 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
 
 // Test n triangles at positions pos0.. of the BVH-ordered arrays; `src` points at the
 // record of position pos0 (in LDS or in HBM).
-template <bool REL, bool PREFILTER, int DG = 0, typename SrcPtr>
+template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
+    if (MIRT_EXP_NO_TRI_TESTS) return;
 #pragma unroll 2
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t k = pos0 + i;
@@ -218,7 +240,7 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         double tt;
         // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
         const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
-        if (mt_test<PREFILTER, DG>(p1or, e1, e2, neg, tt)) {
+        if (mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt)) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
         }
@@ -505,7 +527,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
             diag(SEG ? 14 : 6);
-            test_range<REL, PREFILTER, SEG ? 8 : 0>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
+            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
                                                     vis.tests);
             if (SEG) {
                 live = live && !(b.has && b.d < resolve);
@@ -520,9 +542,19 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
         diag(SEG ? 13 : 5);
         const uint64_t lm = __ballot(live);
         if (oct != kOctMixed) {
+            // far first: slot 0, the nearest, ends on top.  Empty slots come last in a copy,
+            // so slots 4..7 (2..3) are skipped at once when slot 4 (2) is empty; the test of
+            // any other empty slot fails (its box is lo = +inf, hi = -inf).
+            if (nd.child(4) != kBvhEmpty) {
 #pragma unroll
-            for (int c = 7; c >= 0; --c)  // far first: slot 0, the nearest, ends on top
-                stk.push_if(nd.child(c), slab_mask_ordered<true>(nd, c, r, tm), lm);
+                for (int c = 7; c >= 4; --c) stk.push_if(nd.child(c), slab_mask_ordered<true>(nd, c, r, tm), lm);
+            }
+            if (nd.child(2) != kBvhEmpty) {
+#pragma unroll
+                for (int c = 3; c >= 2; --c) stk.push_if(nd.child(c), slab_mask_ordered<true>(nd, c, r, tm), lm);
+            }
+#pragma unroll
+            for (int c = 1; c >= 0; --c) stk.push_if(nd.child(c), slab_mask_ordered<true>(nd, c, r, tm), lm);
         } else if (!all) {
 #pragma unroll
             for (int c = 7; c >= 0; --c) {
@@ -875,6 +907,9 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
                                           !(fa.flags & MIRT_OPT_NO_OCTANT));
     }
     if (b.has && b.d < resolve) return false;
+    // the nearest candidate (not a NaN-distance first hit, which wins regardless) lies beyond
+    // lh + 1e-4 + M from o: the occluder is farther from hit than the light
+    if (b.has && !b.first_nan && b.d > lh + 1e-4 + M) return true;
     uint32_t face, p;
     if (!best_result(b, face, p)) return true;
     V3 world, normal;
@@ -902,8 +937,8 @@ __device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restri
         const V3 ldir = norm(sub(lpos, hit));                         // tracer.go:61
         const V3 refl = sub(scale(n, 2 * dot(ldir, n)), ldir);        // tracer.go:65
         const V3 camdir = norm(sub(cam, hit));                        // tracer.go:66
-        col = c_add(col, c_mul(c_scale(kd, go_max(dot(ldir, n), 0.0)), lcol));                // :69
-        col = c_add(col, c_mul(c_scale(ks, go_pow(go_max(dot(refl, camdir), 0.0), ns)), lcol));  // :72
+        col = c_add(col, c_mul(c_scale(kd, go_max0(dot(ldir, n))), lcol));                // :69
+        col = c_add(col, c_mul(c_scale(ks, go_pow(go_max0(dot(refl, camdir)), ns)), lcol));  // :72
     }
     return col;
 }
@@ -1120,6 +1155,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     // classified (k_trace staging, block_may_meet): 1 culled, 2 may meet, 0 test here
     if (frustum && (classified == 1 || (classified == 0 && block_frustum(wa.fr, frect, px, py, vw, vh) == 0))) {
         ++ws.nodes;
+        diag(21);
         if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
             const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
             if (out.valid) out.valid[oidx] = 0;
@@ -1153,7 +1189,8 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
 
     Visits vis{0, 0, 0, 0};
     pc.lap(0);
-    Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d, active, true, vis, stk);
+    Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d,
+                                                                         active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis, stk);
     pc.lap(1);
     ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
     ws.nodes += vis.nodes;
@@ -1494,23 +1531,26 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
             const uint32_t b = blockIdx.x + (c0 + t) * G;  // over every frame's blocks
             const uint32_t f = b / nbf, bl = b - f * nbf;
             const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(bl % kQShards) * wa.per_shard + bl / kQShards];
-            uint32_t slot = t;
+            ready[t] = 0;
+            // FrameRec::live: a block with no pixel in the frame's live rectangle is not queued
+            const uint32_t px = v[1] & 0xffffu, py = v[1] >> 16, vw = (v[2] >> 16) & 0xffu, vh = v[2] >> 24;
+            const uint32_t* lv = wa.frames[f].live;
+            if (!(px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1])) continue;
             bool culled = false;
-            if (classify) {
-                culled = !block_may_meet(wa.frames[f].fr, frect[f], v[1] & 0xffffu, v[1] >> 16, (v[2] >> 16) & 0xffu,
-                                         v[2] >> 24);
-                if (partition) slot = culled ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
-            }
+            if (classify) culled = !block_may_meet(wa.frames[f].fr, frect[f], px, py, vw, vh);
+            // queue: blocks that may meet the object from the front, culled ones from the back
+            const uint32_t slot = (partition && culled) ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
             bq[slot][0] = v[0];
             bq[slot][1] = v[1];
             bq[slot][2] = v[2];
             bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
             bq_frame[slot] = (uint8_t)f;
-            ready[t] = 0;
         }
         if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
         if (c0 == 0) clock.mark_staged();
         __syncthreads();
+        // queued blocks: [0, s_front) and [s_back, nc); ticket q is entry q or q - nfront + s_back
+        const uint32_t nfront = s_front, back0 = s_back, nq = nfront + (nc - back0);
         LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
         for (;;) {
@@ -1519,9 +1559,13 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
             if (pend == kNone && lds_ld(&s_item) < avail) pend = lds_inc(&s_item);
             if (pend != kNone && pend < avail) {
                 const uint32_t c = pend / nl, l = pend - c * nl;
-                while (lds_ld(&ready[c]) == 0 && ++spins < kSpinLimit) __builtin_amdgcn_s_sleep(1);
+                while (lds_ld(&ready[c]) == 0 && ++spins < kSpinLimit) {
+                    diag(17);
+                    __builtin_amdgcn_s_sleep(1);
+                }
                 if (spins >= kSpinLimit) break;
                 ++taken;
+                diag(19);
                 ic.start();
                 const WaveStats before = wsh;
                 const FrameRec& fr = frame_rec(wa, __builtin_amdgcn_readfirstlane(chunk_frame[c]));
@@ -1532,13 +1576,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 continue;
             }
             // 2. a primary block
-            if (lds_ld(&s_prim) < nc) {
-                const uint32_t t = lds_inc(&s_prim);
-                if (t < nc) {
+            if (lds_ld(&s_prim) < nq) {
+                const uint32_t q = lds_inc(&s_prim);
+                if (q < nq) {
+                    const uint32_t t = q < nfront ? q : q - nfront + back0;
                     const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
                                        (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
                                        (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
                     ++taken;
+                    diag(20);
                     ic.start();
                     const WaveStats before = wp;
                     const uint64_t ph0 = pc.acc[0], ph1 = pc.acc[1];
@@ -1555,7 +1601,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 }
             }
             // 3. nothing available now: leave once every block is done and no item is left
-            if (lds_ld(&s_pdone) >= nc) {
+            if (lds_ld(&s_pdone) >= nq) {
                 const uint32_t total = lds_ld(&s_chunks) * nl;
                 if (pend == kNone) {
                     if (lds_ld(&s_item) >= total) break;
@@ -1565,6 +1611,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 continue;
             }
             if (++spins >= kSpinLimit) break;
+            diag(18);
             __builtin_amdgcn_s_sleep(1);
         }
         __syncthreads();  // every wave is done with this batch before it is restaged
@@ -2105,6 +2152,29 @@ hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uin
 
 // Copy a launch's frame records from pinned host memory to the device (one workgroup; a
 // hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there).
+// launch_fill_planes: grid x over 64 KiB chunks, y over planes, z over frames; 16-byte
+// stores (planes are hipMalloc'd, so 256-byte aligned), the tail byte by byte.
+__global__ __launch_bounds__(256) void k_fill_planes(FillJobs jobs) {
+    const uint32_t f = blockIdx.z, p = blockIdx.y;
+    uint8_t* dst = jobs.ptr[f][p];
+    if (!dst) return;
+    const uint64_t n = jobs.bytes[f][p];
+    const uint32_t v8 = jobs.value[f][p];
+    const uint32_t w = v8 | v8 << 8 | v8 << 16 | v8 << 24;
+    const uint4 q = make_uint4(w, w, w, w);
+    const uint64_t n16 = n / 16;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
+        ((uint4*)dst)[i] = q;
+    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) dst[n16 * 16 + threadIdx.x] = (uint8_t)v8;
+}
+
+hipError_t launch_fill_planes(const FillJobs& jobs, uint32_t nframes, uint64_t max_bytes, hipStream_t s) {
+    if (nframes == 0 || max_bytes == 0) return hipSuccess;
+    const uint32_t gx = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((max_bytes / 16 + 4095) / 4096, 1024));
+    hipLaunchKernelGGL(k_fill_planes, dim3(gx, kFillPlanes, nframes), dim3(256), 0, s, jobs);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                       uint32_t n16) {
     for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];

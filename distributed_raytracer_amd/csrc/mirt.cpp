@@ -498,6 +498,9 @@ void frame_record(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H
     fill_args(c, f, W, H, rec.fa, tris);
     frustum_args(c, f, rec.fa, rec.fr);
     rec.out = out;
+    rec.live[0] = rec.live[1] = 0;  // every block (a frame group narrows it to the hit rectangle)
+    rec.live[2] = W;
+    rec.live[3] = H;
 }
 
 // Frames whose records can share one k_trace launch (same mesh, objects, lights, options
@@ -772,6 +775,11 @@ double mirt_go_tan(double x) {
 }
 
 double mirt_go_pow(double x, double y) { return go_pow(x, y); }
+// test hook: op 0 go_min(a, b), 1 go_max(a, b), 2 go_min1(a), 3 go_max0(a) (the colour
+// code's constant-operand forms, pinned against the general ones by tests/test_host.py)
+double mirt_go_minmax(int op, double a, double b) {
+    return op == 0 ? go_min(a, b) : op == 1 ? go_max(a, b) : op == 2 ? go_min1(a) : go_max0(a);
+}
 
 int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn, uint32_t nn, const uint32_t* fv,
                      const uint32_t* fn, const uint32_t* fmat, uint32_t nf, const mirt_material* mats, uint32_t nm,
@@ -2189,12 +2197,39 @@ static int group_flush(mirt_group* g) {
             if (hipEventQuery(g->ev_done[b % g->FB]) == hipErrorNotReady) ++running;
         max_wg_now = std::max<uint32_t>(1, (uint32_t)(4 * (uint64_t)c->cus / (running + 1)));
     }
+    // Blocks outside a frame's hit rectangle (every ray misses) are not traced: a share's
+    // packed plane is only read inside the rectangle (k_pack_rect), and the whole-screen
+    // planes get their miss values first, one fill per batch (FrameRec::live).
+    bool narrow[kMaxFrames];
+    {
+        FillJobs fj{};
+        uint64_t fill_max = 0;
+        const uint64_t npx = (uint64_t)g->W * g->H;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t* R = br.rect[i];
+            narrow[i] = !(R[0] == 0 && R[1] == 0 && R[2] == g->W && R[3] == g->H) && !g->bbounces &&
+                        !(c->flags & MIRT_OPT_SPLIT_KERNELS);
+            if (!narrow[i] || g->tiled) continue;
+            const OutPlanes& o = g->fb[g->bj[i]];
+            const struct { void* p; uint64_t b; uint8_t v; } planes[kFillPlanes] = {
+                {o.rgb, npx * 24, 0}, {o.rgb8, npx * 3, 0}, {o.valid, npx, 0},
+                {o.face, npx * 4, 0xff}, {o.object, npx * 4, 0xff}, {o.rgbv, npx * 4, 0}};
+            for (int k = 0; k < kFillPlanes; ++k) {
+                fj.ptr[i][k] = (uint8_t*)planes[k].p;
+                fj.bytes[i][k] = planes[k].p ? planes[k].b : 0;
+                fj.value[i][k] = planes[k].v;
+                if (planes[k].p) fill_max = std::max(fill_max, planes[k].b);
+            }
+        }
+        if (fill_max) HIP_TRY(launch_fill_planes(fj, n, fill_max, s));
+    }
     for (Share& sh : g->shares) {
         Slot* sl = sh.slots[bs].get();
         for (uint32_t i = 0; i < n; ++i) {
             sl->h_frames[i] = g->stage[i];
             sl->h_frames[i].out = g->tiled ? OutPlanes{nullptr, nullptr, nullptr, nullptr, nullptr, sh.packed[g->bj[i]]}
                                            : g->fb[g->bj[i]];
+            if (narrow[i]) memcpy(sl->h_frames[i].live, br.rect[i], sizeof(br.rect[i]));
         }
         int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr,
                               max_wg_now);

@@ -208,6 +208,11 @@ struct alignas(16) FrameRec {
     FrameArgs fa;
     OutPlanes out;
     FrustumArgs fr;
+    // Blocks with no pixel in [live[0], live[2]) x [live[1], live[3]) are not traced: every
+    // ray of such a block misses, and the caller either cleared their outputs (a frame
+    // group's whole-screen planes, launch_fill_planes) or never reads them (a share's packed
+    // plane, of which k_pack_rect sends only the hit rectangle).  {0, 0, W, H}: every block.
+    uint32_t live[4];
 };
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
@@ -300,6 +305,16 @@ struct HostCopyJobs {
     uint32_t rect[kMaxFrames][4];  // columns to visit: x0, -, x1, - (half-open)
     uint32_t cur[kMaxFrames][4];   // this frame's hit rectangle (where to look for hits)
 };
+// Miss values into whole planes before a frame is traced (mirt_group, whole screen): per
+// frame up to kFillPlanes byte ranges, each set to one byte value (0, or 0xff for the int32
+// -1 of face / object).
+constexpr int kFillPlanes = 6;
+struct FillJobs {
+    uint8_t* ptr[kMaxFrames][kFillPlanes];
+    uint64_t bytes[kMaxFrames][kFillPlanes];
+    uint8_t value[kMaxFrames][kFillPlanes];
+};
+hipError_t launch_fill_planes(const FillJobs& jobs, uint32_t nframes, uint64_t max_bytes, hipStream_t s);
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
                                  hipStream_t s);
 hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,

@@ -172,6 +172,9 @@ int mirt_camera_init(const double pos[3], const double dir[3], double fov, mirt_
 double mirt_go_tan(double x);
 /* Restatement of Go's math.Pow (the specular term of tracer.go:72). */
 double mirt_go_pow(double x, double y);
+/* Test hook: op 0 Go math.Min(a, b), 1 math.Max(a, b), 2 Min(a, 1.0), 3 Max(a, 0.0) — the
+ * last two as the colour code computes them (colour.go:38-50, tracer.go:69-72). */
+double mirt_go_minmax(int op, double a, double b);
 
 /*
  * Upload one immutable mesh (shared/state/mesh.go:100-106 after MeshFromFile):

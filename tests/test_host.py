@@ -124,9 +124,32 @@ def test_camera_and_go_math_match_oracle():
         assert L.lib().mirt_go_tan(float(x)) == go_tan(float(x))
     for x, y in zip(rng.random(5000), rng.integers(0, 50, 5000)):
         assert L.lib().mirt_go_pow(float(x), float(y)) == go_pow(float(x), float(y))
+    # the small-integer-exponent path and its edges (x in [2^-60, 16], 2 <= y <= 16)
+    xs = np.concatenate([rng.uniform(0, 16.5, 3000), 2.0 ** rng.uniform(-70, -50, 500),
+                         [2.0 ** -60, np.nextafter(2.0 ** -60, 0), 16.0, np.nextafter(16.0, 99), 1.0, 0.5, 0.0, -0.0]])
+    for x in xs:
+        for y in (2.0, 3.0, 7.0, 10.0, 16.0, 17.0, 2.5):
+            assert L.lib().mirt_go_pow(float(x), y) == go_pow(float(x), y), (x, y)
     with pytest.raises(rt.MirtError) as e:
         rt.Camera.new((0, 0, 0), (0, 3, 0), 1.0)
     assert e.value.code == L.MIRT_E_CAMERA
+
+
+def test_constant_operand_min_max_are_go_min_max():
+    """colour.go's clamps with a constant operand (go_min1 = Min(a, 1), go_max0 = Max(a, 0)
+    = Max(0, a)) return Go's Min / Max result bit for bit, signed zeros and NaN included."""
+    import distributed_raytracer_amd._lib as L
+    from oracle.np_oracle import go_max as py_max, go_min as py_min
+    f = L.lib().mirt_go_minmax
+    rng = np.random.default_rng(11)
+    vals = [0.0, -0.0, 1.0, -1.0, 0.5, 1.0 + 2 ** -52, 1.0 - 2 ** -53, np.inf, -np.inf, np.nan, 5e-324, -5e-324,
+            1e308, -1e308] + list(rng.normal(size=200)) + list(rng.uniform(0.9, 1.1, 200))
+    same = lambda a, b: (np.isnan(a) and np.isnan(b)) or (a == b and np.signbit(a) == np.signbit(b))  # noqa: E731
+    for a in vals:
+        a = float(a)
+        assert same(f(2, a, 0.0), f(0, a, 1.0)) and same(f(0, a, 1.0), py_min(a, 1.0)), a
+        assert same(f(3, a, 0.0), f(1, a, 0.0)) and same(f(3, a, 0.0), f(1, 0.0, a)), a
+        assert same(f(1, a, 0.0), py_max(a, 0.0)) and same(f(1, 0.0, a), py_max(0.0, a)), a
 
 
 def test_tile_deal_spreads_rows_and_columns():

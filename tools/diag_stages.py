@@ -28,6 +28,8 @@ def main():
     names = ["tests", "past r2 pre-reject", "past r2 range", "past r3 checks", "hits", "node visits", "leaves"]
     for base, kind in ((0, "primary"), (8, "shadow")):
         print(kind, "  ".join(f"{nm}={c[base + i]:.0f}" for i, nm in enumerate(names)))
+    print("k_trace: ready-wait spins", c[17], " idle spins", c[18], " shadow items", c[19], " primary blocks", c[20],
+          " culled blocks", c[21])
     g.close()
 
 
