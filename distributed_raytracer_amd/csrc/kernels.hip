@@ -2089,46 +2089,49 @@ hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t m
 }
 
 // Bytes [a, b) of src -> dst with the same alignment on both sides (same layout): head
-// bytes, 16-byte words, tail bytes; one workgroup.
+// bytes, 16-byte words, tail bytes; one wave.
 __device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t a,
-                                          uint64_t b) {
+                                          uint64_t b, uint32_t lane) {
     const uint64_t a16 = min(b, (a + 15) & ~15ull), b16 = max(a16, b & ~15ull);
-    for (uint64_t i = a + threadIdx.x; i < a16; i += blockDim.x) dst[i] = src[i];
-    for (uint64_t i = a16 + 16 * threadIdx.x; i < b16; i += 16 * blockDim.x)
-        *(uint4*)(dst + i) = *(const uint4*)(src + i);
-    for (uint64_t i = b16 + threadIdx.x; i < b; i += blockDim.x) dst[i] = src[i];
+    if (a + lane < a16) dst[a + lane] = src[a + lane];
+    for (uint64_t i = a16 + 16 * lane; i < b16; i += 16 * 64) *(uint4*)(dst + i) = *(const uint4*)(src + i);
+    if (b16 + lane < b) dst[b16 + lane] = src[b16 + lane];
 }
-// grid x: columns, z: frame.  Column x holds rows contiguously in both planes (x * H + y).
-// The column's hit span is found from the valid plane inside this frame's hit rectangle;
-// the rows of its union with the span the host slot held are copied.
+// grid x: groups of 4 columns (one wave each), z: frame.  Column x holds rows contiguously
+// in both planes (x * H + y).  The column's hit span is found from the valid plane inside
+// this frame's hit rectangle (64 rows per step, from each end inwards: the rows inside the
+// span are never read); the rows of its union with the span the host slot held are
+// copied.  Waves are independent (no barrier), so a column's wave retires as soon as its
+// copy is issued.
 __global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint32_t H) {
-    __shared__ uint32_t s_lo, s_hi;
-    const uint32_t f = blockIdx.z;
+    const uint32_t f = blockIdx.z, lane = threadIdx.x & 63;
     const uint32_t* R = jobs.rect[f];
     const uint32_t* C = jobs.cur[f];
-    for (uint32_t x = R[0] + blockIdx.x; x < R[2]; x += gridDim.x) {
-        if (threadIdx.x == 0) {
-            s_lo = 0xffffffffu;
-            s_hi = 0;
-        }
-        __syncthreads();
+    for (uint32_t x = R[0] + blockIdx.x * 4 + (threadIdx.x >> 6); x < R[2]; x += gridDim.x * 4) {
+        uint32_t a = 1, b = 0;  // this frame's hit rows [a, b) (empty: a > b)
         if (x >= C[0] && x < C[2]) {
-            uint32_t lo = 0xffffffffu, hi = 0;
             const uint8_t* v = jobs.valid[f] + (uint64_t)x * H;
-            for (uint32_t y = C[1] + threadIdx.x; y < C[3]; y += blockDim.x)
-                if (v[y]) {
-                    lo = min(lo, y);
-                    hi = max(hi, y + 1);
+            bool found = false;
+            for (uint32_t y0 = C[1]; y0 < C[3]; y0 += 64) {  // first hit row, upwards
+                const uint32_t y = y0 + lane;
+                const uint64_t m = __ballot(y < C[3] && v[y] != 0);
+                if (m) {
+                    a = y0 + (uint32_t)__builtin_ctzll(m);
+                    found = true;
+                    break;
                 }
-            if (lo != 0xffffffffu) {
-                atomicMin(&s_lo, lo);
-                atomicMax(&s_hi, hi);
+            }
+            // last hit row, downwards from the rectangle's end (row a is a hit: it stops there)
+            for (uint32_t y1 = C[3]; found; y1 -= 64) {
+                const uint64_t m = __ballot(lane < y1 - a && v[y1 - 1 - lane] != 0);
+                if (m) {
+                    b = y1 - (uint32_t)__builtin_ctzll(m);
+                    break;
+                }
             }
         }
-        __syncthreads();
         const uint32_t prev = jobs.spans[f][x];
         const uint32_t a0 = prev & 0xffffu, b0 = prev >> 16;
-        const uint32_t a = s_lo, b = s_hi;  // empty: a > b
         uint32_t u0 = a0, u1 = b0;
         if (a < b) {
             u0 = a0 < b0 ? min(a, a0) : a;
@@ -2136,16 +2139,15 @@ __global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint3
         }
         if (u0 < u1) {
             const uint64_t p0 = (uint64_t)x * H + u0, p1 = (uint64_t)x * H + u1;
-            copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1);
-            copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1);
+            copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1, lane);
+            copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1, lane);
         }
-        __syncthreads();  // every thread read the old span and s_lo/s_hi
-        if (threadIdx.x == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
+        if (lane == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
     }
 }
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
                                  hipStream_t s) {
-    const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>(max_cols, 2048));
+    const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((max_cols + 3) / 4, 1024));
     hipLaunchKernelGGL(k_copy_rect_host, dim3(gx, 1, nframes), dim3(256), 0, s, jobs, H);
     return hipGetLastError();
 }
