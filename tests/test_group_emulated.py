@@ -107,14 +107,22 @@ def test_bench_path_full_frame(ctx, views):
 @pytest.mark.gpu
 @pytest.mark.parametrize("tile,emulate", [(None, 0), (8, 8)])
 def test_host_output_frames(ctx, views, tile, emulate):
-    """mirt_group_set_host_output: the assembled frame lands in pinned host memory (only the
-    hit rectangle and the previous one are copied); the host planes equal the oracle on
-    every pixel while the rectangle moves and empties between frames."""
+    """mirt_group_set_host_output: the assembled frame lands in pinned host memory (the copy
+    kernel covers only each column's hit span and the slot's previous one); the host planes
+    equal the oracle on every pixel while the rectangle moves and empties between frames,
+    and after host output was switched off and on again."""
     from distributed_raytracer_amd.framebuffer import NativeFrameGroup
     g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=2, batch=1, emulate=emulate, host_output=True)
     try:
         prev = None
-        for name in ORDER:
+        for k, name in enumerate(ORDER):
+            if k == 4:  # frames traced with the host output off never reach the host slots
+                g.set_host_output(False)
+                g.render(views["inside"][0])
+                g.render(views["edge"][0])
+                g.wait()
+                g.set_host_output(True)
+                prev = None
             idx = g.render(views[name][0])
             if prev is not None:
                 rgb8, valid = g.host_frame(prev[0])
