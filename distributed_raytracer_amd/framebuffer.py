@@ -126,6 +126,76 @@ def gather_packed(buf, world: int, rank: int, root: int = 0, group=None):
     return out
 
 
+class PeerFailure(RuntimeError):
+    """Ranks whose frame transfer did not reach the root before the deadline — the
+    torch.distributed counterpart of mirt_group's MIRT_E_PEER (master/pool/pool.go:224-260:
+    a worker that stops answering heartbeats is dropped)."""
+
+    def __init__(self, ranks: Sequence[int], frame: int):
+        self.ranks, self.frame = sorted(ranks), frame
+        super().__init__(f"frame {frame}: no transfer from rank(s) {self.ranks} before the deadline")
+
+
+def gather_with_deadline(pg, buf, me: int, n: int, deadline_s: float = 5.0, frame: int = 0, root: int = 0,
+                         members: Optional[Sequence[int]] = None):
+    """Gather `buf` from every rank of process group `pg` (a ProcessGroup used directly:
+    ranks 0..n-1, this process is `me`) to `root` with point-to-point transfers — the shape
+    of mirt_group's RCCL send/recv group — every receive bounded by one shared deadline.
+    On the root: the list of n buffers, or PeerFailure naming each rank whose transfer
+    missed the deadline or whose process is gone (`members` maps group ranks to the
+    caller's rank numbers; the frame is skipped, as the master skips a frame,
+    master/main.go:153-161).  Elsewhere: None, once the send completed or the deadline
+    passed."""
+    import datetime
+    import time
+    import torch
+    if me != root:
+        w = pg.send([buf], root, frame)
+        try:  # bounded: a root that gave up on this frame never takes the transfer
+            w.wait(datetime.timedelta(seconds=deadline_s))
+        except RuntimeError:
+            pass
+        return None
+    out = [torch.empty_like(buf) for _ in range(n)]
+    out[root].copy_(buf)
+    end = time.monotonic() + deadline_s
+    failed, works = [], {}
+    for q in range(n):
+        if q == root:
+            continue
+        try:
+            works[q] = pg.recv([out[q]], q, frame)
+        except RuntimeError:  # the peer's process is gone (connection closed)
+            failed.append(q)
+    for q, w in works.items():
+        left = max(1e-3, end - time.monotonic())
+        try:
+            ok = w.wait(datetime.timedelta(seconds=left))
+        except RuntimeError:  # gloo reports a timed-out wait (or a lost peer) as an error
+            ok = False
+        if ok is False:
+            failed.append(q)
+    failed = [members[q] if members is not None else q for q in sorted(failed)]
+    if failed:
+        raise PeerFailure(failed, frame)
+    return out
+
+
+def frame_group_gloo(store, ranks: Sequence[int], rank: int, epoch: int, timeout_s: float = 30.0):
+    """A gloo process group over `ranks` (sorted; this process is `rank`), built straight
+    from the shared store: the first group of a frame loop, or after a failure the group of
+    the survivors (mirt_group_exclude's counterpart: a new communicator from the store,
+    never a collective that would wait for the dead rank).  Returns (group, index of this
+    rank in it, group size)."""
+    import datetime
+    import torch.distributed as dist
+    ranks = sorted(ranks)
+    me = ranks.index(rank)
+    pg = dist.ProcessGroupGloo(dist.PrefixStore(f"mirt_frames_{epoch}", store), me, len(ranks),
+                               datetime.timedelta(seconds=timeout_s))
+    return pg, me, len(ranks)
+
+
 @dataclass
 class DevicePlanes:
     """Device tensors of one packed or full-frame output (torch, on the context's GPU)."""
