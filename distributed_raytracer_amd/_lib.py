@@ -23,6 +23,7 @@ MIRT_E_IO = -7
 MIRT_E_TIMEOUT = -8
 MIRT_E_PEER = -9
 MIRT_MAX_OBJECTS = 16
+MIRT_NO_MESH = 0xFFFFFFFF
 MIRT_MAX_LIGHTS = 16
 MIRT_OPT_NO_PREFILTER = 1
 MIRT_OPT_BRUTE_FORCE = 2
@@ -159,6 +160,9 @@ SIGNATURES = {
     "mirt_scene_light_count": (C.c_uint32, [_P]),
     "mirt_scene_light": (C.c_int, [_P, C.c_uint32, C.POINTER(Light)]),
     "mirt_scene_camera": (C.c_int, [_P, C.POINTER(Camera)]),
+    "mirt_scene_from_gob": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "mirt_scene_link_gob": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "mirt_gob_json": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
 _lib = None

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <fstream>
@@ -29,6 +30,7 @@
 #include <vector>
 
 #include "../../include/mirt_scene.h"
+#include "gob.hpp"
 
 namespace {
 
@@ -404,11 +406,14 @@ bool load_mesh(const std::string& path, MeshData& m, std::string& err) {
 }  // namespace
 
 struct mirt_scene {
-    std::vector<std::unique_ptr<MeshData>> meshes;
+    // shared: a scene linked from a gob diff (mirt_scene_link_gob) uses its environment's meshes
+    std::vector<std::shared_ptr<MeshData>> meshes;
     std::vector<mirt_object> objects;
     std::vector<mirt_light> lights;
     mirt_camera cam;
-    int cam_rc = 0;
+    bool has_cam = false;
+    // object id -> mesh index (envImmutables.paths through .meshes; gob environments only)
+    std::map<uint64_t, uint32_t> id_mesh;
 };
 
 extern "C" {
@@ -439,7 +444,7 @@ int mirt_scene_load(const char* path, mirt_scene** out) {
             auto it = by_model.find(mp);
             uint32_t mi;
             if (it == by_model.end()) {
-                std::unique_ptr<MeshData> md(new MeshData());
+                std::shared_ptr<MeshData> md(new MeshData());
                 std::string err;
                 if (!load_mesh(relative_path(path, mp), *md, err)) {
                     md.reset(new MeshData());
@@ -484,12 +489,105 @@ int mirt_scene_load(const char* path, mirt_scene** out) {
     jvec(cam ? cam->get("pos") : nullptr, cp);
     jvec(cam ? cam->get("dir") : nullptr, cd);
     double fov = jnum(cam ? cam->get("fov") : nullptr);
-    s->cam_rc = mirt_camera_init(cp, cd, fov, &s->cam);
-    if (s->cam_rc != MIRT_OK) {
+    if (mirt_camera_init(cp, cd, fov, &s->cam) != MIRT_OK) {
         g_scene_err = "Camera dir is parallel to global up";
         return MIRT_E_CAMERA;
     }
+    s->has_cam = true;
     *out = s.release();
+    return MIRT_OK;
+}
+
+// worker/distributed/main.go:118-126 register: MasterState.state -> the immutable scene.
+// Meshes in model-path order (the wire carries a Go map, whose order is random).
+int mirt_scene_from_gob(const uint8_t* state, size_t n, mirt_scene** out) {
+    if (!state || !out) return MIRT_E_INVALID;
+    *out = nullptr;
+    mirt::gob::Immutables im;
+    std::string err;
+    if (!mirt::gob::decode_environment(state, n, im, err)) {
+        g_scene_err = err;
+        return MIRT_E_IO;
+    }
+    std::sort(im.meshes.begin(), im.meshes.end(),
+              [](const auto& a, const auto& b) { return a.first < b.first; });
+    std::unique_ptr<mirt_scene> s(new mirt_scene());
+    std::map<std::string, uint32_t> by_path;
+    for (auto& pm : im.meshes) {
+        if (by_path.count(pm.first)) {
+            g_scene_err = "gob Environment: model path twice in the mesh map";
+            return MIRT_E_IO;
+        }
+        const mirt::gob::Mesh& g = pm.second;
+        std::shared_ptr<MeshData> md(new MeshData());
+        if (g.v.size() / 3 > 0xffffffffull || g.fmat.size() > 0xffffffffull) {
+            g_scene_err = "gob Environment: mesh too large";
+            return MIRT_E_IO;
+        }
+        md->v = g.v;
+        md->vn = g.vn;
+        // a mesh without normals carries zero normal indices (mesh.go:167-169); keep them so
+        md->fv.assign(g.fv.begin(), g.fv.end());
+        md->fn.assign(g.fn.begin(), g.fn.end());
+        md->fmat.assign(g.fmat.begin(), g.fmat.end());
+        md->mats = g.mats;
+        by_path.emplace(pm.first, (uint32_t)s->meshes.size());
+        s->meshes.push_back(std::move(md));
+    }
+    for (auto& ip : im.paths) {  // LinkTo (environment.go:80-88): id -> path -> mesh
+        auto it = by_path.find(ip.second);
+        if (it != by_path.end()) s->id_mesh[ip.first] = it->second;
+    }
+    *out = s.release();
+    return MIRT_OK;
+}
+
+// worker/distributed/main.go:56-64 BulkTrace: WorkOrder.diff decoded and linked to env.
+int mirt_scene_link_gob(const mirt_scene* env, const uint8_t* diff, size_t n, mirt_scene** out) {
+    if (!env || !diff || !out) return MIRT_E_INVALID;
+    *out = nullptr;
+    mirt::gob::Mutables mu;
+    std::string err;
+    if (!mirt::gob::decode_mutables(diff, n, mu, err)) {
+        g_scene_err = err;
+        return MIRT_E_IO;
+    }
+    std::unique_ptr<mirt_scene> s(new mirt_scene());
+    s->meshes = env->meshes;
+    s->id_mesh = env->id_mesh;
+    for (const auto& o : mu.objects) {
+        mirt_object ob{};
+        auto it = env->id_mesh.find(o.id);
+        ob.mesh_id = it == env->id_mesh.end() ? MIRT_NO_MESH : it->second;  // environment.go:80-88
+        ob.pos[0] = o.pos[0];
+        ob.pos[1] = o.pos[1];
+        ob.pos[2] = o.pos[2];
+        s->objects.push_back(ob);
+    }
+    s->lights = mu.lights;
+    // camera.go:196-200: NewCamera(pos, forward, fov), an error if forward is parallel to up
+    if (mirt_camera_init(mu.cam_pos, mu.cam_forward, mu.fov, &s->cam) != MIRT_OK) {
+        g_scene_err = "gob EnvMutables: Camera dir is parallel to global up";
+        return MIRT_E_CAMERA;
+    }
+    s->has_cam = true;
+    *out = s.release();
+    return MIRT_OK;
+}
+
+int mirt_gob_json(const uint8_t* data, size_t n, char* out, size_t cap, size_t* len) {
+    if (!data || !len) return MIRT_E_INVALID;
+    std::string js, err;
+    if (!mirt::gob::to_json(data, n, js, err)) {
+        g_scene_err = err;
+        return MIRT_E_IO;
+    }
+    *len = js.size();
+    if (out && cap) {
+        const size_t k = std::min(cap - 1, js.size());
+        memcpy(out, js.data(), k);
+        out[k] = 0;
+    }
     return MIRT_OK;
 }
 
@@ -525,7 +623,7 @@ int mirt_scene_light(const mirt_scene* s, uint32_t i, mirt_light* out) {
     return MIRT_OK;
 }
 int mirt_scene_camera(const mirt_scene* s, mirt_camera* out) {
-    if (!s || !out) return MIRT_E_INVALID;
+    if (!s || !out || !s->has_cam) return MIRT_E_INVALID;
     *out = s->cam;
     return MIRT_OK;
 }

@@ -221,48 +221,62 @@ class MeshArrays:
     materials: np.ndarray  # (nm, 10)
 
 
+def _scene_meshes(h) -> List[MeshArrays]:
+    lib = L.lib()
+    meshes = []
+    for i in range(lib.mirt_scene_mesh_count(h)):
+        mv = L.MeshView()
+        L.check(lib.mirt_scene_mesh(h, i, C.byref(mv)))
+
+        def arr(ptr, n, dt):
+            if n == 0 or not ptr:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
+
+        mats = np.zeros((mv.n_materials, 10))
+        for k in range(mv.n_materials):
+            m = mv.materials[k]
+            mats[k] = list(m.ka) + list(m.kd) + list(m.ks) + [m.ns]
+        meshes.append(MeshArrays(
+            vertices=arr(mv.vertices, 3 * mv.n_vertices, np.float64).reshape(-1, 3),
+            normals=arr(mv.normals, 3 * mv.n_normals, np.float64).reshape(-1, 3),
+            face_v=arr(mv.face_v, 3 * mv.n_faces, np.uint32).reshape(-1, 3),
+            face_n=arr(mv.face_n, 3 * mv.n_faces, np.uint32).reshape(-1, 3),
+            face_mat=arr(mv.face_mat, mv.n_faces, np.uint32),
+            materials=mats))
+    return meshes
+
+
+def _scene_mutables(h) -> Tuple[List[Tuple[int, Vec]], List[Light], Camera]:
+    lib = L.lib()
+    objects = []
+    for i in range(lib.mirt_scene_object_count(h)):
+        o = L.Object()
+        L.check(lib.mirt_scene_object(h, i, C.byref(o)))
+        objects.append((o.mesh_id, tuple(o.pos)))
+    lights = []
+    for i in range(lib.mirt_scene_light_count(h)):
+        lt = L.Light()
+        L.check(lib.mirt_scene_light(h, i, C.byref(lt)))
+        lights.append(Light(tuple(lt.pos), tuple(lt.col)))
+    cam = L.Camera()
+    L.check(lib.mirt_scene_camera(h, C.byref(cam)))
+    return objects, lights, Camera._from_c(cam)
+
+
+def _scene_error(rc: int):
+    return L.MirtError(rc, (L.lib().mirt_scene_last_error() or b"").decode())
+
+
 def load_scene_arrays(path: str) -> Tuple[List[MeshArrays], List[Tuple[int, Vec]], List[Light], Camera]:
     """Parse scene.json + OBJ/MTL with the library's C++ loader (mirt_scene_load)."""
     lib = L.lib()
     h = C.c_void_p()
     rc = lib.mirt_scene_load(path.encode(), C.byref(h))
     if rc != L.MIRT_OK:
-        raise L.MirtError(rc, (lib.mirt_scene_last_error() or b"").decode())
+        raise _scene_error(rc)
     try:
-        meshes = []
-        for i in range(lib.mirt_scene_mesh_count(h)):
-            mv = L.MeshView()
-            L.check(lib.mirt_scene_mesh(h, i, C.byref(mv)))
-
-            def arr(ptr, n, dt):
-                if n == 0 or not ptr:
-                    return np.zeros(0, dt)
-                return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
-
-            mats = np.zeros((mv.n_materials, 10))
-            for k in range(mv.n_materials):
-                m = mv.materials[k]
-                mats[k] = list(m.ka) + list(m.kd) + list(m.ks) + [m.ns]
-            meshes.append(MeshArrays(
-                vertices=arr(mv.vertices, 3 * mv.n_vertices, np.float64).reshape(-1, 3),
-                normals=arr(mv.normals, 3 * mv.n_normals, np.float64).reshape(-1, 3),
-                face_v=arr(mv.face_v, 3 * mv.n_faces, np.uint32).reshape(-1, 3),
-                face_n=arr(mv.face_n, 3 * mv.n_faces, np.uint32).reshape(-1, 3),
-                face_mat=arr(mv.face_mat, mv.n_faces, np.uint32),
-                materials=mats))
-        objects = []
-        for i in range(lib.mirt_scene_object_count(h)):
-            o = L.Object()
-            L.check(lib.mirt_scene_object(h, i, C.byref(o)))
-            objects.append((o.mesh_id, tuple(o.pos)))
-        lights = []
-        for i in range(lib.mirt_scene_light_count(h)):
-            lt = L.Light()
-            L.check(lib.mirt_scene_light(h, i, C.byref(lt)))
-            lights.append(Light(tuple(lt.pos), tuple(lt.col)))
-        cam = L.Camera()
-        L.check(lib.mirt_scene_camera(h, C.byref(cam)))
-        return meshes, objects, lights, Camera._from_c(cam)
+        return (_scene_meshes(h),) + _scene_mutables(h)
     finally:
         lib.mirt_scene_free(h)
 
@@ -270,11 +284,13 @@ def load_scene_arrays(path: str) -> Tuple[List[MeshArrays], List[Tuple[int, Vec]
 class Environment:
     """state.Environment: immutable meshes resident on the device + the mutable part."""
 
-    def __init__(self, ctx: Context, mesh_ids: List[int], mutable: EnvMutables, meshes: List[MeshArrays]):
+    def __init__(self, ctx: Context, mesh_ids: List[int], mutable: Optional[EnvMutables], meshes: List[MeshArrays],
+                 gob_scene=None):
         self.ctx = ctx
         self.mesh_ids = mesh_ids
         self._mutable = mutable
         self.meshes = meshes
+        self._gob = gob_scene  # mirt_scene handle of a gob environment (mirt_scene_link_gob)
 
     @classmethod
     def from_file(cls, path: str, ctx: Context) -> "Environment":
@@ -283,8 +299,54 @@ class Environment:
         mut = EnvMutables([SceneObject(ids[mi], pos) for mi, pos in objects], lights, cam)
         return cls(ctx, ids, mut, meshes)
 
+    @classmethod
+    def from_gob(cls, state: bytes, ctx: Context) -> "Environment":
+        """worker/distributed/main.go:118-126: the Register reply's MasterState.state (a gob
+        state.Environment) decoded by the library (mirt_scene_from_gob); meshes uploaded.
+        It has no mutable part until a WorkOrder diff is linked (link_gob)."""
+        lib = L.lib()
+        h = C.c_void_p()
+        rc = lib.mirt_scene_from_gob(bytes(state), len(state), C.byref(h))
+        if rc != L.MIRT_OK:
+            raise _scene_error(rc)
+        try:
+            meshes = _scene_meshes(h)
+            ids = [ctx.upload_mesh(m.vertices, m.normals, m.face_v, m.face_n, m.face_mat, m.materials) for m in meshes]
+        except Exception:
+            lib.mirt_scene_free(h)
+            raise
+        return cls(ctx, ids, None, meshes, gob_scene=h)
+
+    def link_gob(self, diff: bytes) -> EnvMutables:
+        """worker/distributed/main.go:56-64: decode a WorkOrder.diff (gob state.EnvMutables)
+        and LinkTo this environment.  Objects whose id links to no mesh are dropped (a nil
+        mesh is never hit, object.go:73-74)."""
+        if self._gob is None:
+            raise L.MirtError(L.MIRT_E_INVALID, "link_gob needs an environment made by from_gob")
+        lib = L.lib()
+        h = C.c_void_p()
+        rc = lib.mirt_scene_link_gob(self._gob, bytes(diff), len(diff), C.byref(h))
+        if rc != L.MIRT_OK:
+            raise _scene_error(rc)
+        try:
+            objects, lights, cam = _scene_mutables(h)
+        finally:
+            lib.mirt_scene_free(h)
+        return EnvMutables([SceneObject(self.mesh_ids[mi], pos) for mi, pos in objects if mi != L.MIRT_NO_MESH],
+                           lights, cam)
+
     def mutable(self) -> EnvMutables:
+        if self._mutable is None:
+            raise L.MirtError(L.MIRT_E_INVALID, "a gob environment has no mutable part: link a diff (link_gob)")
         return self._mutable
+
+    def __del__(self):
+        if getattr(self, "_gob", None) is not None:
+            try:
+                L.lib().mirt_scene_free(self._gob)
+            except Exception:  # noqa: BLE001 — interpreter shutdown
+                pass
+            self._gob = None
 
 
 # --------------------------------------------------------------------- tracing
@@ -369,13 +431,14 @@ def draw(env: Environment, width: int, height: int, mut: Optional[EnvMutables] =
 # --------------------------------------------------------------------- BulkTrace
 @dataclass
 class WorkOrder:
-    """comms.WorkOrder (comms.proto:25-31).  diff: an EnvMutables for this frame, or None
-    for the registered scene's own state (the Go worker decodes a gob diff instead)."""
+    """comms.WorkOrder (comms.proto:25-31).  diff: the wire bytes (a gob state.EnvMutables,
+    decoded and linked as worker/distributed/main.go:56-64 does), an already decoded
+    EnvMutables, or None for the registered scene's own state."""
     x: int
     y: int
     width: int
     height: int
-    diff: Optional[EnvMutables] = None
+    diff: Optional[object] = None
 
 
 @dataclass
@@ -393,8 +456,9 @@ class Tracer:
         self.screen_height = screen_height
 
     def bulk_trace(self, req: WorkOrder, cancel: Optional[C.c_int] = None) -> TraceResults:
+        diff = self.scene.link_gob(req.diff) if isinstance(req.diff, (bytes, bytearray)) else req.diff
         r = trace_tile(self.scene, req.x, req.y, req.width, req.height, self.screen_width, self.screen_height,
-                       req.diff, cancel)
+                       diff, cancel)
         return TraceResults(r.rgb8)
 
     def heartbeat(self) -> None:

@@ -47,3 +47,34 @@ def test_c_worker_frames_match_golden(tmp_path, W, H, golden, workers):
         hit = np.nonzero(valid)[0]
         assert np.array_equal(hit, g["hit_index"].astype(np.int64))
         assert np.array_equal(rgb8[hit], g["rgb8"]) and not rgb8[valid == 0].any()
+
+
+def _run_gob(name, W, H, out, workers=4):
+    gob = os.path.join(GOLDEN, "gob")
+    return subprocess.run([BIN, "--gob", os.path.join(gob, f"{name}_state.gob"), os.path.join(gob, f"{name}_diff.gob"),
+                           str(W), str(H), str(out), str(workers)], capture_output=True, text=True, timeout=120,
+                          env={k: v for k, v in os.environ.items() if not k.startswith("PYTHON")})
+
+
+def test_c_worker_decodes_the_wire_before_the_device(tmp_path):
+    """--gob: MasterState.state and a WorkOrder.diff decoded in C (no Go, no Python); without
+    a GPU the run gets past the decoding and fails at mirt_create."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = _run_gob("multi", 64, 48, tmp_path / "o.bin")
+    assert r.returncode == 2 and "mirt_create" in r.stderr and "gob" not in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,W,H", [("example", 320, 240), ("multi", 160, 120)])
+def test_c_worker_from_the_wire_matches_oracle(tmp_path, name, W, H):
+    from oracle.oracle import Oracle
+    from test_gob import scenes, wire_scene
+    out = tmp_path / "fb.bin"
+    r = _run_gob(name, W, H, out, 5)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = np.fromfile(out, np.uint8)
+    ref = Oracle(wire_scene(scenes()[name][0])).frame(W, H)
+    assert np.array_equal(raw[W * H * 3:], ref["valid"])
+    assert np.array_equal(raw[:W * H * 3].reshape(W * H, 3), ref["rgb8"])

@@ -1,0 +1,242 @@
+"""The gob wire state (Register's MasterState.state, every WorkOrder.diff) decoded by the
+library's C++ decoder (csrc/gob.cpp, include/mirt_scene.h).
+
+Pinned by the encoding/gob documentation's own vectors (the Point{22, 33} stream with its
+type definition, and 17.0 = FE 31 40) and by hand-assembled streams built from the spec.
+The scene fixtures (tests/golden/gob/*.gob) come from tests/golden/gob_go.py, an encoder
+restatement: parity UNPINNED against a real Go encoder (no Go toolchain in this image).
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import gob_go as G  # noqa: E402
+from distributed_raytracer_amd import _lib as L  # noqa: E402
+from oracle.scene_py import load_scene  # noqa: E402
+
+GOB = os.path.join(HERE, "golden", "gob")
+SCENE = os.path.join(HERE, "golden", "example", "scene.json")
+
+# encoding/gob package documentation: "type Point struct {X, Y int}" and the stream of
+# Point{22, 33}: the type definition message (-65 + wireType) and the value message
+POINT_DOC = bytes.fromhex(
+    "1f ff81 03 01 01 05 506f696e74 01 ff82 00 01 02 01 01 58 01 04 00 01 01 59 01 04 00 00 00"
+    " 07 ff82 01 2c 01 42 00")
+
+
+def gob_json(data: bytes):
+    lib = L.lib()
+    n = C.c_size_t()
+    rc = lib.mirt_gob_json(data, len(data), None, 0, C.byref(n))
+    if rc != L.MIRT_OK:
+        return rc
+    buf = C.create_string_buffer(n.value + 1)
+    L.check(lib.mirt_gob_json(data, len(data), buf, n.value + 1, C.byref(n)))
+    return json.loads(buf.value.decode())
+
+
+def msg(payload: bytes) -> bytes:
+    return G.enc_uint(len(payload)) + payload
+
+
+def read(name: str) -> bytes:
+    with open(os.path.join(GOB, name), "rb") as fh:
+        return fh.read()
+
+
+def test_doc_point_stream():
+    """The documentation's exact bytes decode to Point{22, 33}, and the encoder
+    restatement reproduces them."""
+    assert POINT_DOC[0] == 0x1F and len(POINT_DOC) == 1 + 31 + 1 + 7
+    assert gob_json(POINT_DOC) == [{"X": 22, "Y": 33}]
+    reg = G.REGISTRY.next
+    G.REGISTRY.next = 65
+    try:
+        point = G.Struct("Point", [("X", G.INT), ("Y", G.INT)])
+    finally:
+        G.REGISTRY.next = max(reg, 66)
+    assert G.Encoder().encode(point, {"X": 22, "Y": 33}).bytes() == POINT_DOC
+
+
+def test_doc_float_and_number_encodings():
+    assert G.enc_float(17.0) == bytes([0xFE, 0x31, 0x40])  # the documentation's example
+    assert gob_json(msg(G.enc_int(G.FLOAT) + b"\x00" + bytes([0xFE, 0x31, 0x40]))) == [17.0]
+    # uints: one byte below 128, else byte(-n) + n big-endian bytes
+    for x, enc in ((0, "00"), (127, "7f"), (128, "ff80"), (256, "fe0100"), (2 ** 64 - 1, "f8ffffffffffffffff")):
+        assert G.enc_uint(x) == bytes.fromhex(enc)
+        assert gob_json(msg(G.enc_int(G.UINT) + b"\x00" + bytes.fromhex(enc))) == [x]
+    # ints: x << 1, complemented (low bit set) when negative
+    for x in (0, 1, -1, 63, -64, 2 ** 40, -(2 ** 63)):
+        assert gob_json(msg(G.enc_int(G.INT) + b"\x00" + G.enc_int(x))) == [x]
+    for f in (0.0, -0.0, 1.5, -2.25e-300, 1e308, 0.1):
+        out = gob_json(msg(G.enc_int(G.FLOAT) + b"\x00" + G.enc_float(f)))[0]
+        assert out == f and np.signbit(out) == np.signbit(f)
+    assert gob_json(msg(G.enc_int(G.STRING) + b"\x00" + G.enc_str("a\"b"))) == ['a"b']
+    assert gob_json(msg(G.enc_int(G.BOOL) + b"\x00\x01")) == [True]
+
+
+def test_hand_built_streams():
+    """Omitted zero fields, nested structs, maps, slices, arrays, nil and typed interfaces."""
+    inner = G.Struct("In", [("A", G.FLOAT), ("B", G.STRING)])
+    outer = G.Struct("Out", [("I", inner), ("N", G.UINT), ("S", G.Slice(G.INT)), ("M", G.Map(G.STRING, G.INT)),
+                              ("R", G.Array(G.UINT, 2)), ("X", G.INTERFACE)])
+    v = {"I": {"A": 0.0, "B": "q"}, "N": 0, "S": [], "M": {"k": -3}, "R": [0, 7],
+         "X": G.Iface(inner, {"A": 2.5})}
+    inner.registered = "pkg.In"
+    data = G.Encoder().encode(outer, v).encode(outer, {"I": {}, "R": [1, 2]}).bytes()
+    out = gob_json(data)
+    assert out[0] == {"I": {"B": "q"}, "M": [["k", -3]], "R": [0, 7], "X": {"$type": "pkg.In", "$value": {"A": 2.5}}}
+    assert out[1] == {"I": {}, "R": [1, 2]}
+    # a top-level slice of interfaces, one nil
+    s = G.Slice(G.INTERFACE)
+    data = G.Encoder().encode(s, [None, G.Iface(inner, {"B": "z"})]).bytes()
+    assert gob_json(data) == [[None, {"$type": "pkg.In", "$value": {"B": "z"}}]]
+
+
+def test_malformed_streams_fail_cleanly():
+    diff = read("example_diff.gob")
+    for k in range(len(diff)):  # every truncation
+        assert gob_json(diff[:k]) in (L.MIRT_E_IO, []) if k == 0 else gob_json(diff[:k]) == L.MIRT_E_IO
+    rng = np.random.default_rng(5)
+    env = C.c_void_p()
+    state = read("example_state.gob")
+    L.check(L.lib().mirt_scene_from_gob(state, len(state), C.byref(env)))
+    try:
+        for _ in range(300):  # random corruption: decoded or rejected, never a crash
+            b = bytearray(diff)
+            for p in rng.integers(0, len(b), size=int(rng.integers(1, 4))):
+                b[p] = int(rng.integers(0, 256))
+            h = C.c_void_p()
+            rc = L.lib().mirt_scene_link_gob(env, bytes(b), len(b), C.byref(h))
+            assert rc in (L.MIRT_OK, L.MIRT_E_IO, L.MIRT_E_CAMERA)
+            if rc == L.MIRT_OK:
+                L.lib().mirt_scene_free(h)
+        huge = msg(G.enc_int(G.STRING) + b"\x00" + G.enc_uint(1 << 40))  # a count past the data
+        assert gob_json(huge) == L.MIRT_E_IO
+        assert gob_json(msg(G.enc_int(70) + b"\x00\x00")) == L.MIRT_E_IO  # undefined type id
+    finally:
+        L.lib().mirt_scene_free(env)
+
+
+# ------------------------------------------------------------------ the reference's state
+def u8(c: float) -> int:
+    return int(255.0 * c)
+
+
+def wire_scene(sc):
+    """What a worker holds after the wire (gob round trip): colour.RGB channels quantised
+    to uint8(255 c) and rebuilt as NewRGB (materials and lights), the camera rebuilt by
+    NewCamera(pos, forward = dir.Norm(), fov) (camera.go:156-203)."""
+    w = copy.deepcopy(sc)
+    for m in w.meshes:
+        q = m.materials.copy()
+        q[:, :9] = np.vectorize(lambda c: u8(c) / 255.0)(q[:, :9])
+        m.materials = q
+    w.lights = [(p, tuple(u8(c) / 255.0 for c in col)) for p, col in w.lights]
+    w.cam_dir = G.norm(w.cam_dir)
+    return w
+
+
+def decode_env(name: str):
+    import distributed_raytracer_amd.tracer as T
+    lib = L.lib()
+    h = C.c_void_p()
+    data = read(f"{name}_state.gob")
+    L.check(lib.mirt_scene_from_gob(data, len(data), C.byref(h)))
+    return h, T._scene_meshes(h)
+
+
+def scenes():
+    from scenes import multi_object_scene
+    sc = load_scene(SCENE)
+    return {"example": (sc, ["suzanne.obj"]),
+            "multi": (multi_object_scene(sc.meshes[0]), ["suzanne.obj", "cube.obj", "sphere.obj"])}
+
+
+@pytest.mark.parametrize("name", ["example", "multi"])
+def test_environment_meshes(name):
+    sc, models = scenes()[name]
+    h, meshes = decode_env(name)
+    try:
+        w = wire_scene(sc)
+        order = sorted(range(len(models)), key=lambda k: models[k])  # meshes come in model-path order
+        assert len(meshes) == len(models)
+        for got, k in zip(meshes, order):
+            ref = w.meshes[k]
+            assert np.array_equal(got.vertices, ref.vertices)
+            assert np.array_equal(got.normals.reshape(-1, 3), ref.normals.reshape(-1, 3))
+            assert np.array_equal(got.face_v, ref.face_v) and np.array_equal(got.face_n, ref.face_n)
+            assert np.array_equal(got.face_mat, ref.face_mat)
+            assert np.array_equal(got.materials, ref.materials)
+        cam = L.Camera()
+        assert L.lib().mirt_scene_camera(h, C.byref(cam)) == L.MIRT_E_INVALID  # none before linking
+    finally:
+        L.lib().mirt_scene_free(h)
+
+
+@pytest.mark.parametrize("name", ["example", "multi"])
+def test_mutables_link(name):
+    import distributed_raytracer_amd.tracer as T
+    sc, models = scenes()[name]
+    h, _ = decode_env(name)
+    order = sorted(range(len(models)), key=lambda k: models[k])
+    try:
+        diff = read(f"{name}_diff.gob")
+        m = C.c_void_p()
+        L.check(L.lib().mirt_scene_link_gob(h, diff, len(diff), C.byref(m)))
+        try:
+            objects, lights, cam = T._scene_mutables(m)
+        finally:
+            L.lib().mirt_scene_free(m)
+        w = wire_scene(sc)
+        want = [(order.index(mi), tuple(pos)) for mi, pos in sc.objects]
+        if name == "multi":
+            want.append((L.MIRT_NO_MESH, (0.0, 5.0, -3.0)))
+        assert objects == want
+        assert [(lt.pos, lt.col) for lt in lights] == [(tuple(p), tuple(c)) for p, c in w.lights]
+        ref = T.Camera.new(w.cam_pos, w.cam_dir, w.fov)
+        assert cam == ref
+    finally:
+        L.lib().mirt_scene_free(h)
+
+
+def test_diff_camera_parallel_to_up_is_rejected():
+    h, _ = decode_env("example")
+    try:
+        diff = G.work_order_diff([((0.0, 0.0, 0.0), 1)], [], ((0.0, 0.0, 3.0), (0.0, 1.0, 0.0), 1.0))
+        m = C.c_void_p()
+        assert L.lib().mirt_scene_link_gob(h, diff, len(diff), C.byref(m)) == L.MIRT_E_CAMERA
+    finally:
+        L.lib().mirt_scene_free(h)
+
+
+def test_light_colour_round_trip_quantisation():
+    """colour.RGB on the wire is uint8(255 c): a light of NewRGB(u8) comes back as
+    NewRGB(uint8(255 (u8 / 255))), which for some u8 is u8 - 1."""
+    h, _ = decode_env("example")
+    try:
+        lights = [((1.0, 2.0, 3.0), (u / 255.0, 0.0, 1.0)) for u in range(256)]
+        diff = G.work_order_diff([], lights, ((0.0, 0.0, 3.0), (0.0, 0.0, -1.0), 1.0))
+        m = C.c_void_p()
+        L.check(L.lib().mirt_scene_link_gob(h, diff, len(diff), C.byref(m)))
+        try:
+            got = []
+            for i in range(L.lib().mirt_scene_light_count(m)):
+                lt = L.Light()
+                L.check(L.lib().mirt_scene_light(m, i, C.byref(lt)))
+                got.append(lt.col[0])
+        finally:
+            L.lib().mirt_scene_free(m)
+        assert got == [int(255.0 * (u / 255.0)) / 255.0 for u in range(256)]
+    finally:
+        L.lib().mirt_scene_free(h)

@@ -4,8 +4,10 @@
  * HIP calls of its own, so the HIP runtime comes in through libmirt's RUNPATH.
  *
  *   Register   (worker/distributed/main.go:100-129): the scene -> mirt_create -> one
- *              mirt_mesh_upload per mesh (here mirt_scene_load stands in for the gob-decoded
- *              Environment; shared/state/mesh.go:109-213 semantics).
+ *              mirt_mesh_upload per mesh.  With --gob the scene is MasterState.state, the
+ *              gob-encoded Environment a master sends (mirt_scene_from_gob), and the frame
+ *              is a WorkOrder.diff linked to it (mirt_scene_link_gob, main.go:56-64); without
+ *              it mirt_scene_load reads scene.json (shared/state/mesh.go:109-213 semantics).
  *   BulkTrace  (worker/distributed/main.go:46-89): the master cuts the screen into one
  *              rectangle per worker (master/main.go:54-91, restated below) and each order
  *              is served concurrently — gRPC runs every BulkTrace in its own goroutine — by
@@ -16,6 +18,7 @@
  *              three frames in flight; each host frame must equal the BulkTrace frame.
  *
  *   mirt_worker <scene.json> <W> <H> <out.bin> [workers]
+ *   mirt_worker --gob <state.gob> <diff.gob> <W> <H> <out.bin> [workers]
  * Writes rgb8 (W*H*3) then valid (W*H) of the assembled frame, column-major x*H + y.
  * Exit status 0 = every check passed.
  */
@@ -78,6 +81,18 @@ typedef struct {
 } bulk_trace;
 
 /* One BulkTrace call (worker/distributed/main.go:46-89) on its own thread. */
+static int read_all(const char *path, uint8_t **data, size_t *n) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    fseek(f, 0, SEEK_END);
+    const long len = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    *data = malloc(len > 0 ? (size_t)len : 1);
+    *n = len > 0 && fread(*data, 1, (size_t)len, f) == (size_t)len ? (size_t)len : 0;
+    fclose(f);
+    return len > 0 && *n == (size_t)len ? 0 : -1;
+}
+
 static void *serve(void *p) {
     bulk_trace *b = (bulk_trace *)p;
     const size_t n = (size_t)b->order.w * b->order.h;
@@ -97,26 +112,43 @@ static void *serve(void *p) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 5) {
-        fprintf(stderr, "usage: %s scene.json W H out.bin [workers]\n", argv[0]);
+    const int gob = argc > 1 && strcmp(argv[1], "--gob") == 0;
+    char **a = argv + (gob ? 2 : 0);  /* a[1] = scene (or state.gob; a[0] = diff.gob), a[2] = W, ... */
+    const int na = argc - (gob ? 2 : 0);
+    if (na < 5) {
+        fprintf(stderr, "usage: %s scene.json W H out.bin [workers]\n"
+                        "       %s --gob state.gob diff.gob W H out.bin [workers]\n", argv[0], argv[0]);
         return 2;
     }
-    const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]);
-    uint32_t workers = argc > 5 ? (uint32_t)atoi(argv[5]) : 4;
+    const uint32_t W = (uint32_t)atoi(a[2]), H = (uint32_t)atoi(a[3]);
+    uint32_t workers = na > 5 ? (uint32_t)atoi(a[5]) : 4;
+    const char *out_path = a[4];
     if (mirt_abi_version() != MIRT_ABI_VERSION) {
         fprintf(stderr, "ABI %d, header %d\n", mirt_abi_version(), MIRT_ABI_VERSION);
         return 2;
     }
     /* Register: the scene and its meshes */
-    mirt_scene *scene = NULL;
-    if (mirt_scene_load(argv[1], &scene) != MIRT_OK) {
+    mirt_scene *scene = NULL, *linked = NULL;
+    if (gob) {
+        uint8_t *state = NULL, *diff = NULL;
+        size_t ns = 0, nd = 0;
+        if (read_all(argv[2], &state, &ns) || read_all(argv[3], &diff, &nd)) {
+            fprintf(stderr, "cannot read %s / %s\n", argv[2], argv[3]);
+            return 2;
+        }
+        if (mirt_scene_from_gob(state, ns, &scene) != MIRT_OK || mirt_scene_link_gob(scene, diff, nd, &linked) != MIRT_OK) {
+            fprintf(stderr, "gob: %s\n", mirt_scene_last_error());
+            return 2;
+        }
+        free(state);
+        free(diff);
+    } else if (mirt_scene_load(a[1], &scene) != MIRT_OK) {
         fprintf(stderr, "scene: %s\n", mirt_scene_last_error());
         return 2;
     }
     mirt_ctx *ctx = NULL;
     CHECK(mirt_create(0, &ctx));
-    const uint32_t nm = mirt_scene_mesh_count(scene), no = mirt_scene_object_count(scene),
-                   nl = mirt_scene_light_count(scene);
+    const uint32_t nm = mirt_scene_mesh_count(scene);
     uint32_t *mesh_ids = calloc(nm ? nm : 1, sizeof(uint32_t));
     for (uint32_t i = 0; i < nm; ++i) {
         mirt_mesh_view v;
@@ -124,21 +156,26 @@ int main(int argc, char **argv) {
         CHECK(mirt_mesh_upload(ctx, v.vertices, v.n_vertices, v.normals, v.n_normals, v.face_v, v.face_n, v.face_mat,
                                v.n_faces, v.materials, v.n_materials, &mesh_ids[i]));
     }
+    const mirt_scene *mut = gob ? linked : scene;
+    const uint32_t no_all = mirt_scene_object_count(mut), nl = mirt_scene_light_count(mut);
     /* WorkOrder.diff: objects (their mesh by id), lights, camera */
-    mirt_object *objs = calloc(no ? no : 1, sizeof(mirt_object));
+    mirt_object *objs = calloc(no_all ? no_all : 1, sizeof(mirt_object));
     mirt_light *lights = calloc(nl ? nl : 1, sizeof(mirt_light));
-    for (uint32_t i = 0; i < no; ++i) {
-        CHECK(mirt_scene_object(scene, i, &objs[i]));
-        objs[i].mesh_id = mesh_ids[objs[i].mesh_id];
+    uint32_t no = 0;
+    for (uint32_t i = 0; i < no_all; ++i) {
+        CHECK(mirt_scene_object(mut, i, &objs[no]));
+        if (objs[no].mesh_id == MIRT_NO_MESH) continue; /* LinkTo left its mesh nil: never hit */
+        objs[no].mesh_id = mesh_ids[objs[no].mesh_id];
+        ++no;
     }
-    for (uint32_t i = 0; i < nl; ++i) CHECK(mirt_scene_light(scene, i, &lights[i]));
+    for (uint32_t i = 0; i < nl; ++i) CHECK(mirt_scene_light(mut, i, &lights[i]));
     mirt_frame frame;
     memset(&frame, 0, sizeof(frame));
     frame.objects = objs;
     frame.n_objects = no;
     frame.lights = lights;
     frame.n_lights = nl;
-    CHECK(mirt_scene_camera(scene, &frame.camera));
+    CHECK(mirt_scene_camera(mut, &frame.camera));
 
     /* BulkTrace: the master's partition, every order on its own thread */
     rect orders[256];
@@ -197,13 +234,14 @@ int main(int argc, char **argv) {
     CHECK(mirt_group_wait(g, NULL));
     mirt_group_destroy(g);
 
-    FILE *f = fopen(argv[4], "wb");
+    FILE *f = fopen(out_path, "wb");
     if (!f || fwrite(fb_rgb8, 3, (size_t)W * H, f) != (size_t)W * H || fwrite(fb_valid, 1, (size_t)W * H, f) != (size_t)W * H) {
-        fprintf(stderr, "cannot write %s\n", argv[4]);
+        fprintf(stderr, "cannot write %s\n", out_path);
         return 2;
     }
     fclose(f);
     mirt_destroy(ctx);
+    mirt_scene_free(linked);
     mirt_scene_free(scene);
     printf("mirt_worker: %ux%u, %d BulkTrace orders on %d threads, group frames equal: %s\n", W, H, n, n,
            bad ? "NO" : "yes");
