@@ -930,13 +930,14 @@ __device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restri
     const double ns = mt[9];
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     RGB col = ka;  // tracer.go:56
+    // tracer.go:66 does not depend on the light: computed once (same value for every light)
+    const V3 camdir = lit ? norm(sub(cam, hit)) : V3{0, 0, 0};
     for (uint32_t l = 0; l < (MIRT_EXP_NO_PHONG ? 0u : fa.n_lights); ++l) {
         if (!((lit >> l) & 1u)) continue;
         const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
         const RGB lcol{fa.lcol[l][0], fa.lcol[l][1], fa.lcol[l][2]};
         const V3 ldir = norm(sub(lpos, hit));                         // tracer.go:61
         const V3 refl = sub(scale(n, 2 * dot(ldir, n)), ldir);        // tracer.go:65
-        const V3 camdir = norm(sub(cam, hit));                        // tracer.go:66
         col = c_add(col, c_mul(c_scale(kd, go_max0(dot(ldir, n))), lcol));                // :69
         col = c_add(col, c_mul(c_scale(ks, go_pow(go_max0(dot(refl, camdir)), ns)), lcol));  // :72
     }

@@ -554,16 +554,17 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     wa.nframes = nf;
     wa.per_shard = sl->per_shard;
     wa.hit_cap = (uint32_t)(((uint64_t)sl->nblocks + kQShards - 1) / kQShards * 64);
-    // persistent: two 512-thread workgroups per CU
+    // persistent: kWgPerCu workgroups per CU
     uint64_t per_wg, max_wg;
     {
         std::lock_guard<std::mutex> g(c->mu);
         per_wg = std::max<uint32_t>(c->min_blocks_per_wg, 1);
-        max_wg = c->max_workgroups ? std::min<uint64_t>(c->max_workgroups, (uint64_t)2 * c->cus) : (uint64_t)2 * c->cus;
+        max_wg = c->max_workgroups ? std::min<uint64_t>(c->max_workgroups, (uint64_t)kWgPerCu * c->cus)
+                                    : (uint64_t)kWgPerCu * c->cus;
     }
     // a frame group that knows how many launches are still running sizes this one for the
     // CUs they leave (a lone frame gets the whole chip)
-    if (max_wg_now) max_wg = std::min<uint64_t>(max_wg_now, (uint64_t)2 * c->cus);
+    if (max_wg_now) max_wg = std::min<uint64_t>(max_wg_now, (uint64_t)kWgPerCu * c->cus);
     // at least min(blocks, CUs) workgroups: a small tile list (a BulkTrace order, one
     // rank's share) keeps one block per wave rather than queueing heavy blocks on few waves
     const uint64_t want = std::max<uint64_t>((total + per_wg - 1) / per_wg, std::min<uint64_t>(total, (uint64_t)c->cus));
@@ -597,7 +598,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
 #ifdef MIRT_ITEM_TRACE
             const uint32_t cap = (uint32_t)(c->cus * (kWG / 64)) * 32;  // item records: 32 per wave (diagnostic build)
 #else
-            const uint32_t cap = (uint32_t)(2 * c->cus * (kWG / 64));
+            const uint32_t cap = (uint32_t)(kWgPerCu * c->cus * (kWG / 64));
 #endif
             HIP_TRY(hipMalloc((void**)&c->timeline, sizeof(uint64_t) * kTimelineRec * 2 * cap));
             c->timeline_cap = cap;
@@ -618,7 +619,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     sl->dirty = true;
     sl->parity ^= 1u;
     const int sgrid = (int)std::max<uint64_t>(
-        1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)2 * c->cus));
+        1, std::min<uint64_t>((pixels * std::max<uint32_t>(nl, 1) + kWG - 1) / kWG, (uint64_t)kWgPerCu * c->cus));
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (one_launch) {
         // one launch for the frames (k_trace); its time lands in the primary slot of the profile
@@ -1052,7 +1053,7 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* 
     fill_args(c, f, 1, 1, fa, tris);
     HIP_TRY(hipMemcpyAsync((void*)io.orig, orig, (size_t)n * 24, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync((void*)io.dir, dir, (size_t)n * 24, hipMemcpyHostToDevice, s));
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n + kWG - 1) / kWG, 2 * (uint64_t)c->cus));
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n + kWG - 1) / kWG, kWgPerCu * (uint64_t)c->cus));
     HIP_TRY(launch_rays(fa, io, grid, c->flags, s));
     HIP_TRY(hipMemcpyAsync(ok, io.ok, n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(hit, io.hit, (size_t)n * 24, hipMemcpyDeviceToHost, s));
@@ -2195,7 +2196,7 @@ static int group_flush(mirt_group* g) {
         uint32_t running = 0;
         for (uint64_t b = g->nb > g->FB ? g->nb - g->FB + 1 : 0; b < g->nb; ++b)
             if (hipEventQuery(g->ev_done[b % g->FB]) == hipErrorNotReady) ++running;
-        max_wg_now = std::max<uint32_t>(1, (uint32_t)(4 * (uint64_t)c->cus / (running + 1)));
+        max_wg_now = std::max<uint32_t>(1, (uint32_t)(2 * kWgPerCu * (uint64_t)c->cus / (running + 1)));
     }
     // Blocks outside a frame's hit rectangle (every ray misses) are not traced: a share's
     // packed plane is only read inside the rectangle (k_pack_rect), and the whole-screen
