@@ -251,8 +251,11 @@ def main():
     d2h = not a.no_d2h and sharder == "native"
 
     def native_group(host_output: bool):
+        # N > 1: every host wait of the group is deadline-bounded, so a rank whose transfers never
+        # arrive fails the run (MIRT_E_TIMEOUT / MIRT_E_PEER naming it) instead of hanging it
         return NativeFrameGroup(ctx, W, H, rank, world, a.tile if world > 1 else None, inflight=a.inflight,
-                                tile_h=a.tile_h, batch=a.batch, host_output=host_output and rank == 0)
+                                tile_h=a.tile_h, batch=a.batch, host_output=host_output and rank == 0,
+                                timeout_ms=int(os.environ.get("MIRT_GROUP_TIMEOUT_MS", "60000")) if world > 1 else 0)
 
     sh = None
     err = ""
@@ -276,6 +279,13 @@ def main():
     if a.grid:
         ctx.set_grid(*(int(x) for x in a.grid.split(",")))
 
+    def finish():
+        """The enqueued frames are done (gathers, unpacks and D2H included): at N > 1 a host
+        wait within the group's deadline first, then torch's stream waits for them."""
+        if world > 1 and isinstance(sh, NativeFrameGroup):
+            sh.wait()
+        sh.flush()
+
     # launches per region (the key that partitions the rocprofv3 kernel trace of this command)
     launches = {}
 
@@ -288,7 +298,7 @@ def main():
     with torch.cuda.stream(stream):
         for _ in range(a.warmup):
             sh.render(frame)
-        sh.flush()
+        finish()
         count("warmup", a.warmup)
         torch.cuda.synchronize(dev)
 
@@ -299,7 +309,7 @@ def main():
         last = None
         for _ in range(a.steps):
             last = sh.render(frame)  # N > 1: frame k's gather overlaps frame k+1's tracing
-        sh.flush()                   # the last frame's gather + unpack (+ D2H) are inside the timed region
+        finish()                     # the last frame's gather + unpack (+ D2H) are inside the timed region
         torch.cuda.synchronize(dev)
         barrier()
         t1 = time.perf_counter()
@@ -317,7 +327,7 @@ def main():
             d0 = time.perf_counter()
             for _ in range(a.steps):
                 sh.render(frame)
-            sh.flush()
+            finish()
             torch.cuda.synchronize(dev)
             barrier()
             dev_elapsed = time.perf_counter() - d0
@@ -329,7 +339,7 @@ def main():
         ctx.profile_enable(True)
         for _ in range(a.steps):
             sh.render(frame)
-        sh.flush()
+        finish()
         torch.cuda.synchronize(dev)
         ctx.profile_enable(False)
         count("profiled", a.steps)
@@ -341,7 +351,7 @@ def main():
             torch.cuda.synchronize(dev)
             l0 = time.perf_counter()
             sh.render(frame)
-            sh.flush()
+            finish()
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - l0)
         count("latency", min(a.steps, 20), batched=False)

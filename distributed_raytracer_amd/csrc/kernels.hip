@@ -88,6 +88,9 @@ __device__ __forceinline__ bool t_certainly_negative(double n, double d) {
     return n * __builtin_copysign(0x1p1000, d) < -__builtin_fabs(d);
 }
 
+#ifndef MIRT_TFIRST
+#define MIRT_TFIRST 0
+#endif
 // Möller–Trumbore exactly as triangle.go:37-77, on (p1or = O - P1, E1, E2), returning
 // only the hit decision and the ray parameter.  neg = D * -1 (triangle.go:38).
 //   DG: diagnostic counter base (MIRT_DIAG builds).
@@ -101,10 +104,15 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
     V3 c = cross(e2, neg);
     double inc = dot(e1, c);
     if (inc != 0.0) {
+        double nt = 0.0;
+        if (MIRT_TFIRST && PREFILTER && TPRE) {  // the t pre-reject first (experiment)
+            nt = dot(e1, cross(e2, p1or));
+            if (t_certainly_negative(nt, inc)) return false;
+        }
         double n2 = dot(p1or, c);
         if (PREFILTER && r2_certainly_out(n2, inc)) return false;
-        double nt = 0.0;
-        if (PREFILTER && TPRE) {
+        if (!MIRT_TFIRST && PREFILTER && TPRE) {
+            diag(DG + 7);
             nt = dot(e1, cross(e2, p1or));
             if (t_certainly_negative(nt, inc)) return false;
         }
