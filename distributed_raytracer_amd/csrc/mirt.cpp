@@ -1480,6 +1480,9 @@ struct mirt_group {
     uint32_t bbounces = 0;
     std::vector<BatchRec> binfo;        // per batch slot
     std::vector<uint64_t> slot_frame;   // per frame slot: the frame it holds (~0: none)
+    // per frame slot: columns [dirty0, dirty1) may hold non-miss pixels (whole-screen planes);
+    // a narrow frame refills only those before it traces its hit rectangle
+    std::vector<uint32_t> dirty0, dirty1;
     std::vector<uint64_t> slot_bad;     // per frame slot: deal indices whose transfer failed
     // fault handling (master/pool/pool.go:224-260, master/main.go:111-161)
     uint32_t timeout_ms = 0;
@@ -1973,6 +1976,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->binfo.assign(inflight, BatchRec());
     g->slot_frame.assign(inflight, ~0ull);
     g->slot_bad.assign(inflight, 0);
+    g->dirty0.assign(inflight, 0);  // the planes' first contents are unknown: the whole screen
+    g->dirty1.assign(inflight, W);
     if (is_root && fbs) {
         for (uint32_t j = 0; j < inflight; ++j)
             g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
@@ -2210,16 +2215,34 @@ static int group_flush(mirt_group* g) {
             const uint32_t* R = br.rect[i];
             narrow[i] = !(R[0] == 0 && R[1] == 0 && R[2] == g->W && R[3] == g->H) && !g->bbounces &&
                         !(c->flags & MIRT_OPT_SPLIT_KERNELS);
-            if (!narrow[i] || g->tiled) continue;
-            const OutPlanes& o = g->fb[g->bj[i]];
-            const struct { void* p; uint64_t b; uint8_t v; } planes[kFillPlanes] = {
-                {o.rgb, npx * 24, 0}, {o.rgb8, npx * 3, 0}, {o.valid, npx, 0},
-                {o.face, npx * 4, 0xff}, {o.object, npx * 4, 0xff}, {o.rgbv, npx * 4, 0}};
+            const uint32_t j = g->bj[i];
+            if (g->tiled) continue;
+            if (!narrow[i]) {  // traced whole: every pixel is written
+                g->dirty0[j] = 0;
+                g->dirty1[j] = g->W;
+                continue;
+            }
+            // Only columns an earlier frame of this slot may have hit can hold anything but miss
+            // values (the trace writes every pixel of the blocks meeting this frame's rectangle,
+            // and hit pixels lie inside it): refill those columns, whole 16-byte words (extra
+            // bytes of neighbouring columns get the miss value they already hold).
+            const uint32_t d0 = g->dirty0[j], d1 = g->dirty1[j];
+            g->dirty0[j] = R[0];
+            g->dirty1[j] = R[2];
+            if (d1 <= d0) continue;
+            const OutPlanes& o = g->fb[j];
+            const struct { void* p; uint64_t e; uint8_t v; } planes[kFillPlanes] = {
+                {o.rgb, 24, 0}, {o.rgb8, 3, 0}, {o.valid, 1, 0}, {o.face, 4, 0xff}, {o.object, 4, 0xff}, {o.rgbv, 4, 0}};
             for (int k = 0; k < kFillPlanes; ++k) {
-                fj.ptr[i][k] = (uint8_t*)planes[k].p;
-                fj.bytes[i][k] = planes[k].p ? planes[k].b : 0;
+                fj.ptr[i][k] = nullptr;
+                fj.bytes[i][k] = 0;
                 fj.value[i][k] = planes[k].v;
-                if (planes[k].p) fill_max = std::max(fill_max, planes[k].b);
+                if (!planes[k].p) continue;
+                const uint64_t b0 = (uint64_t)d0 * g->H * planes[k].e & ~15ull;
+                const uint64_t b1 = std::min<uint64_t>(npx * planes[k].e, ((uint64_t)d1 * g->H * planes[k].e + 15) & ~15ull);
+                fj.ptr[i][k] = (uint8_t*)planes[k].p + b0;
+                fj.bytes[i][k] = b1 - b0;
+                fill_max = std::max(fill_max, b1 - b0);
             }
         }
         if (fill_max) HIP_TRY(launch_fill_planes(fj, n, fill_max, s));

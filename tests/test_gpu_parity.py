@@ -528,6 +528,41 @@ def test_native_frame_group_matches_draw(ctx, env, tile, tile_h, inflight, batch
         ctx.set_grid()
 
 
+@pytest.mark.parametrize("inflight", [1, 2, 3])
+def test_frame_slots_refill_only_stale_columns(ctx, env, inflight):
+    """Whole-screen framebuffers are refilled only in the columns an earlier frame of the
+    same slot may have hit: every frame, checked as soon as it is done, equals its frame
+    drawn alone, whatever the slot held before (a wide hit rectangle, then narrow ones, an
+    empty one, the whole screen)."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W, H = 200, 150
+    base = env.mutable()
+    c = base.cam
+    c0 = np.array([1.0, 1.0, -1.0])
+    cams = [rt.Camera.new(tuple(c0 + [0.0, 0.0, 0.1]), (0.0, 0.0, -1.0), 1.2),   # inside the box: wide
+            c,                                                                  # default
+            rt.Camera.new(c.pos, tuple(-np.asarray(c.forward)), c.fov),         # turned away: empty
+            rt.Camera.new(tuple(c0 + [3.0, 0.5, 3.0]), (-0.2, -0.1, -1.0), 0.9),  # cut by the left edge
+            rt.Camera.new(tuple(np.asarray(c.pos) + [-1.5, 0.0, 0.0]), c.forward, c.fov)]  # shifted
+    muts = [rt.EnvMutables(base.objects, base.lights, cm) for cm in cams]
+    frames = [m.to_frame() for m in muts]
+    refs = [rt.draw(env, W, H, m) for m in muts]
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=inflight)
+    try:
+        for k, q in enumerate([0, 1, 2, 3, 0, 4, 1, 3, 2, 0, 1, 4, 4, 3]):
+            g.render(frames[q])
+            g.flush()
+            torch.cuda.synchronize()
+            got = g.frame
+            assert np.array_equal(got.valid.cpu().numpy(), refs[q].valid), f"frame {k} valid differs"
+            assert np.array_equal(got.rgb8.cpu().numpy(), refs[q].rgb8), f"frame {k} rgb8 differs"
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
 def test_group_batch_arguments(ctx):
     """mirt_group_set_batch: 1..min(8, inflight) frames per launch, before the first frame."""
     import distributed_raytracer_amd as rt
