@@ -577,6 +577,10 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
     } while (stk.sp != 0);
 }
 
+// The LDS-resident mesh (RESIDENT kernels): dynamic shared memory sized to the mesh at
+// launch, 72 B per face, after the kernel's static LDS (the launch passes 0 bytes otherwise).
+extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
+
 // Occupancy target of the tracing kernels (waves per SIMD) and LDS-resident meshes.
 #ifndef MIRT_WAVES_PER_EU
 #define MIRT_WAVES_PER_EU 4
@@ -1345,7 +1349,7 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
 // persistent workgroup, relative to the camera (p1or), and every sweep reads LDS.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ uint32_t wstk[kWG / 64][MIRT_PRIMARY_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
     __shared__ float4 frect[8];  // frustum rectangles
@@ -1425,7 +1429,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
 // (light, chunk) of region q.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
     // segment query for one-object frames (BVH kernels only; brute force stays literal)
@@ -1481,7 +1485,7 @@ __device__ __forceinline__ const FrameRec& frame_rec(const WorkArgs& wa, uint32_
 
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ uint32_t wstk[kWG / 64][(MIRT_PRIMARY_WIDE || MIRT_SHADOW_WIDE) ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
     __shared__ float4 frect[kMaxFrames][8];
@@ -1646,7 +1650,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
 // Level 0's phong comes from the shadow kernel (WorkArgs::ph0).
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ cnt_t red[kWG / 64][4];
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     if (RESIDENT) {
@@ -1760,7 +1764,7 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
 // ---------------------------------------------------------------- arbitrary rays
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
-    __shared__ __attribute__((aligned(16))) double lds[RESIDENT ? kLdsTris * kTriD : 1];
+    double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
@@ -1894,11 +1898,14 @@ static bool is_resident(const FrameArgs& fa) {
     return MIRT_LDS_MESH && fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris &&
            fa.obj[0].m.depth <= (uint32_t)kBvhShallowDepth;
 }
+// dynamic LDS bytes of a RESIDENT launch: the mesh
+static size_t mesh_lds_bytes(const FrameArgs& fa) { return (size_t)fa.obj[0].m.ntri * kTriD * sizeof(double); }
 
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_PRIM(P, B, R) hipLaunchKernelGGL((k_primary<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_PRIM(P, B, R) hipLaunchKernelGGL((k_primary<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_PRIM);
 #undef K_PRIM
     return hipGetLastError();
@@ -1907,7 +1914,8 @@ hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                          hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_SHADOW(P, B, R) hipLaunchKernelGGL((k_shadow<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_SHADOW(P, B, R) hipLaunchKernelGGL((k_shadow<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_SHADOW);
 #undef K_SHADOW
     return hipGetLastError();
@@ -1915,7 +1923,8 @@ hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlane
 
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_RAYS(P, B, R) hipLaunchKernelGGL((k_rays<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, io)
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_RAYS(P, B, R) hipLaunchKernelGGL((k_rays<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, io)
     MIRT_DISPATCH(K_RAYS);
 #undef K_RAYS
     return hipGetLastError();
@@ -1924,7 +1933,8 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_REFLECT(P, B, R) hipLaunchKernelGGL((k_reflect<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_REFLECT(P, B, R) hipLaunchKernelGGL((k_reflect<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_REFLECT);
 #undef K_REFLECT
     return hipGetLastError();
@@ -1933,7 +1943,8 @@ hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
 hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                         hipStream_t s) {
     const bool resident = is_resident(fa);
-#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), 0, s, fa, wa, out)
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE
     return hipGetLastError();
