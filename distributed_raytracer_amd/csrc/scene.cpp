@@ -10,7 +10,7 @@
 //       Ka=16/255, Kd=1, Ks=0, Ns=0 when the group's material is unknown.
 //   shared/state/util.go:11-13 relativePath.
 // gwob semantics assumed (github.com/mwindels/gwob is unpinned and not vendored):
-// polygons are fan-triangulated (v0, vi, vi+1); numbers parse as float32 via float64.
+// polygons are fan-triangulated (v0, vi, vi+1); numbers parse as float32 (ParseFloat(s, 32)).
 // Go's encoding/json matches keys to struct fields case-insensitively.
 #include <ctype.h>
 #include <strings.h>
@@ -200,11 +200,14 @@ std::string relative_path(const std::string& original, const std::string& other)
     return original.substr(0, i) + other.substr(j);
 }
 
+// gwob: strconv.ParseFloat(s, 32), the decimal rounded once, correctly, to float32 (glibc's
+// strtof rounds correctly; (float)strtod would round twice and differ near float32
+// halfway points), widened to fp64.
 double f32(const std::string& s, bool& ok) {
     char* e = nullptr;
-    double d = strtod(s.c_str(), &e);
+    const float f = strtof(s.c_str(), &e);
     ok = e && !*e && !s.empty();
-    return (double)(float)d;
+    return (double)f;
 }
 double clamp01(double v) {  // colour.go:33-35 Max(0, Min(v, 1)) (NaN propagates)
     if (v != v) return v;

@@ -13,7 +13,7 @@ Follows (reference paths):
   shared/state/util.go:11-13           relativePath
   shared/colour/colour.go:28-35        NewRGB / NewRGBFromFloats (clamp of float64(f32))
 Third-party semantics assumed (github.com/mwindels/gwob, unpinned, not vendored):
-  coordinates parsed as float32; polygon faces fan-triangulated (v0, vi, vi+1);
+  coordinates parsed as float32 by strconv.ParseFloat(s, 32) (one correct rounding); polygon faces fan-triangulated (v0, vi, vi+1);
   material per face = the last `usemtl` before it; MTL Ka/Kd/Ks/Ns parsed as float32.
 Go's encoding/json matches object keys to struct fields case-insensitively.
 """
@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import math
 import os
+from fractions import Fraction
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -30,7 +31,25 @@ DEFAULT_MATERIAL = (16 / 255, 16 / 255, 16 / 255, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 
 
 
 def _f32(s: str) -> float:
-    return float(np.float32(float(s)))
+    """The decimal string rounded ONCE, correctly, to float32 (Go's strconv.ParseFloat(s, 32),
+    which gwob uses), widened to float64.  float32(float64(s)) rounds twice and differs when
+    the decimal lies within half a float64 ulp of a float32 halfway point; those rare cases
+    are decided exactly."""
+    f = float(s)
+    r = np.float32(f)
+    if float(r) == f or not math.isfinite(f):
+        return float(r)
+    nb = np.nextafter(r, np.float32(np.inf) if f > float(r) else np.float32(-np.inf))
+    mid = (float(r) + float(nb)) / 2  # exact in float64
+    if abs(f - mid) > math.ulp(f):
+        return float(r)  # the exact value is on f's side of the halfway point
+    q = Fraction(s.strip())
+    best = None
+    for c in (np.nextafter(r, np.float32(-np.inf)), r, np.nextafter(r, np.float32(np.inf))):
+        d = abs(Fraction(float(c)) - q)
+        if best is None or d < best[0] or (d == best[0] and int(np.float32(c).view(np.uint32)) & 1 == 0):
+            best = (d, c)
+    return float(best[1])
 
 
 def _clamp01(v: float) -> float:

@@ -109,6 +109,35 @@ def test_loaders_agree_on_obj_variants(tmp_path):
     assert lights[0].col == (1.0, 128 / 255, 0.0)
 
 
+# decimal strings within half a float64 ulp of a float32 halfway point: rounding them to
+# float64 first and then to float32 gives the neighbouring float32 (found by exact search)
+NEAR_HALFWAY = {"-1.462542951107025136484375": -1.4625428915023804, "1.389735043048858652578125": 1.3897351026535034}
+
+
+def test_float32_parse_rounds_once(tmp_path):
+    """gwob parses with strconv.ParseFloat(s, 32): one correct rounding to float32.  Both
+    loaders must agree with the exact rounding where float32(float64(s)) does not."""
+    import distributed_raytracer_amd as rt
+    from fractions import Fraction
+    from oracle.scene_py import _f32, load_scene
+    for s, want in NEAR_HALFWAY.items():
+        assert float(np.float32(float(s))) != want  # the double-rounded value is the other float32
+        assert _f32(s) == want
+        lo = np.nextafter(np.float32(want), np.float32(-np.inf))
+        hi = np.nextafter(np.float32(want), np.float32(np.inf))
+        d = abs(Fraction(want) - Fraction(s))
+        assert d <= abs(Fraction(float(lo)) - Fraction(s)) and d <= abs(Fraction(float(hi)) - Fraction(s))
+    a, b = list(NEAR_HALFWAY)
+    (tmp_path / "h.obj").write_text(f"v {a} {b} 0.5\nv 1 0 {b}\nv {b} 1 {a}\nf 1 2 3\n")
+    (tmp_path / "s.json").write_text('{"objs":[{"model":"h.obj","pos":{"x":0,"y":0,"z":0}}],"lights":[],'
+                                     '"cam":{"pos":{"x":0,"y":0,"z":2},"dir":{"x":0,"y":0,"z":-1},"fov":1.0}}')
+    meshes, _, _, _ = rt.load_scene_arrays(str(tmp_path / "s.json"))
+    py = load_scene(str(tmp_path / "s.json")).meshes[0]
+    want = np.array([[NEAR_HALFWAY[a], NEAR_HALFWAY[b], 0.5], [1, 0, NEAR_HALFWAY[b]],
+                     [NEAR_HALFWAY[b], 1, NEAR_HALFWAY[a]]])
+    assert np.array_equal(meshes[0].vertices, want) and np.array_equal(py.vertices, want)
+
+
 def test_camera_and_go_math_match_oracle():
     import distributed_raytracer_amd as rt
     import distributed_raytracer_amd._lib as L
