@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
     ap.add_argument("--no-octant", action="store_true", help="ablation: generic (sorted) child-box test only")
+    ap.add_argument("--views", action="store_true",
+                    help="experiment: per-frame view tables instead of the BVH walk (DESIGN.md §4.8)")
     ap.add_argument("--split-kernels", action="store_true",
                     help="variant: k_primary then k_shadow (default: one k_trace launch per frame)")
     ap.add_argument("--static-schedule", action="store_true",
@@ -230,7 +232,8 @@ def main():
     ctx = rt.Context(local)
     opts = (rt._lib.MIRT_OPT_NO_OCTANT if a.no_octant else 0) | (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
-        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0)
+        rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
+        rt._lib.MIRT_OPT_VIEWS if a.views else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses

@@ -33,6 +33,7 @@ MIRT_OPT_NO_SEGMENT = 16
 MIRT_OPT_SPLIT_KERNELS = 32
 MIRT_OPT_NO_FRUSTUM = 64
 MIRT_OPT_NO_OCTANT = 128
+MIRT_OPT_VIEWS = 256
 
 D3 = C.c_double * 3
 

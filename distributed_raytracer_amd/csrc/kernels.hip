@@ -72,6 +72,9 @@ __device__ __forceinline__ bool r2_certainly_out(double n, double d) {
 #ifndef MIRT_EXP_NO_TRI_TESTS  // measurement builds only: leaves are entered but never tested
 #define MIRT_EXP_NO_TRI_TESTS 0
 #endif
+#ifndef MIRT_EXP_NO_SHADOW_TESTS  // measurement builds only: shadow leaves entered, never tested (all lit)
+#define MIRT_EXP_NO_SHADOW_TESTS 0
+#endif
 constexpr int kDiagN = 32;
 __device__ unsigned long long g_diag[8 * kDiagN];
 __device__ __forceinline__ void diag(int k) {
@@ -237,7 +240,7 @@ template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, typename SrcP
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
-    if (MIRT_EXP_NO_TRI_TESTS) return;
+    if (MIRT_EXP_NO_TRI_TESTS || (MIRT_EXP_NO_SHADOW_TESTS && TPRE)) return;
 #pragma unroll 2
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t k = pos0 + i;
@@ -777,6 +780,78 @@ __device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t*
     }
 }
 
+// Packet walk of a view table (ViewLeaf) instead of the BVH, for rays that all pass through
+// the view point.  Lane state: its direction (ls, lt) in the view's (s, t) plane, or unb
+// (every direction), and its depth bound zl (a leaf farther from the view point than zl
+// cannot hold a candidate of the lane).  (cs0, cs1) x (ct0, ct1) bounds the live lanes'
+// directions (wave-uniform).  A leaf is tested when some live lane's direction lies in its
+// rectangle within its depth bound; leaves come nearest first, so the walk ends at the first
+// leaf beyond every live lane's bound.
+//   !SEG (primary rays, view = the camera): zl is bvh_sweep's nearest-query bound, tightened
+//   as the lane finds candidates.  SEG (shadow segments, view = the light): zl is fixed,
+//   lanes retire as in bvh_sweep.
+template <bool PREFILTER, bool SEG, typename SrcPtr>
+__device__ __forceinline__ void view_sweep(const DevMesh& m, SrcPtr src, const ViewLeaf* __restrict__ vt, uint32_t n,
+                                           float ls, float lt, bool unb, float cs0, float cs1, float ct0, float ct1,
+                                           float zl, V3 ro, V3 d, V3 neg, bool lane_on, Best& b, Visits& vis,
+                                           double resolve = 0.0, float tseg = 0.0f) {
+    const uint32_t lane = threadIdx.x & 63;
+    bool live = lane_on;
+    // the lane's own ray against a candidate leaf's box, as bvh_sweep's slab test (primary:
+    // bounded by the nearest-query bound zl; segments: by tseg)
+    const Ray32 r32 = ray32(ro, d);
+    const double Mbase =
+        0x1p-36 * (1.0 + fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z)));
+    bool done = false;
+    for (uint32_t p0 = 0; p0 < n && !done; p0 += 64) {
+        const uint32_t j = p0 + lane;
+        float4 a = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+        float dm = __builtin_inff();
+        uint32_t ref = 0, lix = 0;
+        if (j < n) {
+            const float4* q = (const float4*)(vt + j);
+            a = q[0];
+            const float4 c = q[1];
+            dm = c.x;
+            ref = __float_as_uint(c.y);
+            lix = __float_as_uint(c.z);
+        }
+        ++vis.nodes;
+        uint64_t cand = __ballot(j < n && a.x <= cs1 && a.y >= cs0 && a.z <= ct1 && a.w >= ct0);
+        while (cand) {
+            const uint32_t bit = (uint32_t)__builtin_ctzll(cand);
+            cand &= cand - 1;
+            const float dmin = u_lane(dm, bit);
+            if (__ballot(live && dmin <= zl) == 0) {  // this leaf and every later one: beyond all lanes
+                done = true;
+                break;
+            }
+            const float s0 = u_lane(a.x, bit), s1 = u_lane(a.y, bit), t0 = u_lane(a.z, bit), t1 = u_lane(a.w, bit);
+            if (__ballot(live && dmin <= zl && (unb || (ls >= s0 && ls <= s1 && lt >= t0 && lt <= t1))) == 0) continue;
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)ref, (int)bit);
+            const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)lix, (int)bit);
+            const LeafBox* lb = m.leaves + li;
+            if (__ballot(live && lane_box<true>(r32, lb->lo[0], lb->lo[1], lb->lo[2], lb->hi[0], lb->hi[1], lb->hi[2],
+                                                SEG ? tseg : zl)) == 0)
+                continue;
+            const uint32_t first = r & kBvhFirstMask, cnt = (r & ~kBvhLeafBit) >> kBvhCountShift;
+            ++vis.leaves;
+            diag(SEG ? 14 : 6);
+            test_range<false, PREFILTER, SEG ? 8 : 0, SEG>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
+                                                        vis.tests);
+            if (SEG) {
+                live = live && !(b.has && b.d < resolve);
+                if (__ballot(live) == 0) {
+                    done = true;
+                    break;
+                }
+            } else if (b.has) {
+                zl = fminf(zl, (float)(b.d + (Mbase + 0x1p-36 * b.d)) * (1.0f + 0x1p-20f));
+            }
+        }
+    }
+}
+
 struct Nearest {
     bool ok;
     uint32_t obj, face, mat;
@@ -811,9 +886,13 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   RESIDENT: object 0's mesh sits in LDS (`lds`), relative (p1or) when REL.
 //   BRUTE:    sweep every triangle instead of walking the BVH.
 //   COMMON:   every lane's ray starts at o (primary rays): wide cone traversal.
+//   vt (one-object frames, LDS-resident, !REL): the camera's view table; (ls, lt) the lane's
+//   direction and crect the block's range of directions (view_sweep).
 template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
 __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal, Visits& vis, uint32_t* __restrict__ stk = nullptr) {
+                                 bool lane_on, bool want_normal, Visits& vis, uint32_t* __restrict__ stk = nullptr,
+                                 const ViewLeaf* vt = nullptr, uint32_t vn = 0, float ls = 0.0f, float lt = 0.0f,
+                                 float4 crect = float4{0.0f, 0.0f, 0.0f, 0.0f}) {
     Nearest best;
     best.ok = false;
     best.obj = best.face = best.mat = 0;
@@ -842,6 +921,9 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
             else
                 bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
                                                   vis.overflow);
+        } else if (resident && !REL && vt) {
+            view_sweep<PREFILTER, false>(ob.m, lds, vt, vn, ls, lt, false, crect.x, crect.y, crect.z, crect.w,
+                                         __builtin_inff(), ro, d, neg, lane_on, b, vis);
         } else if (resident) {
             bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
                                              !(fa.flags & MIRT_OPT_NO_OCTANT));
@@ -878,10 +960,12 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
 //   every candidate beyond lh + 1e-4 + M  =>  lit, so boxes entered beyond that are culled;
 // otherwise the nearest candidate found is the true nearest and the reference comparison
 // runs unchanged.  M bounds every fp64 rounding involved with a wide margin.
+//   vt / vh (LDS-resident): the light's view table and header (view_sweep from the light).
 template <bool PREFILTER>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
                                                   uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, bool lane_on,
-                                                  Visits& vis) {
+                                                  Visits& vis, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                                  const ViewHead* vh = nullptr) {
     const DevObject& ob = fa.obj[0];
     const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
     const V3 ro = sub(o, pos);  // object.go:71
@@ -911,6 +995,35 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         else
             bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
                                              vis.overflow, tmax, resolve);
+    } else if (resident && vt) {
+        // the lane's direction from the light: its hit point relative to the view point (every
+        // point of the segment short of the light lies in that direction)
+        const double* R0 = vh->R[0];
+        const double* R1 = vh->R[1];
+        const double* R2 = vh->R[2];
+        const V3 X = sub(sub(hit, pos), V3{vh->O[0], vh->O[1], vh->O[2]});
+        const double z = R0[0] * X.x + R0[1] * X.y + R0[2] * X.z;
+        const double mag = fmax(fmax(__builtin_fabs(X.x), __builtin_fabs(X.y)), __builtin_fabs(X.z));
+        const bool unb = !(z > 0x1p-20 * mag);
+        float ls = 0.0f, lt = 0.0f;
+        if (!unb) {
+            ls = (float)((R1[0] * X.x + R1[1] * X.y + R1[2] * X.z) / z);
+            lt = (float)((R2[0] * X.x + R2[1] * X.y + R2[2] * X.z) / z);
+        }
+        const bool any_unb = __ballot(lane_on && unb) != 0;
+        const float inf = __builtin_inff();
+        float cs0 = -inf, cs1 = inf, ct0 = -inf, ct1 = inf;
+        if (!any_unb) {
+            const bool on = lane_on;
+            cs0 = wave_reduce<true>(on ? ls : inf);
+            cs1 = wave_reduce<false>(on ? ls : -inf);
+            ct0 = wave_reduce<true>(on ? lt : inf);
+            ct1 = wave_reduce<false>(on ? lt : -inf);
+        }
+        // a candidate of the segment lies within |L - hit| of the light (or within near_r)
+        const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
+        view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b, vis,
+                                    resolve, tmax);
     } else if (resident) {
         bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
                                           !(fa.flags & MIRT_OPT_NO_OCTANT));
@@ -1157,7 +1270,9 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
                                               bool frustum = false, const float4* __restrict__ frect = nullptr,
-                                              const LocalChunks* lc = nullptr, uint32_t classified = 0) {
+                                              const LocalChunks* lc = nullptr, uint32_t classified = 0,
+                                              const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                              const FrustumArgs* vfr = nullptr) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1201,9 +1316,20 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     V3 d = norm(sub(p, cam));
 
     Visits vis{0, 0, 0, 0};
+    // view table walk: the lane's direction (s_i, t_j) and the block's range (block_frustum's)
+    float ls = 0.0f, lt = 0.0f;
+    float4 crect{0.0f, 0.0f, 0.0f, 0.0f};
+    if (vt) {
+        ls = (float)(vfr->sB - vfr->sA * (double)i);
+        lt = (float)(vfr->tB - vfr->tA * (double)j);
+        const float s0 = (float)(vfr->sB - vfr->sA * (double)px), s1 = (float)(vfr->sB - vfr->sA * (double)(px + vw - 1));
+        const float t0 = (float)(vfr->tB - vfr->tA * (double)py), t1 = (float)(vfr->tB - vfr->tA * (double)(py + vh - 1));
+        crect = float4{fminf(s0, s1), fmaxf(s0, s1), fminf(t0, t1), fmaxf(t0, t1)};
+    }
     pc.lap(0);
     Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d,
-                                                                         active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis, stk);
+                                                                         active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis, stk,
+                                                                         vt, vn, ls, lt, crect);
     pc.lap(1);
     ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
     ws.nodes += vis.nodes;
@@ -1273,10 +1399,11 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
 // the wave that finishes the chunk's last light.  n_lights == 0: one pass that shades.
+//   vf: the chunk's frame within the launch (its view tables, k_trace), ~0u: none.
 template <bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
-                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws) {
+                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
@@ -1298,7 +1425,17 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     } else if (MIRT_EXP_NO_SHADOW_TRACE) {
         is_lit = true;
     } else if (segment) {
-        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis);
+        const ViewLeaf* vt = nullptr;
+        const ViewHead* vh = nullptr;
+        if (vf != ~0u && wa.views) {
+            const uint32_t q = vf * wa.nviews + 1 + l;
+            if (((const __attribute__((address_space(4))) ViewHead*)wa.view_heads)[q].ok) {
+                vh = wa.view_heads + q;
+                vt = wa.views + (size_t)q * wa.view_leaves;
+            }
+        }
+        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis, vt, wa.view_leaves,
+                                              vh);
     } else {
         Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis);
         // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
@@ -1581,9 +1718,10 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 diag(19);
                 ic.start();
                 const WaveStats before = wsh;
-                const FrameRec& fr = frame_rec(wa, __builtin_amdgcn_readfirstlane(chunk_frame[c]));
+                const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
+                const FrameRec& fr = frame_rec(wa, cf);
                 shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
-                                              wsh);
+                                              wsh, RESIDENT ? cf : ~0u);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -1604,9 +1742,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                     const uint32_t f = __builtin_amdgcn_readfirstlane(bq_frame[t]);
                     const FrameRec& fr = frame_rec(wa, f);
                     lc.frame = f;
+                    // the camera's view table of this frame (ViewHead::ok: built)
+                    const ViewLeaf* vt = nullptr;
+                    if (RESIDENT && wa.views && fr.fr.on &&
+                        ((const __attribute__((address_space(4))) ViewHead*)wa.view_heads)[f * wa.nviews].ok)
+                        vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
                                                            use_frustum, frect[f], &lc,
-                                                           __builtin_amdgcn_readfirstlane(bq_cull[t]));
+                                                           __builtin_amdgcn_readfirstlane(bq_cull[t]), vt, wa.view_leaves,
+                                                           &fr.fr);
                     ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
                               (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
                     lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated
@@ -2197,13 +2341,208 @@ hipError_t launch_fill_planes(const FillJobs& jobs, uint32_t nframes, uint64_t m
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                      uint32_t n16) {
-    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+// ---------------------------------------------------------------- view tables (ViewLeaf)
+// the float next to finite f towards -inf / +inf
+__device__ __forceinline__ float f32_prev(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return f == 0.0f ? -0x1p-149f : __uint_as_float((int32_t)b > 0 ? b - 1u : b + 1u);
 }
-hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s) {
+__device__ __forceinline__ float f32_next(float f) { return -f32_prev(-f); }
+// x rounded to float downwards / upwards (NaN stays NaN)
+__device__ __forceinline__ float f32_down(double x) {
+    const float f = (float)x;
+    return ((double)f > x && __builtin_isfinite(f)) ? f32_prev(f) : ((double)f > x ? 0x1.fffffep127f : f);
+}
+__device__ __forceinline__ float f32_up(double x) {
+    const float f = (float)x;
+    return ((double)f < x && __builtin_isfinite(f)) ? f32_next(f) : ((double)f < x ? -0x1.fffffep127f : f);
+}
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+// R = [F L U]^-1 by cofactors (row k: column k+1 x column k+2, / det), as the host's
+// frustum_args; false for a basis far from orthonormal.
+__device__ bool view_rows(const double F[3], const double L[3], const double U[3], double R[3][3]) {
+    cross3(L, U, R[0]);
+    cross3(U, F, R[1]);
+    cross3(F, L, R[2]);
+    const double det = F[0] * R[0][0] + F[1] * R[0][1] + F[2] * R[0][2];
+    if (!(__builtin_fabs(det) > 0.5) || !(__builtin_fabs(det) < 2.0)) return false;
+    for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a) R[k][a] /= det;
+    return true;
+}
+// One workgroup per (frame, view): the view's basis and point, every leaf's rectangle of
+// directions and distance, the table sorted by distance (bitonic, in LDS).  The record is
+// read from the pinned host copy (this kernel also stages it).  Conditions as the host's
+// frustum pre-test: the view point within the mesh's cull limit and below 2^30, a box
+// entirely in front (every corner at z > 2^-20 |X|) gets its corners' bounding rectangle
+// widened by 2^-18 (1 + |x|), a box entirely behind the camera is never met, anything else
+// (and, for a light, any box within near_r of it: a shadow segment ends 1e-4 past the light)
+// gets every direction.
+constexpr uint32_t kViewSort = kMaxViewLeaves;
+__device__ void build_view(const FrameRec* __restrict__ rec, uint32_t v, ViewLeaf* __restrict__ out,
+                           ViewHead* __restrict__ head) {
+    __shared__ float key[kViewSort];
+    __shared__ uint32_t idx[kViewSort];
+    __shared__ ViewLeaf tmp[kViewSort];
+    __shared__ double sR[3][3], sO[3];
+    __shared__ uint32_t s_ok;
+    __shared__ float s_near;
+    const FrameArgs& fa = rec->fa;
+    const DevMesh& m = fa.obj[0].m;
+    const uint32_t n = m.nleaves;
+    if (threadIdx.x == 0) {
+        double O[3], big = 0.0, far = 0.0;
+        const double* P = v == 0 ? fa.cam : fa.lpos[v - 1];
+        for (int k = 0; k < 3; ++k) {
+            O[k] = P[k] - fa.obj[0].pos[k];
+            big = fmax(big, fmax(__builtin_fabs(P[k]), __builtin_fabs(fa.obj[0].pos[k])));
+            far = fmax(far, __builtin_fabs(O[k]));
+        }
+        bool ok = far <= m.cull_limit && big <= 0x1p30 && n <= kMaxViewLeaves && (v > 0 || rec->fr.on);
+        double R[3][3] = {};
+        if (ok && v == 0) {
+            ok = view_rows(fa.fwd, fa.left, fa.up, R);
+        } else if (ok) {  // a light: look from it at the mesh's centre
+            double F[3] = {m.center[0] - O[0], m.center[1] - O[1], m.center[2] - O[2]};
+            const double fl = sqrt(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]);
+            if (fl > 0x1p-40 * (1.0 + far)) {
+                for (int k = 0; k < 3; ++k) F[k] /= fl;
+            } else {
+                F[0] = 0.0, F[1] = 0.0, F[2] = 1.0;
+            }
+            const int a = (__builtin_fabs(F[0]) <= __builtin_fabs(F[1]) && __builtin_fabs(F[0]) <= __builtin_fabs(F[2])) ? 0
+                          : (__builtin_fabs(F[1]) <= __builtin_fabs(F[2]) ? 1 : 2);
+            const double A[3] = {a == 0 ? 1.0 : 0.0, a == 1 ? 1.0 : 0.0, a == 2 ? 1.0 : 0.0};
+            double Lb[3], U[3];
+            cross3(A, F, Lb);
+            const double ll = sqrt(Lb[0] * Lb[0] + Lb[1] * Lb[1] + Lb[2] * Lb[2]);
+            for (int k = 0; k < 3; ++k) Lb[k] /= ll;
+            cross3(F, Lb, U);
+            ok = view_rows(F, Lb, U, R);
+        }
+        for (int k = 0; k < 3; ++k) {
+            sO[k] = O[k];
+            for (int a = 0; a < 3; ++a) sR[k][a] = R[k][a];
+        }
+        s_ok = ok ? 1u : 0u;
+        s_near = v == 0 ? 0.0f : f32_up(2.5e-4 + 0x1p-26 * (1.0 + far + m.cull_limit));
+        head->ok = s_ok;
+        head->near_r = s_near;
+        for (int k = 0; k < 3; ++k) {
+            head->O[k] = O[k];
+            for (int a = 0; a < 3; ++a) head->R[k][a] = R[k][a];
+        }
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const float inf = __builtin_inff();
+    uint32_t n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (uint32_t j = threadIdx.x; j < n2; j += blockDim.x) {
+        if (j >= n) {
+            key[j] = inf;
+            idx[j] = 0xffffffffu;
+            continue;
+        }
+        const LeafBox lb = m.leaves[j];
+        double slo = inf, shi = -inf, tlo = inf, thi = -inf, d2 = 0.0;
+        int front = 0, behind = 0;
+        for (int a = 0; a < 3; ++a) {
+            const double g = fmax(fmax((double)lb.lo[a] - sO[a], 0.0), sO[a] - (double)lb.hi[a]);
+            d2 += g * g;
+        }
+        for (int k = 0; k < 8; ++k) {
+            const double X[3] = {(double)((k & 1) ? lb.hi[0] : lb.lo[0]) - sO[0],
+                                 (double)((k & 2) ? lb.hi[1] : lb.lo[1]) - sO[1],
+                                 (double)((k & 4) ? lb.hi[2] : lb.lo[2]) - sO[2]};
+            const double mag = fmax(fmax(__builtin_fabs(X[0]), __builtin_fabs(X[1])), __builtin_fabs(X[2]));
+            const double z = sR[0][0] * X[0] + sR[0][1] * X[1] + sR[0][2] * X[2];
+            if (z > 0x1p-20 * mag) {
+                ++front;
+                const double ss = (sR[1][0] * X[0] + sR[1][1] * X[1] + sR[1][2] * X[2]) / z;
+                const double tt = (sR[2][0] * X[0] + sR[2][1] * X[1] + sR[2][2] * X[2]) / z;
+                slo = fmin(slo, ss);
+                shi = fmax(shi, ss);
+                tlo = fmin(tlo, tt);
+                thi = fmax(thi, tt);
+            } else if (z < 0.0) {
+                ++behind;
+            }
+        }
+        ViewLeaf r;
+        r.ref = lb.ref;
+        r.pad[0] = j;  // the leaf's box: DevMesh::leaves[j]
+        r.pad[1] = 0;
+        const float dmin = f32_down(sqrt(d2) * (1.0 - 0x1p-30));
+        r.dmin = dmin;
+        const bool never = v == 0 && behind == 8;
+        const bool every = front < 8 || !(__builtin_fabs(slo) + __builtin_fabs(shi) + __builtin_fabs(tlo) +
+                                              __builtin_fabs(thi) < 0x1p60) ||
+                           (v > 0 && dmin <= s_near);
+        if (never) {
+            r.dmin = inf;
+            r.s0 = r.t0 = inf;
+            r.s1 = r.t1 = -inf;
+        } else if (every) {
+            r.s0 = r.t0 = -inf;
+            r.s1 = r.t1 = inf;
+        } else {
+            r.s0 = f32_down(slo - 0x1p-18 * (1.0 + __builtin_fabs(slo)));
+            r.s1 = f32_up(shi + 0x1p-18 * (1.0 + __builtin_fabs(shi)));
+            r.t0 = f32_down(tlo - 0x1p-18 * (1.0 + __builtin_fabs(tlo)));
+            r.t1 = f32_up(thi + 0x1p-18 * (1.0 + __builtin_fabs(thi)));
+        }
+        tmp[j] = r;
+        key[j] = r.dmin;
+        idx[j] = j;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1)  // bitonic sort by distance, ascending
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) {
+                const uint32_t x = i ^ jj;
+                if (x > i) {
+                    const bool up = (i & k) == 0;
+                    const bool gt = key[i] > key[x] || (key[i] == key[x] && idx[i] > idx[x]);
+                    if (gt == up) {
+                        const float tk = key[i];
+                        key[i] = key[x];
+                        key[x] = tk;
+                        const uint32_t ti = idx[i];
+                        idx[i] = idx[x];
+                        idx[x] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = tmp[idx[j]];
+}
+
+// Block 0 copies a launch's frame records from pinned host memory to the device (a
+// hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there);
+// blocks 1 + f * nviews + v build view v of frame f (views != nullptr).
+__global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      uint32_t n16, ViewLeaf* __restrict__ views,
+                                                      ViewHead* __restrict__ heads, uint32_t nviews) {
+    if (blockIdx.x == 0) {
+        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+        return;
+    }
+    const uint32_t q = blockIdx.x - 1, f = q / nviews, v = q - f * nviews;
+    const FrameRec* rec = (const FrameRec*)src + f;
+    build_view(rec, v, views + (size_t)q * rec->fa.obj[0].m.nleaves, heads + q);
+}
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s, ViewLeaf* views,
+                               ViewHead* heads, uint32_t nviews) {
     const uint32_t n16 = (uint32_t)(n * sizeof(FrameRec) / 16);
-    hipLaunchKernelGGL(k_stage_frames, dim3(1), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16);
+    const uint32_t blocks = 1 + (views ? n * nviews : 0u);
+    hipLaunchKernelGGL(k_stage_frames, dim3(blocks), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16, views,
+                       heads, nviews);
     return hipGetLastError();
 }
 

@@ -52,6 +52,9 @@ struct MeshDev {
     uint32_t* fidx = nullptr;
     Bvh8Dev* nodes = nullptr;
     double* mats = nullptr;
+    LeafBox* leaves = nullptr;  // the BVH's leaves (view tables)
+    uint32_t nleaves = 0;
+    double center[3] = {0, 0, 0};  // bounding-box centre
     uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
     Bvh8Node root{};     // host copy of the BVH root (frustum pre-test rectangles)
@@ -111,6 +114,10 @@ struct Slot {
     cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
     FrameRec* h_frames = nullptr; // kMaxFrames pinned records of the next k_trace launch
     FrameRec* d_frames = nullptr; // their device copy
+    ViewLeaf* views = nullptr;    // view tables of the next k_trace launch (WorkArgs::views)
+    size_t views_cap = 0;
+    ViewHead* view_heads = nullptr;
+    size_t view_heads_cap = 0;
     bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
     uint32_t parity = 0;          // counter set of the next frame (two sets of kCntN)
     // device-side outputs for the host-buffer API
@@ -149,7 +156,8 @@ struct mirt_ctx {
 namespace {
 
 void mesh_free(MeshDev& m) {
-    for (void* p : {(void*)m.tri, (void*)m.vnrm, (void*)m.fmat, (void*)m.fidx, (void*)m.nodes, (void*)m.mats})
+    for (void* p : {(void*)m.tri, (void*)m.vnrm, (void*)m.fmat, (void*)m.fidx, (void*)m.nodes, (void*)m.mats,
+                    (void*)m.leaves})
         if (p) (void)hipFree(p);
     m = MeshDev();
 }
@@ -190,7 +198,7 @@ void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0,
                     (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
-                    (void*)s->d_frames})
+                    (void*)s->d_frames, (void*)s->views, (void*)s->view_heads})
         if (p) (void)hipFree(p);
     if (s->h_blocks) (void)hipHostFree(s->h_blocks);
     if (s->h_tiles) (void)hipHostFree(s->h_tiles);
@@ -315,6 +323,9 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         o.m.fmat = m.fmat;
         o.m.fidx = m.fidx;
         o.m.nodes = m.nodes;
+        o.m.leaves = m.leaves;
+        o.m.nleaves = m.nleaves;
+        for (int k = 0; k < 3; ++k) o.m.center[k] = m.center[k];
         o.m.nnodes = m.nnodes;
         o.m.depth = m.depth;
         // culling needs bounded coordinates (fp32 slab arithmetic); beyond 2^40 never cull
@@ -625,7 +636,26 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         // one launch for the frames (k_trace); its time lands in the primary slot of the profile
         FrameRec* src = nullptr;
         HIP_TRY(hipHostGetDevicePointer((void**)&src, sl->h_frames, 0));
-        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
+        // per-view leaf tables (MIRT_OPT_VIEWS; one-object frames with an LDS-resident mesh):
+        // computed by the staging kernel from the same records, one workgroup per (frame, view).
+        // Off by default: the staging kernel then waits ~43 us for a free CU ahead of k_trace,
+        // which costs more than the 9% it saves inside k_trace
+        const DevMesh& m0 = fa.obj[0].m;
+        const bool views = fa.n_objects == 1 && (c->flags & MIRT_OPT_VIEWS) && !(c->flags & MIRT_OPT_BRUTE_FORCE) &&
+                           m0.ntri <= (uint32_t)kLdsTris && m0.depth <= (uint32_t)kBvhShallowDepth &&
+                           m0.nleaves > 0 && m0.nleaves <= kMaxViewLeaves && m0.leaves;
+        uint32_t nviews = 0;
+        if (views) {
+            nviews = 1 + nl;
+            if ((r = dev_grow(sl->views, sl->views_cap, (size_t)nf * nviews * m0.nleaves)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->view_heads, sl->view_heads_cap, (size_t)nf * nviews)) != MIRT_OK) return r;
+            wa.views = sl->views;
+            wa.view_heads = sl->view_heads;
+            wa.nviews = nviews;
+            wa.view_leaves = m0.nleaves;
+        }
+        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s, views ? sl->views : nullptr,
+                                    views ? sl->view_heads : nullptr, nviews));
         wa.frames = sl->d_frames;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
@@ -840,7 +870,25 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         mt[10 * m + 9] = mats[m].ns;
     }
     const std::vector<Bvh8Dev> dev_nodes = make_dev_nodes(bvh.nodes);
+    // the leaves with the boxes their parents hold, for the per-frame view tables
+    std::vector<LeafBox> leaves;
+    double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const Bvh8Node& n : bvh.nodes)
+        for (int ch = 0; ch < 8; ++ch) {
+            if (n.child[ch] == kBvhEmpty || !(n.child[ch] & kBvhLeafBit)) continue;
+            LeafBox lb{};
+            for (int a = 0; a < 3; ++a) {
+                lb.lo[a] = n.lo(a, ch);
+                lb.hi[a] = n.hi(a, ch);
+                blo[a] = std::min(blo[a], (double)lb.lo[a]);
+                bhi[a] = std::max(bhi[a], (double)lb.hi[a]);
+            }
+            lb.ref = n.child[ch];
+            leaves.push_back(lb);
+        }
     MeshDev md;
+    md.nleaves = (uint32_t)leaves.size();
+    for (int a = 0; a < 3; ++a) md.center[a] = md.nleaves ? 0.5 * (blo[a] + bhi[a]) : 0.0;
     md.ntri = nf;
     md.nmat = nm;
     md.has_normals = has_n;
@@ -862,7 +910,8 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         (r = upload((void**)&md.fmat, fm.data(), (size_t)nf * 4)) != MIRT_OK ||
         (r = upload((void**)&md.fidx, bvh.order.data(), (size_t)nf * 4)) != MIRT_OK ||
         (r = upload((void**)&md.nodes, dev_nodes.data(), dev_nodes.size() * sizeof(Bvh8Dev))) != MIRT_OK ||
-        (r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK) {
+        (r = upload((void**)&md.mats, mt.data(), mt.size() * 8)) != MIRT_OK ||
+        (r = upload((void**)&md.leaves, leaves.data(), leaves.size() * sizeof(LeafBox))) != MIRT_OK) {
         mesh_free(md);
         return r;
     }

@@ -75,6 +75,13 @@ constexpr int kWideBatch = 8;
 // One uploaded mesh, device pointers (shared/state/mesh.go:100-106).  Every per-face
 // array is stored in BVH leaf order; fidx maps a position back to the face index of
 // the uploaded mesh (reported outputs and tie-breaking use that original index).
+// A BVH leaf as the view tables see it: its inflated fp32 box (the one its parent node
+// holds) and its ref (kBvhLeafBit | count << kBvhCountShift | first).
+struct LeafBox {
+    float lo[3], hi[3];
+    uint32_t ref, pad;
+};
+
 struct DevMesh {
     const double* tri;       // ntri * 9 : P1, E1, E2
     const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
@@ -82,14 +89,45 @@ struct DevMesh {
     const uint32_t* fidx;    // ntri     : original face index
     const Bvh8Dev* nodes;    // root first
     const double* mats;      // nmat * 10: ka[3] kd[3] ks[3] ns
+    const LeafBox* leaves;   // nleaves BVH leaves (view tables)
     uint32_t ntri;
     uint32_t has_normals;
     uint32_t nnodes;
     uint32_t depth;
     int32_t wide_thresh;     // wide traversal batches nodes only while sp <= this (< 0: never)
-    uint32_t pad;
+    uint32_t nleaves;
     double cull_limit;       // rays whose object-space origin has a coordinate beyond this
                              // are never culled (tolerance scales with |origin|)
+    double center[3];        // centre of the mesh's bounding box (light views look at it)
+};
+
+// View tables (one-object frames with an LDS-resident mesh).  A view is a point every ray
+// of a packet passes through: the camera for primary rays, a light for shadow rays (a
+// shadow segment runs from its hit point to the light).  With R = [F L U]^-1 for a basis
+// (F, L, U) of the view, a point X (relative to the view point) lies in direction
+// (s, t) = (R1.X / z, R2.X / z) at depth z = R0.X.  Per frame and view the staging kernel
+// projects every leaf box (a box entirely in front: the bounding rectangle of its corners'
+// (s, t), rounded outward with a relative margin of 2^-18; anything else: every direction)
+// and sorts the leaves by their distance from the view point.  A packet then scans the
+// table instead of walking the BVH: a leaf is tested when some live lane's direction lies
+// in its rectangle and the leaf is not farther than that lane's depth bound; the scan stops
+// at the first leaf farther than every live lane's bound.  Exact for the reason the block
+// frustum pre-test is: a hit lies in its inflated leaf box, so its direction from the view
+// point lies in the box's projection.
+struct ViewLeaf {
+    float s0, s1, t0, t1;  // rectangle of directions (every direction: -inf, inf, -inf, inf)
+    float dmin;            // distance from the view point to the box, rounded down (+inf: never met)
+    uint32_t ref;          // the BVH leaf ref
+    uint32_t pad[2];
+};
+constexpr uint32_t kMaxViewLeaves = 512;  // meshes with more leaves walk the BVH
+// One view of one frame: 0 = the camera, 1 + l = light l.  ok = 0: no table (walk the BVH).
+struct ViewHead {
+    uint32_t ok;
+    float near_r;          // light views: leaves within this distance of the light are always tested
+    uint32_t pad[2];
+    double R[3][3];        // the view's projection rows
+    double O[3];           // the view point, object space
 };
 
 // Kernel modes (mirt_set_options): exact BVH culling (default) or brute force.
@@ -242,6 +280,12 @@ struct WorkArgs {
     const FrameRec* frames;  // k_trace: nframes records; blocks [f * nblocks_frame, ...) are frame f's
     uint32_t nframes;
     uint32_t nblocks_frame;  // nblocks = nframes * nblocks_frame; the table describes one frame
+    // view tables (k_trace, one-object frames, nullptr: none): frame f, view v at
+    // views + (f * nviews + v) * nleaves, its header at view_heads[f * nviews + v]
+    const ViewLeaf* views;
+    const ViewHead* view_heads;
+    uint32_t nviews;         // 1 + lights
+    uint32_t view_leaves;    // leaves per table
 };
 constexpr int kTimelineRec = 8;
 // WorkArgs::dynamic: kernels whose waves take work items dynamically (primary: LDS tickets
@@ -261,7 +305,8 @@ struct RayIO {
     uint32_t n;
 };
 
-hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s);
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s,
+                               ViewLeaf* views = nullptr, ViewHead* heads = nullptr, uint32_t nviews = 0);
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,

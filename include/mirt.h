@@ -242,6 +242,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_SPLIT_KERNELS 32u  /* k_primary then k_shadow (default: one k_trace launch per frame) */
 #define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
 #define MIRT_OPT_NO_OCTANT 128u     /* generic child-box test (no sign-octant variants; same decisions) */
+#define MIRT_OPT_VIEWS 256u         /* per-frame view tables instead of the BVH walk (same results; slower) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 /*
  * Launch shape of the frame kernel: every workgroup owns at least min_blocks_per_wg 8x8

@@ -78,7 +78,7 @@ def _variants(ctx, fn):
                      rt._lib.MIRT_OPT_BRUTE_FORCE | rt._lib.MIRT_OPT_NO_PREFILTER,
                      rt._lib.MIRT_OPT_STATIC_SCHEDULE, rt._lib.MIRT_OPT_NO_SEGMENT,
                      rt._lib.MIRT_OPT_SPLIT_KERNELS, rt._lib.MIRT_OPT_SPLIT_KERNELS | rt._lib.MIRT_OPT_BRUTE_FORCE,
-                     rt._lib.MIRT_OPT_NO_FRUSTUM):
+                     rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_VIEWS):
             ctx.set_options(opts)
             out[opts] = fn()
     finally:
@@ -143,7 +143,7 @@ def test_block_frustum_exact_at_awkward_cameras(ctx, env):
         cam = rt.Camera.new(tuple(pos), tuple(look), fov)
         mut = rt.EnvMutables(base.objects, base.lights, cam)
         res = {}
-        for opts in (0, rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_BRUTE_FORCE):
+        for opts in (0, rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_VIEWS, rt._lib.MIRT_OPT_BRUTE_FORCE):
             ctx.set_options(opts)
             res[opts] = rt.draw(env, W, H, mut)
         ctx.set_options(0)
@@ -172,12 +172,41 @@ def test_shadow_segments_exact_with_lights_near_surfaces(ctx, env):
             lights.append(rt.Light(tuple(float(x) for x in p), (1.0, 200 / 255, 100 / 255)))
         mut = rt.EnvMutables(base.objects, lights, base.cam)
         res = {}
-        for opts in (0, rt._lib.MIRT_OPT_BRUTE_FORCE, rt._lib.MIRT_OPT_NO_SEGMENT, rt._lib.MIRT_OPT_SPLIT_KERNELS):
+        for opts in (0, rt._lib.MIRT_OPT_BRUTE_FORCE, rt._lib.MIRT_OPT_NO_SEGMENT, rt._lib.MIRT_OPT_SPLIT_KERNELS,
+                     rt._lib.MIRT_OPT_VIEWS):
             ctx.set_options(opts)
             res[opts] = rt.draw(env, 320, 240, mut)
         ctx.set_options(0)
         assert res[0].valid.sum() > 1000
         _same_frames(res)
+
+
+def test_view_tables_exact_for_light_and_camera_placements(ctx, env):
+    """The per-view leaf tables (primary rays from the camera, shadow segments from each
+    light) never change a pixel: lights far away, at the mesh's centre, inside its bounding
+    box, just above the surface, behind the camera and level with the object; cameras from
+    several sides.  The BVH walk (default) vs view tables (MIRT_OPT_VIEWS) vs brute force, bit-exact."""
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    c0 = np.array([1.0, 1.0, -1.0])
+    v = np.asarray(env.meshes[0].vertices, np.float64).reshape(-1, 3) + c0
+    col = (1.0, 200 / 255, 100 / 255)
+    lights = [c0 + [0.0, 0.0, 40.0], c0 + [0.0, 0.0, 0.0], c0 + [0.1, 0.2, -0.1], v[17] * 1.0 + [0.0, 0.0, 1e-3],
+              np.asarray(base.cam.pos) + [0.0, 0.0, 1.0], c0 + [3.0, 0.0, 0.0], c0 + [0.0, -5.0, 0.0],
+              v[200] + [0.0, 1e-4, 0.0]]
+    cams = [(base.cam.pos, base.cam.forward, base.cam.fov), (c0 + [4.0, 1.0, 0.5], (-1.0, -0.2, -0.1), 0.9),
+            (c0 + [0.0, -3.0, 0.2], (0.0, 1.0, -0.05), 1.1)]
+    for pos, fwd, fov in cams:
+        for k in range(0, len(lights), 4):
+            mut = rt.EnvMutables(base.objects, [rt.Light(tuple(float(x) for x in p), col) for p in lights[k:k + 4]],
+                                 rt.Camera.new(tuple(pos), tuple(fwd), fov))
+            res = {}
+            for opts in (0, rt._lib.MIRT_OPT_VIEWS, rt._lib.MIRT_OPT_BRUTE_FORCE):
+                ctx.set_options(opts)
+                res[opts] = rt.draw(env, 256, 192, mut)
+            ctx.set_options(0)
+            assert res[0].valid.sum() > 500
+            _same_frames(res)
 
 
 def test_bvh_far_camera_and_streamed_mesh(ctx, py_scene):
