@@ -997,7 +997,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
                                              vis.overflow, tmax, resolve);
     } else if (resident && vt) {
         // the lane's direction from the light: its hit point relative to the view point (every
-        // point of the segment short of the light lies in that direction, DESIGN.md §4.9)
+        // point of the segment short of the light lies in that direction, DESIGN.md §4.8)
         const double* R0 = vh->R[0];
         const double* R1 = vh->R[1];
         const double* R2 = vh->R[2];
@@ -1395,6 +1395,233 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     pc.lap(2);
 }
 
+// ---------------------------------------------------------------- view tables (ViewLeaf)
+// the float next to finite f towards -inf / +inf
+__device__ __forceinline__ float f32_prev(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return f == 0.0f ? -0x1p-149f : __uint_as_float((int32_t)b > 0 ? b - 1u : b + 1u);
+}
+__device__ __forceinline__ float f32_next(float f) { return -f32_prev(-f); }
+// x rounded to float downwards / upwards (NaN stays NaN)
+__device__ __forceinline__ float f32_down(double x) {
+    const float f = (float)x;
+    return ((double)f > x && __builtin_isfinite(f)) ? f32_prev(f) : ((double)f > x ? 0x1.fffffep127f : f);
+}
+__device__ __forceinline__ float f32_up(double x) {
+    const float f = (float)x;
+    return ((double)f < x && __builtin_isfinite(f)) ? f32_next(f) : ((double)f < x ? -0x1.fffffep127f : f);
+}
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+// R = [F L U]^-1 by cofactors (row k: column k+1 x column k+2, / det), as the host's
+// frustum_args; false for a basis far from orthonormal.
+__device__ bool view_rows(const double F[3], const double L[3], const double U[3], double R[3][3]) {
+    cross3(L, U, R[0]);
+    cross3(U, F, R[1]);
+    cross3(F, L, R[2]);
+    const double det = F[0] * R[0][0] + F[1] * R[0][1] + F[2] * R[0][2];
+    if (!(__builtin_fabs(det) > 0.5) || !(__builtin_fabs(det) < 2.0)) return false;
+    for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a) R[k][a] /= det;
+    return true;
+}
+// One workgroup per (frame, view): the view's basis and point, every leaf's rectangle of
+// directions and distance, the table sorted by distance (bitonic, in the LDS scratch), then
+// published: every thread's stores fenced at agent scope, then the header's tag stored with
+// release semantics (readers: view_ready).  Conditions as the host's
+// frustum pre-test: the view point within the mesh's cull limit and below 2^30, a box
+// entirely in front (every corner at z > 2^-20 |X|) gets its corners' bounding rectangle
+// widened by 2^-18 (1 + |x|), a box entirely behind the camera is never met, anything else
+// (and, for a light, any box within near_r of it: a shadow segment ends 1e-4 past the light)
+// gets every direction.
+constexpr uint32_t kViewSort = kMaxViewLeaves;
+struct ViewScratch {
+    ViewLeaf tmp[kViewSort];
+    float key[kViewSort];
+    uint32_t idx[kViewSort];
+    double R[3][3], O[3];
+    uint32_t ok;
+    float near_r;
+};
+constexpr size_t kViewScratchBytes = sizeof(ViewScratch);
+__device__ void build_view(const FrameRec& rec, uint32_t v, ViewLeaf* __restrict__ out, ViewHead* __restrict__ head,
+                           void* scratch, uint32_t tag) {
+    ViewScratch& sc = *(ViewScratch*)scratch;
+    float* const key = sc.key;
+    uint32_t* const idx = sc.idx;
+    ViewLeaf* const tmp = sc.tmp;
+    double (*const sR)[3] = sc.R;
+    double* const sO = sc.O;
+    const FrameArgs& fa = rec.fa;
+    const DevMesh& m = fa.obj[0].m;
+    const uint32_t n = m.nleaves;
+    if (threadIdx.x == 0) {
+        double O[3], big = 0.0, far = 0.0;
+        const double* P = v == 0 ? fa.cam : fa.lpos[v - 1];
+        for (int k = 0; k < 3; ++k) {
+            O[k] = P[k] - fa.obj[0].pos[k];
+            big = fmax(big, fmax(__builtin_fabs(P[k]), __builtin_fabs(fa.obj[0].pos[k])));
+            far = fmax(far, __builtin_fabs(O[k]));
+        }
+        bool ok = far <= m.cull_limit && big <= 0x1p30 && n <= kMaxViewLeaves && (v > 0 || rec.fr.on);
+        double R[3][3] = {};
+        if (ok && v == 0) {
+            ok = view_rows(fa.fwd, fa.left, fa.up, R);
+        } else if (ok) {  // a light: look from it at the mesh's centre
+            double F[3] = {m.center[0] - O[0], m.center[1] - O[1], m.center[2] - O[2]};
+            const double fl = sqrt(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]);
+            if (fl > 0x1p-40 * (1.0 + far)) {
+                for (int k = 0; k < 3; ++k) F[k] /= fl;
+            } else {
+                F[0] = 0.0, F[1] = 0.0, F[2] = 1.0;
+            }
+            const int a = (__builtin_fabs(F[0]) <= __builtin_fabs(F[1]) && __builtin_fabs(F[0]) <= __builtin_fabs(F[2])) ? 0
+                          : (__builtin_fabs(F[1]) <= __builtin_fabs(F[2]) ? 1 : 2);
+            const double A[3] = {a == 0 ? 1.0 : 0.0, a == 1 ? 1.0 : 0.0, a == 2 ? 1.0 : 0.0};
+            double Lb[3], U[3];
+            cross3(A, F, Lb);
+            const double ll = sqrt(Lb[0] * Lb[0] + Lb[1] * Lb[1] + Lb[2] * Lb[2]);
+            for (int k = 0; k < 3; ++k) Lb[k] /= ll;
+            cross3(F, Lb, U);
+            ok = view_rows(F, Lb, U, R);
+        }
+        for (int k = 0; k < 3; ++k) {
+            sO[k] = O[k];
+            for (int a = 0; a < 3; ++a) sR[k][a] = R[k][a];
+        }
+        sc.ok = ok ? 1u : 0u;
+        sc.near_r = v == 0 ? 0.0f : f32_up(2.5e-4 + 0x1p-26 * (1.0 + far + m.cull_limit));
+        head->ok = sc.ok;
+        head->near_r = sc.near_r;
+        for (int k = 0; k < 3; ++k) {
+            head->O[k] = O[k];
+            for (int a = 0; a < 3; ++a) head->R[k][a] = R[k][a];
+        }
+    }
+    __syncthreads();
+    const float inf = __builtin_inff();
+    const float s_near = sc.near_r;
+    uint32_t n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    const uint32_t nt = sc.ok ? n2 : 0u;  // an unusable view publishes its header only
+    for (uint32_t j = threadIdx.x; j < nt; j += blockDim.x) {
+        if (j >= n) {
+            key[j] = inf;
+            idx[j] = 0xffffffffu;
+            continue;
+        }
+        const LeafBox lb = m.leaves[j];
+        double slo = inf, shi = -inf, tlo = inf, thi = -inf, d2 = 0.0;
+        int front = 0, behind = 0;
+        for (int a = 0; a < 3; ++a) {
+            const double g = fmax(fmax((double)lb.lo[a] - sO[a], 0.0), sO[a] - (double)lb.hi[a]);
+            d2 += g * g;
+        }
+        for (int k = 0; k < 8; ++k) {
+            const double X[3] = {(double)((k & 1) ? lb.hi[0] : lb.lo[0]) - sO[0],
+                                 (double)((k & 2) ? lb.hi[1] : lb.lo[1]) - sO[1],
+                                 (double)((k & 4) ? lb.hi[2] : lb.lo[2]) - sO[2]};
+            const double mag = fmax(fmax(__builtin_fabs(X[0]), __builtin_fabs(X[1])), __builtin_fabs(X[2]));
+            const double z = sR[0][0] * X[0] + sR[0][1] * X[1] + sR[0][2] * X[2];
+            if (z > 0x1p-20 * mag) {
+                ++front;
+                const double ss = (sR[1][0] * X[0] + sR[1][1] * X[1] + sR[1][2] * X[2]) / z;
+                const double tt = (sR[2][0] * X[0] + sR[2][1] * X[1] + sR[2][2] * X[2]) / z;
+                slo = fmin(slo, ss);
+                shi = fmax(shi, ss);
+                tlo = fmin(tlo, tt);
+                thi = fmax(thi, tt);
+            } else if (z < 0.0) {
+                ++behind;
+            }
+        }
+        ViewLeaf r;
+        r.ref = lb.ref;
+        r.pad[0] = j;  // the leaf's box: DevMesh::leaves[j]
+        r.pad[1] = 0;
+        const float dmin = f32_down(sqrt(d2) * (1.0 - 0x1p-30));
+        r.dmin = dmin;
+        const bool never = v == 0 && behind == 8;
+        const bool every = front < 8 || !(__builtin_fabs(slo) + __builtin_fabs(shi) + __builtin_fabs(tlo) +
+                                              __builtin_fabs(thi) < 0x1p60) ||
+                           (v > 0 && dmin <= s_near);
+        if (never) {
+            r.dmin = inf;
+            r.s0 = r.t0 = inf;
+            r.s1 = r.t1 = -inf;
+        } else if (every) {
+            r.s0 = r.t0 = -inf;
+            r.s1 = r.t1 = inf;
+        } else {
+            r.s0 = f32_down(slo - 0x1p-18 * (1.0 + __builtin_fabs(slo)));
+            r.s1 = f32_up(shi + 0x1p-18 * (1.0 + __builtin_fabs(shi)));
+            r.t0 = f32_down(tlo - 0x1p-18 * (1.0 + __builtin_fabs(tlo)));
+            r.t1 = f32_up(thi + 0x1p-18 * (1.0 + __builtin_fabs(thi)));
+        }
+        tmp[j] = r;
+        key[j] = r.dmin;
+        idx[j] = j;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= nt; k <<= 1)  // bitonic sort by distance, ascending
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) {
+                const uint32_t x = i ^ jj;
+                if (x > i) {
+                    const bool up = (i & k) == 0;
+                    const bool gt = key[i] > key[x] || (key[i] == key[x] && idx[i] > idx[x]);
+                    if (gt == up) {
+                        const float tk = key[i];
+                        key[i] = key[x];
+                        key[x] = tk;
+                        const uint32_t ti = idx[i];
+                        idx[i] = idx[x];
+                        idx[x] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    if (sc.ok)
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = tmp[idx[j]];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&head->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The workgroup's copies of the launch's view headers (k_trace's LDS): state 0 = not seen
+// published yet, 1 = published and usable, 2 = published, not usable.
+struct ViewCache {
+    ViewHead* head;
+    uint32_t* state;
+};
+// Table q of this launch if it is published and usable, else nullptr (the caller walks the
+// BVH).  The first wave of a workgroup to see the builder's tag (an agent-scope acquire
+// after it) copies the header into the workgroup's LDS and publishes that to its peers; the
+// table itself is read after that acquire.
+__device__ __forceinline__ const ViewHead* view_lookup(const WorkArgs& wa, uint32_t q, const ViewCache& vc) {
+    uint32_t st = __hip_atomic_load(&vc.state[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (st == 0) {
+        if (__hip_atomic_load(&wa.view_heads[q].tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != wa.view_tag)
+            return nullptr;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // lanes 0..9 copy one 8-byte word of ok / near_r / R / O each, past the scalar cache
+        const uint32_t lane = threadIdx.x & 63;
+        const unsigned long long* src = (const unsigned long long*)&wa.view_heads[q];
+        unsigned long long* dst = (unsigned long long*)&vc.head[q];
+        constexpr uint32_t kWords = sizeof(ViewHead) / 8;
+        if (lane < kWords)
+            dst[lane] = __hip_atomic_load((unsigned long long*)src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st = __hip_atomic_load((uint32_t*)&wa.view_heads[q].ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 2u;
+        __hip_atomic_store(&vc.state[q], st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return st == 1 ? &vc.head[q] : nullptr;
+}
+
+
+
 // ---------------------------------------------------------------- shadow item
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
@@ -1403,7 +1630,8 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
 template <bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
-                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u) {
+                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u,
+                                            const ViewCache* vc = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
@@ -1427,12 +1655,10 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     } else if (segment) {
         const ViewLeaf* vt = nullptr;
         const ViewHead* vh = nullptr;
-        if (vf != ~0u && wa.views) {
+        if (vf != ~0u && wa.views && vc) {
             const uint32_t q = vf * wa.nviews + 1 + l;
-            if (((const __attribute__((address_space(4))) ViewHead*)wa.view_heads)[q].ok) {
-                vh = wa.view_heads + q;
-                vt = wa.views + (size_t)q * wa.view_leaves;
-            }
+            vh = view_lookup(wa, q, *vc);
+            if (vh) vt = wa.views + (size_t)q * wa.view_leaves;
         }
         is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis, vt, wa.view_leaves,
                                               vh);
@@ -1632,6 +1858,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
     __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
+    __shared__ ViewHead s_vhead[RESIDENT ? kMaxViewTables : 1];
+    __shared__ uint32_t s_vstate[RESIDENT ? kMaxViewTables : 1];
+    const ViewCache vc{s_vhead, s_vstate};
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     WaveClock clock;
     uint32_t taken = 0;
@@ -1642,6 +1871,14 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     if (use_frustum && threadIdx.x < 8 * NF) {
         const float* r = wa.frames[threadIdx.x >> 3].fr.rect[threadIdx.x & 7];
         frect[threadIdx.x >> 3][threadIdx.x & 7] = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    if (RESIDENT && threadIdx.x < kMaxViewTables) s_vstate[threadIdx.x] = 0;  // read after the batch barrier
+    if (RESIDENT && wa.views && blockIdx.x < NF * wa.nviews) {
+        // the launch's first workgroups build the view tables in the mesh's LDS, then stage it
+        const uint32_t q = blockIdx.x, f = q / wa.nviews;
+        build_view(frame_rec(wa, f), q - f * wa.nviews, wa.views + (size_t)q * wa.view_leaves, wa.view_heads + q, lds,
+                   wa.view_tag);
+        __syncthreads();
     }
     if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
     uint32_t* stk = wstk[threadIdx.x >> 6];
@@ -1721,7 +1958,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
                 const FrameRec& fr = frame_rec(wa, cf);
                 shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
-                                              wsh, RESIDENT ? cf : ~0u);
+                                              wsh, RESIDENT ? cf : ~0u, &vc);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -1742,10 +1979,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                     const uint32_t f = __builtin_amdgcn_readfirstlane(bq_frame[t]);
                     const FrameRec& fr = frame_rec(wa, f);
                     lc.frame = f;
-                    // the camera's view table of this frame (ViewHead::ok: built)
+                    // the camera's view table of this frame, once published (and usable)
                     const ViewLeaf* vt = nullptr;
-                    if (RESIDENT && wa.views && fr.fr.on &&
-                        ((const __attribute__((address_space(4))) ViewHead*)wa.view_heads)[f * wa.nviews].ok)
+                    if (RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
                                                            use_frustum, frect[f], &lc,
@@ -2087,7 +2323,7 @@ hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
 hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                         hipStream_t s) {
     const bool resident = is_resident(fa);
-    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+    const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0) : 0;
 #define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE
@@ -2341,208 +2577,15 @@ hipError_t launch_fill_planes(const FillJobs& jobs, uint32_t nframes, uint64_t m
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- view tables (ViewLeaf)
-// the float next to finite f towards -inf / +inf
-__device__ __forceinline__ float f32_prev(float f) {
-    const uint32_t b = __float_as_uint(f);
-    return f == 0.0f ? -0x1p-149f : __uint_as_float((int32_t)b > 0 ? b - 1u : b + 1u);
-}
-__device__ __forceinline__ float f32_next(float f) { return -f32_prev(-f); }
-// x rounded to float downwards / upwards (NaN stays NaN)
-__device__ __forceinline__ float f32_down(double x) {
-    const float f = (float)x;
-    return ((double)f > x && __builtin_isfinite(f)) ? f32_prev(f) : ((double)f > x ? 0x1.fffffep127f : f);
-}
-__device__ __forceinline__ float f32_up(double x) {
-    const float f = (float)x;
-    return ((double)f < x && __builtin_isfinite(f)) ? f32_next(f) : ((double)f < x ? -0x1.fffffep127f : f);
-}
-__device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
-    r[0] = a[1] * b[2] - a[2] * b[1];
-    r[1] = a[2] * b[0] - a[0] * b[2];
-    r[2] = a[0] * b[1] - a[1] * b[0];
-}
-// R = [F L U]^-1 by cofactors (row k: column k+1 x column k+2, / det), as the host's
-// frustum_args; false for a basis far from orthonormal.
-__device__ bool view_rows(const double F[3], const double L[3], const double U[3], double R[3][3]) {
-    cross3(L, U, R[0]);
-    cross3(U, F, R[1]);
-    cross3(F, L, R[2]);
-    const double det = F[0] * R[0][0] + F[1] * R[0][1] + F[2] * R[0][2];
-    if (!(__builtin_fabs(det) > 0.5) || !(__builtin_fabs(det) < 2.0)) return false;
-    for (int k = 0; k < 3; ++k)
-        for (int a = 0; a < 3; ++a) R[k][a] /= det;
-    return true;
-}
-// One workgroup per (frame, view): the view's basis and point, every leaf's rectangle of
-// directions and distance, the table sorted by distance (bitonic, in LDS).  The record is
-// read from the pinned host copy (this kernel also stages it).  Conditions as the host's
-// frustum pre-test: the view point within the mesh's cull limit and below 2^30, a box
-// entirely in front (every corner at z > 2^-20 |X|) gets its corners' bounding rectangle
-// widened by 2^-18 (1 + |x|), a box entirely behind the camera is never met, anything else
-// (and, for a light, any box within near_r of it: a shadow segment ends 1e-4 past the light)
-// gets every direction.
-constexpr uint32_t kViewSort = kMaxViewLeaves;
-__device__ void build_view(const FrameRec* __restrict__ rec, uint32_t v, ViewLeaf* __restrict__ out,
-                           ViewHead* __restrict__ head) {
-    __shared__ float key[kViewSort];
-    __shared__ uint32_t idx[kViewSort];
-    __shared__ ViewLeaf tmp[kViewSort];
-    __shared__ double sR[3][3], sO[3];
-    __shared__ uint32_t s_ok;
-    __shared__ float s_near;
-    const FrameArgs& fa = rec->fa;
-    const DevMesh& m = fa.obj[0].m;
-    const uint32_t n = m.nleaves;
-    if (threadIdx.x == 0) {
-        double O[3], big = 0.0, far = 0.0;
-        const double* P = v == 0 ? fa.cam : fa.lpos[v - 1];
-        for (int k = 0; k < 3; ++k) {
-            O[k] = P[k] - fa.obj[0].pos[k];
-            big = fmax(big, fmax(__builtin_fabs(P[k]), __builtin_fabs(fa.obj[0].pos[k])));
-            far = fmax(far, __builtin_fabs(O[k]));
-        }
-        bool ok = far <= m.cull_limit && big <= 0x1p30 && n <= kMaxViewLeaves && (v > 0 || rec->fr.on);
-        double R[3][3] = {};
-        if (ok && v == 0) {
-            ok = view_rows(fa.fwd, fa.left, fa.up, R);
-        } else if (ok) {  // a light: look from it at the mesh's centre
-            double F[3] = {m.center[0] - O[0], m.center[1] - O[1], m.center[2] - O[2]};
-            const double fl = sqrt(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]);
-            if (fl > 0x1p-40 * (1.0 + far)) {
-                for (int k = 0; k < 3; ++k) F[k] /= fl;
-            } else {
-                F[0] = 0.0, F[1] = 0.0, F[2] = 1.0;
-            }
-            const int a = (__builtin_fabs(F[0]) <= __builtin_fabs(F[1]) && __builtin_fabs(F[0]) <= __builtin_fabs(F[2])) ? 0
-                          : (__builtin_fabs(F[1]) <= __builtin_fabs(F[2]) ? 1 : 2);
-            const double A[3] = {a == 0 ? 1.0 : 0.0, a == 1 ? 1.0 : 0.0, a == 2 ? 1.0 : 0.0};
-            double Lb[3], U[3];
-            cross3(A, F, Lb);
-            const double ll = sqrt(Lb[0] * Lb[0] + Lb[1] * Lb[1] + Lb[2] * Lb[2]);
-            for (int k = 0; k < 3; ++k) Lb[k] /= ll;
-            cross3(F, Lb, U);
-            ok = view_rows(F, Lb, U, R);
-        }
-        for (int k = 0; k < 3; ++k) {
-            sO[k] = O[k];
-            for (int a = 0; a < 3; ++a) sR[k][a] = R[k][a];
-        }
-        s_ok = ok ? 1u : 0u;
-        s_near = v == 0 ? 0.0f : f32_up(2.5e-4 + 0x1p-26 * (1.0 + far + m.cull_limit));
-        head->ok = s_ok;
-        head->near_r = s_near;
-        for (int k = 0; k < 3; ++k) {
-            head->O[k] = O[k];
-            for (int a = 0; a < 3; ++a) head->R[k][a] = R[k][a];
-        }
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const float inf = __builtin_inff();
-    uint32_t n2 = 1;
-    while (n2 < n) n2 <<= 1;
-    for (uint32_t j = threadIdx.x; j < n2; j += blockDim.x) {
-        if (j >= n) {
-            key[j] = inf;
-            idx[j] = 0xffffffffu;
-            continue;
-        }
-        const LeafBox lb = m.leaves[j];
-        double slo = inf, shi = -inf, tlo = inf, thi = -inf, d2 = 0.0;
-        int front = 0, behind = 0;
-        for (int a = 0; a < 3; ++a) {
-            const double g = fmax(fmax((double)lb.lo[a] - sO[a], 0.0), sO[a] - (double)lb.hi[a]);
-            d2 += g * g;
-        }
-        for (int k = 0; k < 8; ++k) {
-            const double X[3] = {(double)((k & 1) ? lb.hi[0] : lb.lo[0]) - sO[0],
-                                 (double)((k & 2) ? lb.hi[1] : lb.lo[1]) - sO[1],
-                                 (double)((k & 4) ? lb.hi[2] : lb.lo[2]) - sO[2]};
-            const double mag = fmax(fmax(__builtin_fabs(X[0]), __builtin_fabs(X[1])), __builtin_fabs(X[2]));
-            const double z = sR[0][0] * X[0] + sR[0][1] * X[1] + sR[0][2] * X[2];
-            if (z > 0x1p-20 * mag) {
-                ++front;
-                const double ss = (sR[1][0] * X[0] + sR[1][1] * X[1] + sR[1][2] * X[2]) / z;
-                const double tt = (sR[2][0] * X[0] + sR[2][1] * X[1] + sR[2][2] * X[2]) / z;
-                slo = fmin(slo, ss);
-                shi = fmax(shi, ss);
-                tlo = fmin(tlo, tt);
-                thi = fmax(thi, tt);
-            } else if (z < 0.0) {
-                ++behind;
-            }
-        }
-        ViewLeaf r;
-        r.ref = lb.ref;
-        r.pad[0] = j;  // the leaf's box: DevMesh::leaves[j]
-        r.pad[1] = 0;
-        const float dmin = f32_down(sqrt(d2) * (1.0 - 0x1p-30));
-        r.dmin = dmin;
-        const bool never = v == 0 && behind == 8;
-        const bool every = front < 8 || !(__builtin_fabs(slo) + __builtin_fabs(shi) + __builtin_fabs(tlo) +
-                                              __builtin_fabs(thi) < 0x1p60) ||
-                           (v > 0 && dmin <= s_near);
-        if (never) {
-            r.dmin = inf;
-            r.s0 = r.t0 = inf;
-            r.s1 = r.t1 = -inf;
-        } else if (every) {
-            r.s0 = r.t0 = -inf;
-            r.s1 = r.t1 = inf;
-        } else {
-            r.s0 = f32_down(slo - 0x1p-18 * (1.0 + __builtin_fabs(slo)));
-            r.s1 = f32_up(shi + 0x1p-18 * (1.0 + __builtin_fabs(shi)));
-            r.t0 = f32_down(tlo - 0x1p-18 * (1.0 + __builtin_fabs(tlo)));
-            r.t1 = f32_up(thi + 0x1p-18 * (1.0 + __builtin_fabs(thi)));
-        }
-        tmp[j] = r;
-        key[j] = r.dmin;
-        idx[j] = j;
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= n2; k <<= 1)  // bitonic sort by distance, ascending
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) {
-                const uint32_t x = i ^ jj;
-                if (x > i) {
-                    const bool up = (i & k) == 0;
-                    const bool gt = key[i] > key[x] || (key[i] == key[x] && idx[i] > idx[x]);
-                    if (gt == up) {
-                        const float tk = key[i];
-                        key[i] = key[x];
-                        key[x] = tk;
-                        const uint32_t ti = idx[i];
-                        idx[i] = idx[x];
-                        idx[x] = ti;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = tmp[idx[j]];
-}
-
-// Block 0 copies a launch's frame records from pinned host memory to the device (a
-// hipMemcpyAsync of a few KB from pinned memory held the host until the stream got there);
-// blocks 1 + f * nviews + v build view v of frame f (views != nullptr).
+// Copies a launch's frame records from pinned host memory to the device (a hipMemcpyAsync
+// of a few KB from pinned memory held the host until the stream got there).
 __global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                      uint32_t n16, ViewLeaf* __restrict__ views,
-                                                      ViewHead* __restrict__ heads, uint32_t nviews) {
-    if (blockIdx.x == 0) {
-        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
-        return;
-    }
-    const uint32_t q = blockIdx.x - 1, f = q / nviews, v = q - f * nviews;
-    const FrameRec* rec = (const FrameRec*)src + f;
-    build_view(rec, v, views + (size_t)q * rec->fa.obj[0].m.nleaves, heads + q);
+                                                      uint32_t n16) {
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
 }
-hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s, ViewLeaf* views,
-                               ViewHead* heads, uint32_t nviews) {
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s) {
     const uint32_t n16 = (uint32_t)(n * sizeof(FrameRec) / 16);
-    const uint32_t blocks = 1 + (views ? n * nviews : 0u);
-    hipLaunchKernelGGL(k_stage_frames, dim3(blocks), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16, views,
-                       heads, nviews);
+    hipLaunchKernelGGL(k_stage_frames, dim3(1), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16);
     return hipGetLastError();
 }
 

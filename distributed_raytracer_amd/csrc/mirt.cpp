@@ -118,6 +118,7 @@ struct Slot {
     size_t views_cap = 0;
     ViewHead* view_heads = nullptr;
     size_t view_heads_cap = 0;
+    uint32_t view_tag = 0;  // the last launch's WorkArgs::view_tag
     bool dirty = false;           // counters possibly non-zero (a frame stopped half-way)
     uint32_t parity = 0;          // counter set of the next frame (two sets of kCntN)
     // device-side outputs for the host-buffer API
@@ -637,25 +638,28 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         FrameRec* src = nullptr;
         HIP_TRY(hipHostGetDevicePointer((void**)&src, sl->h_frames, 0));
         // per-view leaf tables (MIRT_OPT_VIEWS; one-object frames with an LDS-resident mesh):
-        // computed by the staging kernel from the same records, one workgroup per (frame, view).
-        // Off by default: the staging kernel then waits ~43 us for a free CU ahead of k_trace,
-        // which costs more than the 9% it saves inside k_trace
+        // built by k_trace's first workgroups, one per (frame, view)
         const DevMesh& m0 = fa.obj[0].m;
         const bool views = fa.n_objects == 1 && (c->flags & MIRT_OPT_VIEWS) && !(c->flags & MIRT_OPT_BRUTE_FORCE) &&
                            m0.ntri <= (uint32_t)kLdsTris && m0.depth <= (uint32_t)kBvhShallowDepth &&
                            m0.nleaves > 0 && m0.nleaves <= kMaxViewLeaves && m0.leaves;
         uint32_t nviews = 0;
-        if (views) {
+        if (views && (size_t)nf * (1 + nl) <= kMaxViewTables) {
             nviews = 1 + nl;
             if ((r = dev_grow(sl->views, sl->views_cap, (size_t)nf * nviews * m0.nleaves)) != MIRT_OK) return r;
+            const size_t heads_cap = sl->view_heads_cap;
             if ((r = dev_grow(sl->view_heads, sl->view_heads_cap, (size_t)nf * nviews)) != MIRT_OK) return r;
+            // a fresh buffer holds no tag (tags start at 1)
+            if (sl->view_heads_cap != heads_cap)
+                HIP_TRY(hipMemsetAsync(sl->view_heads, 0, sl->view_heads_cap * sizeof(ViewHead), s));
+            if (++sl->view_tag == 0) sl->view_tag = 1;
+            wa.view_tag = sl->view_tag;
             wa.views = sl->views;
             wa.view_heads = sl->view_heads;
             wa.nviews = nviews;
             wa.view_leaves = m0.nleaves;
         }
-        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s, views ? sl->views : nullptr,
-                                    views ? sl->view_heads : nullptr, nviews));
+        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
         wa.frames = sl->d_frames;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);

@@ -105,15 +105,17 @@ struct DevMesh {
 // of a packet passes through: the camera for primary rays, a light for shadow rays (a
 // shadow segment runs from its hit point to the light).  With R = [F L U]^-1 for a basis
 // (F, L, U) of the view, a point X (relative to the view point) lies in direction
-// (s, t) = (R1.X / z, R2.X / z) at depth z = R0.X.  Per frame and view the staging kernel
-// projects every leaf box (a box entirely in front: the bounding rectangle of its corners'
+// (s, t) = (R1.X / z, R2.X / z) at depth z = R0.X.  Per frame and view one workgroup of
+// k_trace (the launch's first ones, before they stage the mesh) projects every leaf box (a box entirely in front: the bounding rectangle of its corners'
 // (s, t), rounded outward with a relative margin of 2^-18; anything else: every direction)
-// and sorts the leaves by their distance from the view point.  A packet then scans the
+// and sorts the leaves by their distance from the view point, then publishes the table
+// (ViewHead::tag = WorkArgs::view_tag, an agent-scope release); until a wave has seen the
+// tag it walks the BVH, so no wave ever waits for a table.  A packet then scans the
 // table instead of walking the BVH: a leaf is tested when some live lane's direction lies
 // in its rectangle and the leaf is not farther than that lane's depth bound; the scan stops
 // at the first leaf farther than every live lane's bound.  Exact for the reason the block
 // frustum pre-test is: a hit lies in its inflated leaf box, so its direction from the view
-// point lies in the box's projection (DESIGN.md §4.9).
+// point lies in the box's projection (DESIGN.md §4.8).
 struct ViewLeaf {
     float s0, s1, t0, t1;  // rectangle of directions (every direction: -inf, inf, -inf, inf)
     float dmin;            // distance from the view point to the box, rounded down (+inf: never met)
@@ -121,11 +123,13 @@ struct ViewLeaf {
     uint32_t pad[2];
 };
 constexpr uint32_t kMaxViewLeaves = 512;  // meshes with more leaves walk the BVH
+constexpr uint32_t kMaxViewTables = 16;   // frames x views per launch (more: the BVH walk)
 // One view of one frame: 0 = the camera, 1 + l = light l.  ok = 0: no table (walk the BVH).
 struct ViewHead {
-    uint32_t ok;
+    uint32_t ok;           // the table is usable (0: view point out of range, basis degenerate)
     float near_r;          // light views: leaves within this distance of the light are always tested
-    uint32_t pad[2];
+    uint32_t tag;          // WorkArgs::view_tag of the launch that built it (written last, release)
+    uint32_t pad;
     double R[3][3];        // the view's projection rows
     double O[3];           // the view point, object space
 };
@@ -282,10 +286,12 @@ struct WorkArgs {
     uint32_t nblocks_frame;  // nblocks = nframes * nblocks_frame; the table describes one frame
     // view tables (k_trace, one-object frames, nullptr: none): frame f, view v at
     // views + (f * nviews + v) * nleaves, its header at view_heads[f * nviews + v]
-    const ViewLeaf* views;
-    const ViewHead* view_heads;
+    ViewLeaf* views;
+    ViewHead* view_heads;
     uint32_t nviews;         // 1 + lights
     uint32_t view_leaves;    // leaves per table
+    uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
+    uint32_t view_pad;
 };
 constexpr int kTimelineRec = 8;
 // WorkArgs::dynamic: kernels whose waves take work items dynamically (primary: LDS tickets
@@ -305,8 +311,7 @@ struct RayIO {
     uint32_t n;
 };
 
-hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s,
-                               ViewLeaf* views = nullptr, ViewHead* heads = nullptr, uint32_t nviews = 0);
+hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s);
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
