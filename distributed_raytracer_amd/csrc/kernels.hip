@@ -1842,12 +1842,19 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
 // The launch's frame records, read through the constant address space: the kernel never
 // writes them, so their loads stay scalar and are not repeated after the kernel's stores.
 typedef const __attribute__((address_space(4))) FrameRec ConstFrameRec;
-__device__ __forceinline__ const FrameRec& frame_rec(const WorkArgs& wa, uint32_t f) {
-    return *(const FrameRec*)((ConstFrameRec*)wa.frames + f);
+__device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uint32_t f) {
+    return *(const FrameRec*)((ConstFrameRec*)frames + f);
 }
 
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+// rec: frame 0's record (a kernel argument); a launch of several frames reads them all from
+// WorkArgs::frames (staged by k_stage_frames), a one-frame launch (frames == nullptr) from rec.
+MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
+    const FrameArgs& fa = rec.fa;
+    // (rec is the first kernel argument: offset 0 of the kernarg segment; taking &rec would
+    // copy it to scratch)
+    const FrameRec* const frames =
+        wa.frames ? wa.frames : (const FrameRec*)(ConstFrameRec*)__builtin_amdgcn_kernarg_segment_ptr();
     double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ uint32_t wstk[kWG / 64][(MIRT_PRIMARY_WIDE || MIRT_SHADOW_WIDE) ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
@@ -1869,14 +1876,14 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
     const uint32_t NF = wa.nframes, nbf = wa.nblocks_frame;  // the host checks NF <= kMaxFrames
     const bool use_frustum = !BRUTE && MIRT_BLOCK_FRUSTUM && wa.fr.on;  // same for every frame (host)
     if (use_frustum && threadIdx.x < 8 * NF) {
-        const float* r = wa.frames[threadIdx.x >> 3].fr.rect[threadIdx.x & 7];
+        const float* r = frame_rec(frames, threadIdx.x >> 3).fr.rect[threadIdx.x & 7];
         frect[threadIdx.x >> 3][threadIdx.x & 7] = make_float4(r[0], r[1], r[2], r[3]);
     }
     if (RESIDENT && threadIdx.x < kMaxViewTables) s_vstate[threadIdx.x] = 0;  // read after the batch barrier
     if (RESIDENT && wa.views && blockIdx.x < NF * wa.nviews) {
         // the launch's first workgroups build the view tables in the mesh's LDS, then stage it
         const uint32_t q = blockIdx.x, f = q / wa.nviews;
-        build_view(frame_rec(wa, f), q - f * wa.nviews, wa.views + (size_t)q * wa.view_leaves, wa.view_heads + q, lds,
+        build_view(frame_rec(frames, f), q - f * wa.nviews, wa.views + (size_t)q * wa.view_leaves, wa.view_heads + q, lds,
                    wa.view_tag);
         __syncthreads();
     }
@@ -1921,10 +1928,10 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
             ready[t] = 0;
             // FrameRec::live: a block with no pixel in the frame's live rectangle is not queued
             const uint32_t px = v[1] & 0xffffu, py = v[1] >> 16, vw = (v[2] >> 16) & 0xffu, vh = v[2] >> 24;
-            const uint32_t* lv = wa.frames[f].live;
+            const uint32_t* lv = frame_rec(frames, f).live;
             if (!(px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1])) continue;
             bool culled = false;
-            if (classify) culled = !block_may_meet(wa.frames[f].fr, frect[f], px, py, vw, vh);
+            if (classify) culled = !block_may_meet(frame_rec(frames, f).fr, frect[f], px, py, vw, vh);
             // queue: blocks that may meet the object from the front, culled ones from the back
             const uint32_t slot = (partition && culled) ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
             bq[slot][0] = v[0];
@@ -1956,7 +1963,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                 ic.start();
                 const WaveStats before = wsh;
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
-                const FrameRec& fr = frame_rec(wa, cf);
+                const FrameRec& fr = frame_rec(frames, cf);
                 shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
                                               wsh, RESIDENT ? cf : ~0u, &vc);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
@@ -1977,7 +1984,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameArgs fa, const WorkArgs wa, OutPlanes 
                     const WaveStats before = wp;
                     const uint64_t ph0 = pc.acc[0], ph1 = pc.acc[1];
                     const uint32_t f = __builtin_amdgcn_readfirstlane(bq_frame[t]);
-                    const FrameRec& fr = frame_rec(wa, f);
+                    const FrameRec& fr = frame_rec(frames, f);
                     lc.frame = f;
                     // the camera's view table of this frame, once published (and usable)
                     const ViewLeaf* vt = nullptr;
@@ -2320,11 +2327,12 @@ hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
     return hipGetLastError();
 }
 
-hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint32_t opts,
                         hipStream_t s) {
+    const FrameArgs& fa = rec.fa;
     const bool resident = is_resident(fa);
     const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0) : 0;
-#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
+#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, rec, wa)
     MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE
     return hipGetLastError();

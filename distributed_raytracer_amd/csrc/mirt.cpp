@@ -659,11 +659,12 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             wa.nviews = nviews;
             wa.view_leaves = m0.nleaves;
         }
-        HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
-        wa.frames = sl->d_frames;
+        // one frame: its record travels as k_trace's argument (no staging kernel ahead of it)
+        if (nf > 1) HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
+        wa.frames = nf > 1 ? sl->d_frames : nullptr;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
-        HIP_TRY(launch_trace(fa, wa, out, pgrid, c->flags, s));
+        HIP_TRY(launch_trace(sl->h_frames[0], wa, pgrid, c->flags, s));
         HT(3);
         if (prof) {
             HIP_TRY(hipEventRecord(pr.ev[1], s));
@@ -1533,9 +1534,10 @@ struct mirt_group {
     uint32_t bbounces = 0;
     std::vector<BatchRec> binfo;        // per batch slot
     std::vector<uint64_t> slot_frame;   // per frame slot: the frame it holds (~0: none)
-    // per frame slot: columns [dirty0, dirty1) may hold non-miss pixels (whole-screen planes);
-    // a narrow frame refills only those before it traces its hit rectangle
-    std::vector<uint32_t> dirty0, dirty1;
+    // per frame slot: only [dirty0, dirty1) x [dirty_y0, dirty_y1) may hold non-miss pixels
+    // (whole-screen planes); a narrow frame refills those columns before it traces its hit
+    // rectangle, unless the rectangle covers them (the trace rewrites every pixel in it)
+    std::vector<uint32_t> dirty0, dirty1, dirty_y0, dirty_y1;
     std::vector<uint64_t> slot_bad;     // per frame slot: deal indices whose transfer failed
     // fault handling (master/pool/pool.go:224-260, master/main.go:111-161)
     uint32_t timeout_ms = 0;
@@ -2031,6 +2033,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->slot_bad.assign(inflight, 0);
     g->dirty0.assign(inflight, 0);  // the planes' first contents are unknown: the whole screen
     g->dirty1.assign(inflight, W);
+    g->dirty_y0.assign(inflight, 0);
+    g->dirty_y1.assign(inflight, H);
     if (is_root && fbs) {
         for (uint32_t j = 0; j < inflight; ++j)
             g->fb.push_back(OutPlanes{fbs[j].rgb, fbs[j].rgb8, fbs[j].valid, fbs[j].face, fbs[j].object, fbs[j].rgbv});
@@ -2273,16 +2277,21 @@ static int group_flush(mirt_group* g) {
             if (!narrow[i]) {  // traced whole: every pixel is written
                 g->dirty0[j] = 0;
                 g->dirty1[j] = g->W;
+                g->dirty_y0[j] = 0;
+                g->dirty_y1[j] = g->H;
                 continue;
             }
             // Only columns an earlier frame of this slot may have hit can hold anything but miss
             // values (the trace writes every pixel of the blocks meeting this frame's rectangle,
             // and hit pixels lie inside it): refill those columns, whole 16-byte words (extra
             // bytes of neighbouring columns get the miss value they already hold).
-            const uint32_t d0 = g->dirty0[j], d1 = g->dirty1[j];
+            const uint32_t d0 = g->dirty0[j], d1 = g->dirty1[j], e0 = g->dirty_y0[j], e1 = g->dirty_y1[j];
             g->dirty0[j] = R[0];
             g->dirty1[j] = R[2];
-            if (d1 <= d0) continue;
+            g->dirty_y0[j] = R[1];
+            g->dirty_y1[j] = R[3];
+            if (d1 <= d0 || e1 <= e0) continue;
+            if (R[0] <= d0 && d1 <= R[2] && R[1] <= e0 && e1 <= R[3]) continue;  // rewritten by this trace
             const OutPlanes& o = g->fb[j];
             const struct { void* p; uint64_t e; uint8_t v; } planes[kFillPlanes] = {
                 {o.rgb, 24, 0}, {o.rgb8, 3, 0}, {o.valid, 1, 0}, {o.face, 4, 0xff}, {o.object, 4, 0xff}, {o.rgbv, 4, 0}};

@@ -60,7 +60,7 @@ constexpr uint32_t kBvhEmpty = 0xffffffffu;
 constexpr uint32_t kBvhLeafBit = 0x80000000u;
 constexpr int kBvhCountShift = 24;
 constexpr uint32_t kBvhFirstMask = 0x00ffffffu;
-constexpr int kBvhLeaf = 4;           // max triangles per leaf
+constexpr int kBvhLeaf = 3;           // max triangles per leaf (2: +0%, 4: +2.6% frame interval)
 constexpr int kBvhStack = 128;        // per-wave traversal stack entries (two VGPRs / LDS)
 constexpr int kBvhMaxDepth = (kBvhStack - 1) / 7;
 // A traversal pushes every entered child (leaves too): at most 7 per inner level plus the
@@ -316,7 +316,7 @@ hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                          hipStream_t s);
-hipError_t launch_trace(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint32_t opts,
                         hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
