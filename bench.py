@@ -449,6 +449,16 @@ def main():
                          "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
                          "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(prim_ms, 4)},
         }
+        # north_star's own target: the brute-force work, bytes/tri-test x tris
+        # x rays, over the frame interval, against >= 40% of the per-GPU HBM roofline.  Culling
+        # makes this an "effective" rate far above the physical peak; `roofline` above counts the
+        # tests actually performed and `roofs` the physical limits.
+        bf_bytes = BYTES_PER_TRI_TEST * float(tris) * rays_per_frame
+        line["north_star_target"] = {
+            "definition": "72 B x triangles x rays per frame (brute-force equivalent) / device ms per frame",
+            "effective_tb_s": round(bf_bytes / (dev_ms / 1e3) / 1e12, 1),
+            "frac_of_hbm": round(bf_bytes / (dev_ms / 1e3) / 1e9 / (HBM_PEAK_GBS * world), 2),
+            "target_frac": 0.40, "met": bool(bf_bytes / (dev_ms / 1e3) / 1e9 >= 0.40 * HBM_PEAK_GBS * world)}
         if pj:
             # physical roofs over the frame interval (counters of this exact command, profiles/)
             per_frame = lambda x: x / pj["frames_per_launch"]  # noqa: E731
