@@ -268,7 +268,8 @@ struct Visits {
 // in LDS and one lane of the workgroup adds the sums into shard blockIdx % kStatShards:
 // one atomic per statistic per workgroup (see the counter layout in mirt_internal.hpp).
 struct WaveStats {
-    cnt_t tests, nodes, leaves, hits, overflow;
+    cnt_t tests;                               // lane tests: can pass 2^32 per wave (brute force)
+    uint32_t nodes, leaves, hits, overflow;    // wave-level counts (fewer live SGPRs)
 };
 // MIRT_PHASE_TIMING (diagnostic builds only): shader-clock cycles per phase of the primary
 // blocks, reported in the timeline record instead of the wave's start/end clocks.
@@ -1846,9 +1847,11 @@ __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uin
     return *(const FrameRec*)((ConstFrameRec*)frames + f);
 }
 
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 // rec: frame 0's record (a kernel argument); a launch of several frames reads them all from
 // WorkArgs::frames (staged by k_stage_frames), a one-frame launch (frames == nullptr) from rec.
+// VIEWS: the instantiation that uses view tables (MIRT_OPT_VIEWS); the default one has no
+// view code at all (present, it cost 6 spilled VGPRs and 1.7% of the frame interval).
+template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
 MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     const FrameArgs& fa = rec.fa;
     // (rec is the first kernel argument: offset 0 of the kernarg segment; taking &rec would
@@ -1865,8 +1868,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
     __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
-    __shared__ ViewHead s_vhead[RESIDENT ? kMaxViewTables : 1];
-    __shared__ uint32_t s_vstate[RESIDENT ? kMaxViewTables : 1];
+    __shared__ ViewHead s_vhead[VIEWS ? kMaxViewTables : 1];
+    __shared__ uint32_t s_vstate[VIEWS ? kMaxViewTables : 1];
     const ViewCache vc{s_vhead, s_vstate};
     const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
     WaveClock clock;
@@ -1879,8 +1882,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
         const float* r = frame_rec(frames, threadIdx.x >> 3).fr.rect[threadIdx.x & 7];
         frect[threadIdx.x >> 3][threadIdx.x & 7] = make_float4(r[0], r[1], r[2], r[3]);
     }
-    if (RESIDENT && threadIdx.x < kMaxViewTables) s_vstate[threadIdx.x] = 0;  // read after the batch barrier
-    if (RESIDENT && wa.views && blockIdx.x < NF * wa.nviews) {
+    if (VIEWS && threadIdx.x < kMaxViewTables) s_vstate[threadIdx.x] = 0;  // read after the batch barrier
+    if (VIEWS && RESIDENT && wa.views && blockIdx.x < NF * wa.nviews) {
         // the launch's first workgroups build the view tables in the mesh's LDS, then stage it
         const uint32_t q = blockIdx.x, f = q / wa.nviews;
         build_view(frame_rec(frames, f), q - f * wa.nviews, wa.views + (size_t)q * wa.view_leaves, wa.view_heads + q, lds,
@@ -1965,7 +1968,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
                 const FrameRec& fr = frame_rec(frames, cf);
                 shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
-                                              wsh, RESIDENT ? cf : ~0u, &vc);
+                                              wsh, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -1988,7 +1991,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                     lc.frame = f;
                     // the camera's view table of this frame, once published (and usable)
                     const ViewLeaf* vt = nullptr;
-                    if (RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
+                    if (VIEWS && RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
                                                            use_frustum, frect[f], &lc,
@@ -2141,7 +2144,7 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
         }
     }
     // reflection rays and their shadow rays as two extra statistics (per workgroup)
-    WaveStats extra{refl_rays, refl_shadow, 0, 0, 0};
+    WaveStats extra{refl_rays, (uint32_t)refl_shadow, 0, 0, 0};  // per wave: well below 2^32
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     __syncthreads();
     stats_flush(wa.counters, red, kStatReflRays, kStatReflShadowRays, -1, -1, extra);
@@ -2333,7 +2336,10 @@ hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint3
     const bool resident = is_resident(fa);
     const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0) : 0;
 #define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, rec, wa)
-    MIRT_DISPATCH(K_TRACE);
+    if (wa.views && resident && !(opts & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)))
+        hipLaunchKernelGGL((k_trace<true, false, true, true>), dim3(grid), dim3(kWG), dyn, s, rec, wa);
+    else
+        MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE
     return hipGetLastError();
 }

@@ -640,7 +640,8 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         // per-view leaf tables (MIRT_OPT_VIEWS; one-object frames with an LDS-resident mesh):
         // built by k_trace's first workgroups, one per (frame, view)
         const DevMesh& m0 = fa.obj[0].m;
-        const bool views = fa.n_objects == 1 && (c->flags & MIRT_OPT_VIEWS) && !(c->flags & MIRT_OPT_BRUTE_FORCE) &&
+        const bool views = fa.n_objects == 1 && (c->flags & MIRT_OPT_VIEWS) &&
+                           !(c->flags & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)) &&
                            m0.ntri <= (uint32_t)kLdsTris && m0.depth <= (uint32_t)kBvhShallowDepth &&
                            m0.nleaves > 0 && m0.nleaves <= kMaxViewLeaves && m0.leaves;
         uint32_t nviews = 0;
