@@ -1797,7 +1797,8 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
     __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
     // segment query for one-object frames (BVH kernels only; brute force stays literal)
-    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    // RESIDENT implies one object and no MIRT_OPT_NO_SEGMENT (is_resident): a constant there
+    const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
     WaveClock clock;
     uint32_t taken = 0;
     if (RESIDENT) {
@@ -1871,7 +1872,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __shared__ ViewHead s_vhead[VIEWS ? kMaxViewTables : 1];
     __shared__ uint32_t s_vstate[VIEWS ? kMaxViewTables : 1];
     const ViewCache vc{s_vhead, s_vstate};
-    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    // RESIDENT implies one object and no MIRT_OPT_NO_SEGMENT (is_resident): a constant there
+    const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
     WaveClock clock;
     uint32_t taken = 0;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
@@ -2042,7 +2044,8 @@ template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ cnt_t red[kWG / 64][4];
-    const bool segment = !BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT);
+    // RESIDENT implies one object and no MIRT_OPT_NO_SEGMENT (is_resident): a constant there
+    const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
     if (RESIDENT) {
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
@@ -2284,9 +2287,11 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
         }                                                                                          \
     } while (0)
 
+// (the MIRT_OPT_NO_SEGMENT ablation runs the general kernels, so the resident ones carry
+// only the segment query for shadow rays)
 static bool is_resident(const FrameArgs& fa) {
     return MIRT_LDS_MESH && fa.n_objects == 1 && fa.obj[0].m.ntri <= (uint32_t)kLdsTris &&
-           fa.obj[0].m.depth <= (uint32_t)kBvhShallowDepth;
+           fa.obj[0].m.depth <= (uint32_t)kBvhShallowDepth && !(fa.flags & MIRT_OPT_NO_SEGMENT);
 }
 // dynamic LDS bytes of a RESIDENT launch: the mesh
 static size_t mesh_lds_bytes(const FrameArgs& fa) { return (size_t)fa.obj[0].m.ntri * kTriD * sizeof(double); }
