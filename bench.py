@@ -220,10 +220,14 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
+        # a collective that never completes (a rank that died before joining) fails the run
+        # after MIRT_DIST_TIMEOUT_S instead of hanging it
+        import datetime
+        to = datetime.timedelta(seconds=int(os.environ.get("MIRT_DIST_TIMEOUT_S", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=to)
 
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd.framebuffer import FrameSharder, NativeFrameGroup
