@@ -120,6 +120,40 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
             if (t_certainly_negative(nt, inc)) return false;
         }
         diag(DG + 1);
+        if (PREFILTER) {
+            // Divide-free classification of the barycentric conditions:
+            // with q2 = n2/inc, q3 = n3/inc exact, q2, q3 >= 2^-40 and q2 + q3 <= 1 - 2^-40
+            // make every rounded condition hold; q3 < -2^-40 or q2 + q3 > 1 + 2^-40 (q2 is
+            // within [-2^-1000, 1 + 2^-51] past the pre-reject) make one fail.  Only lanes in
+            // neither case take the divides.  |inc| >= 2^-900 keeps 2^-40 |inc| exact; an
+            // infinite n3 or sum decides correctly, an overflowing bound only stays undecided,
+            // and NaN lands in neither case.
+            const double n3 = dot(e1, cross(p1or, neg));
+            const double ai = __builtin_fabs(inc);
+            const double p2 = inc < 0.0 ? -n2 : n2, p3 = inc < 0.0 ? -n3 : n3;
+            const double m = 0x1p-40 * ai, sum = p2 + p3;
+            const bool sane = ai >= 0x1p-900;
+            const bool in = sane && p2 >= m && p3 >= m && sum <= ai - 0x1p-39 * ai;
+            const bool out = sane && (p3 < -m || sum > ai + 0x1p-39 * ai);
+            if (out) return false;
+            if (!in) {  // tracer.go / triangle.go:50-66 as written
+                diag(DG + 2);
+                const double r2 = n2 / inc;
+                if (!(0.0 <= r2 && r2 <= 1.0)) return false;
+                const double r3 = n3 / inc;
+                if (!(0.0 <= r2 + r3 && r2 + r3 <= 1.0)) return false;
+                const double r1 = 1.0 - r2 - r3;
+                if (!(r1 >= 0.0 && r2 >= 0.0 && r3 >= 0.0)) return false;
+            }
+            diag(DG + 3);
+            const double t = (TPRE ? nt : dot(e1, cross(e2, p1or))) / inc;
+            if (t >= 0.0) {
+                diag(DG + 4);
+                t_out = t;
+                return true;
+            }
+            return false;
+        }
         double r2 = n2 / inc;
         if (0.0 <= r2 && r2 <= 1.0) {
             diag(DG + 2);
@@ -128,7 +162,7 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
                 double r1 = 1.0 - r2 - r3;
                 if (r1 >= 0.0 && r2 >= 0.0 && r3 >= 0.0) {
                     diag(DG + 3);
-                    double t = (PREFILTER && TPRE ? nt : dot(e1, cross(e2, p1or))) / inc;
+                    double t = dot(e1, cross(e2, p1or)) / inc;
                     if (t >= 0.0) {
                         diag(DG + 4);
                         t_out = t;

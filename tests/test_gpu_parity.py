@@ -680,3 +680,46 @@ def test_near_coplanar_and_subnormal_direction_rays(ctx, env, py_scene):
                     "the culled walk differs on a ray whose reference hit is finite (or absent)"
     finally:
         ctx.set_options(0)
+
+
+@pytest.mark.gpu
+def test_rays_at_triangle_edges_and_vertices(ctx, env, py_scene):
+    """The divide-free classification of the barycentric conditions on the
+    rays it must leave undecided: rays aimed exactly at vertices, edge midpoints and points
+    1e-15 .. 1e-9 (relative) inside and outside edges, from random origins (primary-like)
+    and from just above the surface (shadow-like).  Default kernel, MIRT_OPT_NO_PREFILTER
+    (the reference's divides for every lane) and brute force all equal the oracle."""
+    import distributed_raytracer_amd as rt
+    import distributed_raytracer_amd._lib as L
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(31)
+    m = py_scene.meshes[0]
+    pos = np.array(py_scene.objects[0][1])
+    V = np.asarray(m.vertices, np.float64).reshape(-1, 3)[np.asarray(m.face_v).reshape(-1, 3)] + pos
+    faces = rng.choice(len(V), 200, replace=False)
+    P1, P2, P3 = V[faces, 0], V[faces, 1], V[faces, 2]
+    C = (P1 + P2 + P3) / 3
+    targets = [P1, P2, P3, (P1 + P2) / 2, (P2 + P3) / 2, (P3 + P1) / 2]
+    for eps in (1e-15, 1e-12, 1e-9):
+        M = (P1 + P2) / 2
+        targets += [M + (C - M) * eps, M - (C - M) * eps]
+    T = np.concatenate(targets)
+    n = np.cross(P2 - P1, P3 - P1)
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    N = np.tile(n, (len(targets), 1))
+    far = T + rng.normal(size=T.shape) * 3.0
+    near = T + N * 1e-3 + rng.normal(size=T.shape) * 1e-3
+    origins = np.concatenate([far, near])
+    dirs = np.concatenate([T, T]) - origins
+    dirs /= np.linalg.norm(dirs, axis=1)[:, None]
+    ref = Oracle(py_scene, use_rtree=False).trace_rays(origins, dirs)
+    assert ref["ok"].sum() > len(origins) // 2
+    try:
+        for opts in (0, L.MIRT_OPT_NO_PREFILTER, L.MIRT_OPT_BRUTE_FORCE):
+            ctx.set_options(opts)
+            got = rt.trace_rays(origins, dirs, env)
+            for k in ("ok", "face"):
+                assert np.array_equal(got[k], ref[k]), (opts, k, int((got[k] != ref[k]).sum()))
+            assert np.array_equal(got["hit"], ref["hit"], equal_nan=True), opts
+    finally:
+        ctx.set_options(0)

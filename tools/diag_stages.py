@@ -25,8 +25,10 @@ def main():
     g.wait()
     torch.cuda.synchronize()
     c = ctx.debug_counters() / n
-    names = ["tests", "past r2 pre-reject", "past r2 range", "past r3 checks", "hits", "node visits", "leaves",
-             "reach t pre-test"]
+    # stage 2: waves with a lane the divide-free classification leaves undecided (they run the
+    # r2 / r3 divides); stage 3: waves with a lane inside the triangle (they run the t divide)
+    names = ["tests", "past the pre-rejects", "take the r2/r3 divides", "inside (t divide)", "hits", "node visits",
+             "leaves", "reach t pre-test"]
     for base, kind in ((0, "primary"), (8, "shadow")):
         print(kind, "  ".join(f"{nm}={c[base + i]:.0f}" for i, nm in enumerate(names)))
     print("k_trace: ready-wait spins", c[17], " idle spins", c[18], " shadow items", c[19], " primary blocks", c[20],
