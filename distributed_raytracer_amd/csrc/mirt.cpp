@@ -67,7 +67,7 @@ struct MeshDev {
 // printed when the group is destroyed (tools/group_probe.py with MIRT_LIB).
 #ifdef MIRT_HOST_TIMERS
 #include <chrono>
-static double g_ht[8];
+static double g_ht[16];
 static std::chrono::steady_clock::time_point g_ht_t;
 #define HT_START() (g_ht_t = std::chrono::steady_clock::now())
 #define HT(i)                                                                                   \
@@ -554,6 +554,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     const FrameArgs& fa = sl->h_frames[0].fa;
     const OutPlanes out = sl->h_frames[0].out;
     if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
+    HT(9);
     uint64_t pixels = 0;
     for (uint32_t t = 0; t < n; ++t) pixels += (uint64_t)tiles[t].w * tiles[t].h;
     const uint32_t nl = fa.n_lights;
@@ -661,7 +662,9 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             wa.view_leaves = m0.nleaves;
         }
         // one frame: its record travels as k_trace's argument (no staging kernel ahead of it)
+        HT(10);
         if (nf > 1) HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
+        HT(11);
         wa.frames = nf > 1 ? sl->d_frames : nullptr;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
@@ -1925,8 +1928,10 @@ int mirt_group_unique_id(uint8_t* id) {
 void mirt_group_destroy(mirt_group* g) {
     if (!g) return;
 #ifdef MIRT_HOST_TIMERS
-    fprintf(stderr, "host_timers_us_per_frame wait %.2f record %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f\n",
-            g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k);
+    fprintf(stderr, "host_timers_us_per_frame wait %.2f record %.2f prep %.2f launch %.2f post+gather %.2f unpack %.2f done %.2f"
+                    " | hit_rect %.2f fill %.2f blocks %.2f setup %.2f stage %.2f\n",
+            g_ht[0] / g->k, g_ht[1] / g->k, g_ht[2] / g->k, g_ht[3] / g->k, g_ht[4] / g->k, g_ht[5] / g->k, g_ht[6] / g->k,
+            g_ht[7] / g->k, g_ht[8] / g->k, g_ht[9] / g->k, g_ht[10] / g->k, g_ht[11] / g->k);
 #endif
     (void)hipSetDevice(g->c->device);
     if (g->comm) {
@@ -2249,6 +2254,7 @@ static int group_flush(mirt_group* g) {
         memcpy(jobs.rect[i], br.rect[i], sizeof(jobs.rect[i]));
         jobs.tag[i] = transfer_tag(br.first + i);
     }
+    HT(7);
     // a sender reuses its packed planes only after their previous batch's sends are done (the
     // root's stream already waited for that gather before its unpacks)
     if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
@@ -2310,6 +2316,7 @@ static int group_flush(mirt_group* g) {
         }
         if (fill_max) HIP_TRY(launch_fill_planes(fj, n, fill_max, s));
     }
+    HT(8);
     for (Share& sh : g->shares) {
         Slot* sl = sh.slots[bs].get();
         for (uint32_t i = 0; i < n; ++i) {
