@@ -7,7 +7,8 @@
 // the rounding error of the fp64 Möller–Trumbore test and of the fp32 slab test that
 // reads it.
 //
-// Build: binned SAH (16 bins on centroids, longest axis) into a binary tree with leaves
+// Build: SAH on all three axes (an exact sweep for nodes of <= 256 faces, else 32 bins on
+// centroids) into a binary tree with leaves
 // of <= kBvhLeaf faces, then collapse to 8-wide nodes by repeatedly opening the child
 // with the largest surface area.  Faces are reordered so that every leaf is one
 // contiguous range.
@@ -82,38 +83,80 @@ struct Builder {
             nodes[idx].count = cnt;
             return idx;
         }
+        // SAH split on every axis: an exact sweep over the sorted centroids for up to
+        // kSweep faces, else 32 bins on the centroid extent
         int axis = 0;
         for (int k = 1; k < 3; ++k)
             if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
         uint32_t mid = begin + cnt / 2;
-        const double ext = cb.hi[axis] - cb.lo[axis];
-        if (ext > 0) {
-            constexpr int B = 16;
-            Box bb[B];
-            uint32_t bc[B] = {0};
-            auto bin = [&](uint32_t f) {
-                int b = (int)((ce[f][axis] - cb.lo[axis]) / ext * B);
-                return std::min(B - 1, std::max(0, b));
-            };
-            for (uint32_t i = begin; i < end; ++i) {
-                int b = bin(order[i]);
-                bb[b].grow(fbox[order[i]]);
-                bc[b]++;
+        double best = INFINITY;
+        int best_axis = -1;
+        uint32_t best_cut = 0;   // sweep: faces left of the cut; bins: first bin on the right
+        constexpr uint32_t kSweep = 256;
+        constexpr int B = 32;
+        std::vector<uint32_t> tmp;
+        std::vector<double> rarea;
+        for (int a = 0; a < 3; ++a) {
+            const double ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0)) continue;
+            if (cnt <= kSweep) {
+                tmp.assign(order.begin() + begin, order.begin() + end);
+                std::sort(tmp.begin(), tmp.end(), [&](uint32_t x, uint32_t y) {
+                    return ce[x][a] < ce[y][a] || (ce[x][a] == ce[y][a] && x < y);
+                });
+                rarea.assign(cnt + 1, 0.0);
+                Box r;
+                for (uint32_t i = cnt; i-- > 1;) {
+                    r.grow(fbox[tmp[i]]);
+                    rarea[i] = r.area();
+                }
+                Box l;
+                for (uint32_t i = 1; i < cnt; ++i) {
+                    l.grow(fbox[tmp[i - 1]]);
+                    const double cost = l.area() * i + rarea[i] * (cnt - i);
+                    if (cost < best) {
+                        best = cost;
+                        best_axis = a;
+                        best_cut = i;
+                    }
+                }
+            } else {
+                Box bb[B];
+                uint32_t bc[B] = {0};
+                for (uint32_t i = begin; i < end; ++i) {
+                    const uint32_t f = order[i];
+                    const int b = std::min(B - 1, std::max(0, (int)((ce[f][a] - cb.lo[a]) / ext * B)));
+                    bb[b].grow(fbox[f]);
+                    bc[b]++;
+                }
+                for (int sp = 1; sp < B; ++sp) {
+                    Box l, r;
+                    uint32_t nl = 0, nr = 0;
+                    for (int b = 0; b < sp; ++b) if (bc[b]) { l.grow(bb[b]); nl += bc[b]; }
+                    for (int b = sp; b < B; ++b) if (bc[b]) { r.grow(bb[b]); nr += bc[b]; }
+                    if (!nl || !nr) continue;
+                    const double cost = l.area() * nl + r.area() * nr;
+                    if (cost < best) {
+                        best = cost;
+                        best_axis = a;
+                        best_cut = (uint32_t)sp;
+                    }
+                }
             }
-            double best = INFINITY;
-            int best_split = -1;
-            for (int s = 1; s < B; ++s) {
-                Box l, r;
-                uint32_t nl = 0, nr = 0;
-                for (int b = 0; b < s; ++b) if (bc[b]) { l.grow(bb[b]); nl += bc[b]; }
-                for (int b = s; b < B; ++b) if (bc[b]) { r.grow(bb[b]); nr += bc[b]; }
-                if (!nl || !nr) continue;
-                double cost = l.area() * nl + r.area() * nr;
-                if (cost < best) { best = cost; best_split = s; }
-            }
-            if (best_split > 0) {
-                auto it = std::partition(order.begin() + begin, order.begin() + end,
-                                         [&](uint32_t f) { return bin(f) < best_split; });
+        }
+        if (best_axis >= 0) {
+            const int a = best_axis;
+            axis = a;
+            if (cnt <= kSweep) {
+                std::sort(order.begin() + begin, order.begin() + end, [&](uint32_t x, uint32_t y) {
+                    return ce[x][a] < ce[y][a] || (ce[x][a] == ce[y][a] && x < y);
+                });
+                mid = begin + best_cut;
+            } else {
+                const double ext = cb.hi[a] - cb.lo[a];
+                auto it = std::partition(order.begin() + begin, order.begin() + end, [&](uint32_t f) {
+                    return std::min(B - 1, std::max(0, (int)((ce[f][a] - cb.lo[a]) / ext * B))) < (int)best_cut;
+                });
                 mid = (uint32_t)(it - order.begin());
             }
         }
