@@ -723,3 +723,34 @@ def test_rays_at_triangle_edges_and_vertices(ctx, env, py_scene):
             assert np.array_equal(got["hit"], ref["hit"], equal_nan=True), opts
     finally:
         ctx.set_options(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inflight,batch", [(4, 1), (8, 2)])
+def test_1080p_frame_group_bench_path_matches_oracle(ctx, env, py_scene, inflight, batch):
+    """The bench's own path at configs[1] size: the native frame group (frames in flight,
+    `batch` frames per k_trace launch, host output on), every pixel of the D2H'd rgb8 and
+    valid planes and of the device fp64 rgb plane against the oracle, for the last frame
+    of a run long enough to reuse every frame slot."""
+    import torch
+    from oracle.oracle import Oracle
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W, H = 1920, 1080
+    ref = Oracle(py_scene, use_rtree=True).frame(W, H, nthreads=16)
+    fr = env.mutable().to_frame()
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=inflight, batch=batch, with_rgb=True, host_output=True)
+    try:
+        last = None
+        for _ in range(2 * inflight + 1):
+            last = g.render(fr)
+        g.wait()
+        g.flush()
+        torch.cuda.synchronize()
+        rgb8, valid = g.host_frame(last)
+        assert np.array_equal(valid, ref["valid"])
+        assert np.array_equal(rgb8, ref["rgb8"])
+        dev = g.frames[last % inflight]
+        assert np.array_equal(dev.rgb.cpu().numpy(), ref["rgb"])
+        assert int(valid.sum()) == 209584
+    finally:
+        g.close()
