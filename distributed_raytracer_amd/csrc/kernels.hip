@@ -1878,6 +1878,9 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
 // The launch's frame records, read through the constant address space: the kernel never
 // writes them, so their loads stay scalar and are not repeated after the kernel's stores.
 typedef const __attribute__((address_space(4))) FrameRec ConstFrameRec;
+// k_trace's arguments (frame 0's record, then the work description) must fit the 4 KB
+// kernarg segment; frame_rec finds the record at its offset 0.
+static_assert(sizeof(FrameRec) + sizeof(WorkArgs) <= 4096, "k_trace arguments exceed the kernarg segment");
 __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uint32_t f) {
     return *(const FrameRec*)((ConstFrameRec*)frames + f);
 }
