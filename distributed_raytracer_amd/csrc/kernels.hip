@@ -1473,6 +1473,9 @@ __device__ bool view_rows(const double F[3], const double L[3], const double U[3
 // (and, for a light, any box within near_r of it: a shadow segment ends 1e-4 past the light)
 // gets every direction.
 constexpr uint32_t kViewSort = kMaxViewLeaves;
+// k_trace's queue buckets: unknown cost, 8 log2 classes of the last primary trace time
+// (units of 64 shader cycles; >= 2^12, i.e. >= ~110 us, first), and the culled blocks.
+constexpr int kQueueBuckets = 10;
 struct ViewScratch {
     ViewLeaf tmp[kViewSort];
     float key[kViewSort];
@@ -1903,6 +1906,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __shared__ uint32_t bq[kBlkQ][3];
     __shared__ uint8_t bq_cull[kBlkQ];   // 1: the block frustum pre-test culled it at staging
     __shared__ uint8_t bq_frame[kBlkQ];  // the block's frame within the launch
+    __shared__ uint32_t bq_bl[kBlkQ];    // the block's index in the frame's table (WorkArgs::block_cost)
+    __shared__ uint32_t s_bucket[kQueueBuckets];
     __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
     __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
@@ -1958,29 +1963,65 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     if (classify) __syncthreads();  // the frustum rectangles are staged
     for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
         const uint32_t nc = min(mine - c0, (uint32_t)kBlkQ);
+        // Queue order, by buckets filled in one pass (nc <= kBlkQ <= kWG: one entry per
+        // thread): blocks that may meet the object before culled ones; with cost estimates
+        // (WorkArgs::block_cost) unknown ones first, then by their last primary trace time,
+        // longest first (log2 buckets), so the long single-wave chains start at once.
+        static_assert(kBlkQ <= kWG, "one queue entry per thread");
         if (threadIdx.x == 0) {
             s_front = 0;
-            s_back = nc;
+            s_back = nc;  // every queued block goes to [0, s_front)
         }
-        if (classify) __syncthreads();
-        for (uint32_t t = threadIdx.x; t < nc; t += kWG) {
+        if (threadIdx.x < kQueueBuckets) s_bucket[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t t = threadIdx.x;
+        uint32_t cls = ~0u, qbl = 0, qf = 0;
+        u32x4 qv{0u, 0u, 0u, 0u};
+        bool culled = false;
+        if (t < nc) {
             const uint32_t b = blockIdx.x + (c0 + t) * G;  // over every frame's blocks
-            const uint32_t f = b / nbf, bl = b - f * nbf;
-            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(bl % kQShards) * wa.per_shard + bl / kQShards];
+            qf = b / nbf;
+            qbl = b - qf * nbf;
+            qv = ((const u32x4*)wa.blocks)[(size_t)(qbl % kQShards) * wa.per_shard + qbl / kQShards];
             ready[t] = 0;
             // FrameRec::live: a block with no pixel in the frame's live rectangle is not queued
-            const uint32_t px = v[1] & 0xffffu, py = v[1] >> 16, vw = (v[2] >> 16) & 0xffu, vh = v[2] >> 24;
-            const uint32_t* lv = frame_rec(frames, f).live;
-            if (!(px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1])) continue;
-            bool culled = false;
-            if (classify) culled = !block_may_meet(frame_rec(frames, f).fr, frect[f], px, py, vw, vh);
-            // queue: blocks that may meet the object from the front, culled ones from the back
-            const uint32_t slot = (partition && culled) ? atomicSub(&s_back, 1u) - 1u : atomicAdd(&s_front, 1u);
-            bq[slot][0] = v[0];
-            bq[slot][1] = v[1];
-            bq[slot][2] = v[2];
+            const uint32_t px = qv[1] & 0xffffu, py = qv[1] >> 16, vw = (qv[2] >> 16) & 0xffu, vh = qv[2] >> 24;
+            const uint32_t* lv = frame_rec(frames, qf).live;
+            if (px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1]) {
+                if (classify) culled = !block_may_meet(frame_rec(frames, qf).fr, frect[qf], px, py, vw, vh);
+                if (!partition) {
+                    cls = 0;
+                } else if (culled) {
+                    cls = kQueueBuckets - 1;
+                } else if (wa.block_cost) {
+                    const uint32_t est = wa.block_cost[qbl];
+                    const int lg = est ? 31 - __builtin_clz(est) : 0;
+                    cls = est == 0 ? 0u : 1u + (uint32_t)min(kQueueBuckets - 3, max(0, 12 - lg));
+                } else {
+                    cls = 0;
+                }
+            }
+        }
+        if (cls != ~0u) atomicAdd(&s_bucket[cls], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int k = 0; k < kQueueBuckets; ++k) {
+                const uint32_t c = s_bucket[k];
+                s_bucket[k] = acc;
+                acc += c;
+            }
+            s_front = acc;
+        }
+        __syncthreads();
+        if (cls != ~0u) {
+            const uint32_t slot = atomicAdd(&s_bucket[cls], 1u);
+            bq_bl[slot] = qbl;
+            bq[slot][0] = qv[0];
+            bq[slot][1] = qv[1];
+            bq[slot][2] = qv[2];
             bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
-            bq_frame[slot] = (uint8_t)f;
+            bq_frame[slot] = (uint8_t)qf;
         }
         if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
         if (c0 == 0) clock.mark_staged();
@@ -2032,10 +2073,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                     const ViewLeaf* vt = nullptr;
                     if (VIEWS && RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
+                    const uint64_t cost0 = wa.block_cost ? __builtin_amdgcn_s_memtime() : 0;
                     primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
                                                            use_frustum, frect[f], &lc,
                                                            __builtin_amdgcn_readfirstlane(bq_cull[t]), vt, wa.view_leaves,
                                                            &fr.fr);
+                    if (wa.block_cost && (threadIdx.x & 63) == 0) {  // this trace's time, for the slot's next frame
+                        const uint64_t dc = (__builtin_amdgcn_s_memtime() - cost0) >> 6;
+                        wa.block_cost[bq_bl[t]] = (uint16_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));
+                    }
                     ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
                               (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
                     lds_inc(&s_pdone);  // after the block's chunk (if any) was allocated

@@ -96,6 +96,8 @@ struct Slot {
     size_t dir0_cap = 0;
     double* ph0 = nullptr;    // configs[4] reflections: phong of the primary hit per slot
     size_t ph0_cap = 0;
+    uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
+    size_t cost_cap = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
@@ -198,7 +200,7 @@ int slot_init(Slot* s) {
 void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0,
-                    (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
+                    (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
                     (void*)s->d_frames, (void*)s->views, (void*)s->view_heads})
         if (p) (void)hipFree(p);
     if (s->h_blocks) (void)hipHostFree(s->h_blocks);
@@ -594,6 +596,12 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         if ((r = dev_grow(sl->ph0, sl->ph0_cap, 3 * hit_slots)) != MIRT_OK) return r;
         wa.dir0 = sl->dir0;
         wa.ph0 = sl->ph0;
+    }
+    if (one_launch && !getenv("MIRT_NO_COST_ORDER")) {
+        const size_t cap0 = sl->cost_cap;
+        if ((r = dev_grow(sl->cost, sl->cost_cap, (size_t)sl->nblocks)) != MIRT_OK) return r;
+        if (sl->cost_cap != cap0) HIP_TRY(hipMemsetAsync(sl->cost, 0, sl->cost_cap * sizeof(uint16_t), s));
+        wa.block_cost = sl->cost;
     }
     wa.hits = sl->hits;
     wa.litw = sl->litw;

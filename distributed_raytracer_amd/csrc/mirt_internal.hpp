@@ -290,6 +290,10 @@ struct WorkArgs {
     ViewHead* view_heads;
     uint32_t nviews;         // 1 + lights
     uint32_t view_leaves;    // leaves per table
+    // k_trace's queue order: per block of the table, the primary trace time of its last
+    // frame on this slot (units of 64 shader cycles, 0 = unknown); blocks that took long go
+    // first (order only: every block is traced the same way)
+    uint16_t* block_cost;
     uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
     uint32_t view_pad;
 };
