@@ -532,15 +532,16 @@ class NativeFrameGroup:
         MirtError MIRT_E_PEER / MIRT_E_TIMEOUT naming the failed frame and ranks."""
         L.check(L.lib().mirt_group_wait(self._h, None))
 
-    def host_frame(self, index: int):
+    def host_frame(self, index: int, copy: bool = True):
         """(rgb8 (W*H, 3), valid (W*H,)) numpy copies of frame `index` from the group's
-        pinned host planes (host_output=True): the frame after its D2H."""
+        pinned host planes (host_output=True): the frame after its D2H.  copy=False: views
+        of the pinned planes, valid while host output stays off or the slot is not reused."""
         out = L.Outputs()
         L.check(L.lib().mirt_group_frame_host(self._h, int(index), C.byref(out)))
         n = self.W * self.H
-        rgb8 = np.ctypeslib.as_array(C.cast(out.rgb8, C.POINTER(C.c_uint8)), shape=(n * 3,)).reshape(n, 3).copy()
-        valid = np.ctypeslib.as_array(C.cast(out.valid, C.POINTER(C.c_uint8)), shape=(n,)).copy()
-        return rgb8, valid
+        rgb8 = np.ctypeslib.as_array(C.cast(out.rgb8, C.POINTER(C.c_uint8)), shape=(n * 3,)).reshape(n, 3)
+        valid = np.ctypeslib.as_array(C.cast(out.valid, C.POINTER(C.c_uint8)), shape=(n,))
+        return (rgb8.copy(), valid.copy()) if copy else (rgb8, valid)
 
     def set_host_output(self, enable: bool) -> None:
         """Copy frames enqueued from now on to pinned host memory (or stop)."""
