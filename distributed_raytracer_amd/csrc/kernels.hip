@@ -1238,6 +1238,16 @@ __device__ __forceinline__ uint32_t shard_items(uint32_t n, uint32_t q) {
 // ---------------------------------------------------------------- hit slots
 // A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.
 __device__ __forceinline__ void st64(uint64_t* p, uint64_t v) { *p = v; }
+// A miss's fp64 colour (three zeros), its zero made at the store: a zero hoisted out of the
+// block loops would stay live across the traversal, and k_trace spilled it to scratch.
+__device__ __forceinline__ void store_black(double* p) {
+    uint64_t z = 0;
+    asm volatile("" : "+v"(z));
+    uint64_t* q = (uint64_t*)p;
+    q[0] = z;
+    q[1] = z;
+    q[2] = z;
+}
 __device__ __forceinline__ uint64_t ld64(const uint64_t* p) { return *p; }
 __device__ __forceinline__ void st32(uint32_t* p, uint32_t v) { *p = v; }
 __device__ __forceinline__ double bitsd(uint64_t x) { return __longlong_as_double((long long)x); }
@@ -1324,11 +1334,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
             if (out.valid) out.valid[oidx] = 0;
             if (out.face) out.face[oidx] = -1;
             if (out.object) out.object[oidx] = -1;
-            if (out.rgb) {
-                out.rgb[3 * oidx] = 0.0;
-                out.rgb[3 * oidx + 1] = 0.0;
-                out.rgb[3 * oidx + 2] = 0.0;
-            }
+            if (out.rgb) store_black(out.rgb + 3 * oidx);
             if (out.rgb8) {
                 out.rgb8[3 * oidx] = 0;
                 out.rgb8[3 * oidx + 1] = 0;
@@ -1381,7 +1387,11 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         uint32_t base = 0;
         if (lane == 0) base = lc ? atomicAdd(lc->count, 1u) : atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
         base = __builtin_amdgcn_readfirstlane(base);
-        const size_t slot = lc ? lc->base + (size_t)base * 64 + lane : (size_t)q * wa.hit_cap + base + lane;
+        // (the lane offset made here: base + lane hoisted out of the block loop stays live
+        // across the traversal as a 64-bit pair, and k_trace spilled it to scratch)
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        const size_t slot = lc ? (size_t)(lc->base + (size_t)base * 64) + ln : (size_t)q * wa.hit_cap + base + lane;
         uint64_t* w = (uint64_t*)&wa.hits[slot];
         if (is_hit) {
             st64(w + 0, dbits(nh.hit.x));
@@ -1392,7 +1402,9 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
             st64(w + 5, dbits(nh.normal.z));
             st64(w + 6, oidx);
             st64(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
-            if (wa.bounces) vstore(wa.dir0 + 3 * slot, d);  // the reflect kernel's incoming D
+            // the reflect kernel's incoming D (reflection frames run the split kernels: k_trace,
+            // the caller with local chunks, never sees one, launch_frames)
+            if (!lc && wa.bounces) vstore(wa.dir0 + 3 * slot, d);
         } else {
             st64(w + 7, (uint64_t)kNoHit);
         }
@@ -1414,11 +1426,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
         if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
         if (!is_hit) {
-            if (out.rgb) {
-                out.rgb[3 * oidx] = 0.0;
-                out.rgb[3 * oidx + 1] = 0.0;
-                out.rgb[3 * oidx + 2] = 0.0;
-            }
+            if (out.rgb) store_black(out.rgb + 3 * oidx);
             if (out.rgb8) {
                 out.rgb8[3 * oidx] = 0;
                 out.rgb8[3 * oidx + 1] = 0;
