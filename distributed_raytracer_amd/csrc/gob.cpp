@@ -17,6 +17,7 @@
 // fieldType 21, []fieldType 22, mapType 23; user types from 65.
 #include "gob.hpp"
 
+#include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -132,6 +133,12 @@ struct Stream {
     int depth = 0;
 
     explicit Stream(const uint8_t* data, size_t n) : r{data, data + n} {}
+
+    // a negative type id introduces a definition; INT64_MIN has no positive counterpart
+    static int64_t defined_id(int64_t id) {
+        if (id == INT64_MIN) bad("gob type id out of range");
+        return -id;
+    }
 
     // --- type definitions: a wireType value (encoding/gob type.go wireType and its parts)
     void common(Reader& m, WireType& t) {  // CommonType{Name string; Id int}
@@ -286,7 +293,7 @@ struct Stream {
         if (v.bytes.empty()) return v;
         int64_t id = m.i();
         while (id < 0) {  // a type definition inside the value (encoding/gob decodeTypeSequence)
-            define(m, -id);
+            define(m, defined_id(id));
             if (!m.done()) (void)m.u();
             id = m.i();
         }
@@ -303,7 +310,7 @@ struct Stream {
             Reader m = r.sub(r.count());
             const int64_t id = m.i();
             if (id < 0) {
-                define(m, -id);
+                define(m, defined_id(id));
                 if (!m.done()) bad("extra data after a gob type definition");
                 continue;
             }

@@ -1784,8 +1784,6 @@ int group_plan(mirt_group* g) {
         HIP_TRY(hipMemcpy(g->d_regions, rd.data(), rd.size() * sizeof(RegionDesc), hipMemcpyHostToDevice));
         if (g->h_bad_cap < (size_t)g->F * P) {
             if (g->h_bad) (void)hipHostFree(g->h_bad);
-    if (g->d_spans) (void)hipFree(g->d_spans);
-    for (void* p : g->own) (void)hipFree(p);
             g->h_bad = nullptr;
             g->h_bad_cap = 0;
             HIP_TRY(hipHostMalloc((void**)&g->h_bad, (size_t)g->F * P));

@@ -474,7 +474,8 @@ class NativeFrameGroup:
 
     def __init__(self, ctx, W: int, H: int, rank: int = 0, world: int = 1, tile: Optional[int] = 8,
                  inflight: int = 4, group=None, with_rgb: bool = False, tile_h: Optional[int] = 0,
-                 batch: int = 1, emulate: int = 0, host_output: bool = False, timeout_ms: int = 0):
+                 batch: int = 1, emulate: int = 0, host_output: bool = False, timeout_ms: int = 0,
+                 library_planes: bool = False):
         import torch
         self.ctx, self.W, self.H, self.rank, self.world = ctx, W, H, rank, world
         self.F = max(1, int(inflight))
@@ -500,7 +501,10 @@ class NativeFrameGroup:
                 t.copy_(torch.frombuffer(bytearray(bytes(uid)), dtype=torch.uint8))
             dist.broadcast(t, src=0, group=group)
             uid = (C.c_uint8 * 128)(*t.cpu().tolist())
-        self.frames = [alloc_planes(W * H, self.device, with_rgb) for _ in range(self.F)] if rank == 0 else None
+        # library_planes: fbs == NULL, the group owns its rgb8 + valid planes (callers that read
+        # frames only through host_frame, like the C / Go workers)
+        self.frames = ([alloc_planes(W * H, self.device, with_rgb) for _ in range(self.F)]
+                       if rank == 0 and not library_planes else None)
         fbs = (L.Outputs * self.F)(*[p.outputs() for p in self.frames]) if self.frames else None
         self._h = C.c_void_p()
         L.check(L.lib().mirt_group_create(ctx.handle, C.cast(uid, C.c_void_p) if world > 1 else None, rank, world,

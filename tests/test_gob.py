@@ -124,6 +124,11 @@ def test_malformed_streams_fail_cleanly():
         huge = msg(G.enc_int(G.STRING) + b"\x00" + G.enc_uint(1 << 40))  # a count past the data
         assert gob_json(huge) == L.MIRT_E_IO
         assert gob_json(msg(G.enc_int(70) + b"\x00\x00")) == L.MIRT_E_IO  # undefined type id
+        # a type id of INT64_MIN (uint 2^64-1, zig-zag): a definition id with no positive
+        # counterpart, rejected before it is negated (top level and inside an interface)
+        assert gob_json(msg(bytes.fromhex("f8ffffffffffffffff") + b"\x00")) == L.MIRT_E_IO
+        iface = G.enc_int(G.INTERFACE) + b"\x00" + G.enc_uint(1) + b"X" + bytes.fromhex("f8ffffffffffffffff")
+        assert gob_json(msg(iface)) == L.MIRT_E_IO
     finally:
         L.lib().mirt_scene_free(env)
 

@@ -137,6 +137,39 @@ def test_host_output_frames(ctx, views, tile, emulate):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("emulate_after_host_output", [False, True])
+def test_library_owned_planes_host_output(ctx, views, emulate_after_host_output):
+    """fbs == NULL on a tiled root (the group allocates its own rgb8 + valid planes, as the
+    C / Go workers use it at N > 1) with host output on, and mirt_group_emulate called
+    before or after mirt_group_set_host_output: group_plan's buffer growth must not free the
+    group's own planes or the host-copy spans (a regression: it once did, and the unpack and
+    host copy then wrote freed memory).  Every host frame equals the oracle."""
+    from distributed_raytracer_amd import _lib as L
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    if emulate_after_host_output:
+        g = NativeFrameGroup(ctx, W, H, 0, 1, 8, inflight=2, batch=1, host_output=True, library_planes=True)
+        L.check(L.lib().mirt_group_emulate(g._h, 4))
+    else:
+        g = NativeFrameGroup(ctx, W, H, 0, 1, 8, inflight=2, batch=1, emulate=4, host_output=True,
+                             library_planes=True)
+    try:
+        assert g.frames is None
+        prev = None
+        for name in ORDER:
+            idx = g.render(views[name][0])
+            if prev is not None:
+                rgb8, valid = g.host_frame(prev[0])
+                _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+            prev = (idx, name)
+        rgb8, valid = g.host_frame(prev[0])
+        _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+        g.wait()
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 def test_peer_failure_is_named_and_redealt(ctx, views):
     """A rank that stops answering (emulated: its transfers are dropped) fails the frame
     with MIRT_E_PEER naming that rank — the master skips such frames, master/main.go:153-161
