@@ -60,9 +60,3 @@ func (em *EnvMutables) MirtObjects(e Environment) []MirtObject {
 	}
 	return out
 }
-
-// Mutable returns the environment's mutable part (for a worker that traces the scene it
-// registered with, before any diff arrived).
-func (e Environment) Mutable() *EnvMutables {
-	return e.mutable
-}

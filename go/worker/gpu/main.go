@@ -55,8 +55,12 @@ func (t *Tracer) BulkTrace(ctx context.Context, req *comms.WorkOrder) (*comms.Tr
 	width, height := int(req.GetWidth()), int(req.GetHeight())
 	results := &comms.TraceResults{Results: make([]*comms.TraceResults_Colour, width*height, width*height)}
 
-	// The frame's mutable state (main.go:57-65).  Without a diff the reference traces an
-	// empty EnvMutables (every pixel black); so does this worker.
+	// The frame's mutable state (main.go:57-65).  Without a diff the reference's pixel loop
+	// would call tracer.Trace on a zero EnvMutables, whose nil Objs R-tree tracer.go:32
+	// dereferences (a panic that ends the worker process; the master would then time the
+	// order out).  This worker answers such an order with black pixels instead: the one
+	// place where its behaviour differs, and only for an order no master sends
+	// (master/main.go:130-150 always attaches the frame's diff).
 	var diff state.EnvMutables
 	env := &diff
 	if req.GetDiff() != nil {

@@ -7,9 +7,15 @@
 // checks its frames bit for bit.
 package gpu
 
+// Where libmirt lives is the builder's environment, not this file's (INTEGRATION.md §cgo):
+//
+//	MIRT=/path/to/this/repo
+//	CGO_CFLAGS="-I$MIRT/include" \
+//	CGO_LDFLAGS="-L$MIRT/distributed_raytracer_amd -Wl,-rpath,$MIRT/distributed_raytracer_amd" \
+//	go build ./worker/gpu
+
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../../../distributed_raytracer_amd -lmirt -Wl,-rpath,${SRCDIR}/../../../../distributed_raytracer_amd
+#cgo LDFLAGS: -lmirt
 #include <stdlib.h>
 #include "mirt.h"
 */
