@@ -47,6 +47,68 @@ VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions per second: 1
 HOST_CORES = 16  # the GPU box's CPU share for one GPU (os.cpu_count() shows the whole machine)
 
 
+LDS_RESIDENT_FACES = 1024  # meshes up to this many faces are staged whole into each workgroup's LDS
+
+
+def scene_tag(path: str) -> str:
+    """Which scene a profile was taken on: the scene file's directory and name."""
+    p = os.path.abspath(path)
+    return os.path.join(os.path.basename(os.path.dirname(p)), os.path.basename(p))
+
+
+def find_profile(path: str, shape: dict):
+    """The committed rocprofv3 summary of THIS command (tools/roofline.py): the given file, or
+    the newest profiles/*_roofline.json (by tag) whose launch shape equals this run's;
+    counters from another shape are never mixed in."""
+    import glob
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), reverse=True)
+    for c in cands:
+        pj = load_profile(c, shape)
+        if pj:
+            return pj, c
+    return None, None
+
+
+def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch, launch_ms,
+                   mesh_lds_resident):
+    """`roofline` of the bench line: the PHYSICAL binding roof of the frame kernel.  The
+    kernels are fp64 VALU code whose mesh sits in LDS (suzanne) or streams from L2/HBM
+    (configs[3]); the committed PMC passes of this exact command (profiles/) show VALU issue as
+    the binding roof, so achieved = wave64 VALU instructions per frame (SQ_INSTS_VALU of the
+    frame kernel, from the committed PMC pass) / ms_per_step (the headline frame interval,
+    measured live), against the chip's wave64 issue rate (1,024 SIMDs x 2.4 GHz / 4 cycles).
+    traffic = HBM bytes per frame from the PMC passes ((2 FETCH_SIZE + WRITE_SIZE) x 1024).
+    The north star's algorithmic HBM figure (72 B x ray-triangle tests / launch duration) is
+    kept as `algorithmic`.  Without a committed profile of this command the algorithmic figure
+    is the roofline (and says so)."""
+    alg = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "kind": "algorithmic (north star): 72 B fp64 triangle record x ray-triangle tests performed "
+                   "(device counter) per launch / mean HIP-event duration of the launch" + (
+                       "; the mesh is LDS-resident, so these bytes are LDS reads, not HBM traffic"
+                       if mesh_lds_resident else "; the mesh is HBM-resident (scalar loads through L2/MALL)"),
+           "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
+           "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(launch_ms, 4)}
+    if not pj or "sq_insts_valu_per_launch" not in pj:
+        out = dict(alg)
+        out["traffic"] = None
+        out["note"] = "no committed PMC profile of this command's shape: algorithmic roofline only"
+        return out
+    fpl = pj["frames_per_launch"]
+    valu = pj["sq_insts_valu_per_launch"] / fpl
+    ach = valu / (ms / 1e3) / 1e9
+    peak = VALU_ISSUE_PER_S / 1e9
+    hbm = pj.get("hbm_bytes_per_launch")
+    return {"bound": "valu", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "G wave64-VALU-inst/s",
+            "frac": round(ach / peak, 4), "traffic": int(hbm / fpl) if hbm is not None else None,
+            "traffic_unit": "HBM bytes per frame (PMC)",
+            "kind": "physical: SQ_INSTS_VALU of " + kname + " per frame (committed PMC pass of this command) / "
+                    "ms_per_step, against 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction",
+            "kernel": kname, "valu_insts_per_frame": int(valu), "interval_ms": round(ms, 4),
+            "device_interval_frac": round(valu / (dev_ms / 1e3) / VALU_ISSUE_PER_S, 4),
+            "source": os.path.relpath(pj_path, ROOT), "algorithmic": alg}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +132,11 @@ def parse():
     ap.add_argument("--sharder", choices=("native", "torch"), default="native",
                     help="per-frame driver: native (libmirt mirt_trace_frame, RCCL called from C) or torch "
                          "(framebuffer.FrameSharder over torch.distributed)")
+    ap.add_argument("--camera", choices=("static", "orbit"), default="static",
+                    help="static: the scene's frame-0 camera every frame; orbit: a camera that changes every "
+                         "frame (the scene camera orbited about the first object, --orbit-deg per frame, "
+                         "NewCamera per frame), as the reference master issues frames while the camera moves")
+    ap.add_argument("--orbit-deg", type=float, default=1.0, help="orbit step per frame (degrees)")
     ap.add_argument("--no-d2h", action="store_true", help="leave the assembled frames in HBM (no host output)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -83,9 +150,10 @@ def parse():
                     help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02_roofline.json"),
+    ap.add_argument("--profile-json", default="",
                     help="per-launch counters of the dominant kernel from rocprofv3 passes of this command "
-                         "(tools/roofline.py writes it; used only when its launch shape equals this run's)")
+                         "(tools/roofline.py writes it; used only when its launch shape equals this run's); "
+                         "default: the newest profiles/*_roofline.json whose shape matches")
     a = ap.parse_args()
     resolve_shape(a)
     return a
@@ -175,14 +243,36 @@ def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
     return out
 
 
+def orbit_cameras(cam_pos, cam_dir, fov, center, n: int, step_deg: float):
+    """n cameras orbiting `center` about the world y axis from the scene camera's position,
+    each looking at the center: (pos, forward, fov) for NewCamera (camera.go:35-44), which
+    normalises the forward itself.  Frame data only — the reference's camera motion code is
+    out of scope."""
+    import math
+    c = np.asarray(center, np.float64)
+    r = np.asarray(cam_pos, np.float64) - c
+    out = []
+    for k in range(n):
+        a = math.radians(step_deg * k)
+        ca, sa = math.cos(a), math.sin(a)
+        p = c + np.array([ca * r[0] + sa * r[2], r[1], -sa * r[0] + ca * r[2]])
+        out.append((tuple(p), tuple(c - p), fov))
+    return out
+
+
 def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int,
-                 bounces: int = 0) -> dict:
+                 bounces: int = 0, camera=None) -> dict:
     """Parity gate of the timed frames: EVERY pixel of the last timed
     frame against the oracle (R-tree restatement, 16 threads), valid mask and rgb8
     bit-exact; with the D2H on, the frame checked is the host copy."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
-    orc = Oracle(load_scene(scene_path), use_rtree=True)
+    sc = load_scene(scene_path)
+    if camera is not None:  # the moving-camera line's last timed frame
+        import copy
+        sc = copy.copy(sc)
+        sc.cam_pos, sc.cam_dir, sc.fov = tuple(map(float, camera[0])), tuple(map(float, camera[1])), float(camera[2])
+    orc = Oracle(sc, use_rtree=True)
     orc.set_bounces(bounces)
     ref = orc.frame(W, H, nthreads=HOST_CORES)
     ok = bool(np.array_equal(fb_valid, ref["valid"]) and np.array_equal(fb_rgb8, ref["rgb8"]))
@@ -241,7 +331,17 @@ def main():
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses
-    frame = dataclasses.replace(env.mutable(), max_bounces=a.bounces).to_frame()
+    base = dataclasses.replace(env.mutable(), max_bounces=a.bounces)
+    cams = [None]
+    if a.camera == "orbit":
+        c = base.cam
+        cams = orbit_cameras(c.pos, c.forward, c.fov, base.objects[0].pos, max(a.steps, a.warmup), a.orbit_deg)
+        seq = [dataclasses.replace(base, cam=rt.Camera.new(*cam)).to_frame() for cam in cams]
+    else:
+        seq = [base.to_frame()]
+
+    def frame_at(k):
+        return seq[k % len(seq)]
     tris = sum(len(m.face_v) for m in env.meshes)
     nl = len(env.mutable().lights)
     dev = torch.device("cuda", local)
@@ -307,8 +407,8 @@ def main():
     stream = torch.cuda.Stream(dev)
     host_last = None
     with torch.cuda.stream(stream):
-        for _ in range(a.warmup):
-            sh.render(frame)
+        for k in range(a.warmup):
+            sh.render(frame_at(k))
         finish()
         count("warmup", a.warmup)
         torch.cuda.synchronize(dev)
@@ -318,8 +418,8 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         last = None
-        for _ in range(a.steps):
-            last = sh.render(frame)  # N > 1: frame k's gather overlaps frame k+1's tracing
+        for k in range(a.steps):
+            last = sh.render(frame_at(k))  # N > 1: frame k's gather overlaps frame k+1's tracing
         finish()                     # the last frame's gather + unpack (+ D2H) are inside the timed region
         torch.cuda.synchronize(dev)
         barrier()
@@ -339,8 +439,8 @@ def main():
             barrier()
             torch.cuda.synchronize(dev)
             d0 = time.perf_counter()
-            for _ in range(a.steps):
-                sh.render(frame)
+            for k in range(a.steps):
+                sh.render(frame_at(k))
             finish()
             torch.cuda.synchronize(dev)
             barrier()
@@ -353,8 +453,8 @@ def main():
 
         # profiled region: HIP events around every k_trace launch + device counters
         ctx.profile_enable(True)
-        for _ in range(a.steps):
-            sh.render(frame)
+        for k in range(a.steps):
+            sh.render(frame_at(k))
         finish()
         torch.cuda.synchronize(dev)
         ctx.profile_enable(False)
@@ -362,11 +462,11 @@ def main():
 
         # single-frame latency: one frame alone (render, gather + unpack, D2H, host sync), median
         lat = []
-        for _ in range(min(a.steps, 20)):
+        for k in range(min(a.steps, 20)):
             barrier()
             torch.cuda.synchronize(dev)
             l0 = time.perf_counter()
-            sh.render(frame)
+            sh.render(frame_at(k))
             finish()
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - l0)
@@ -396,22 +496,25 @@ def main():
         rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
         nlaunch = max(prof["launches"], 1)
         prim_ms = prof["primary_ms_sum"] / nlaunch
-        # the dominant kernel: k_trace (the whole frame, one launch) or, split, k_primary;
-        # reflection frames always run split (k_primary, k_shadow, k_reflect)
+        # the dominant kernel: k_trace (the whole frame, one launch); split frames: k_primary,
+        # and reflection frames (split, k_primary -> k_shadow -> k_reflect) k_reflect, the
+        # longest of the three (profiles/r02_bench_config4.log: 2.67 of 3.81 ms)
         one = not a.split_kernels and not a.bounces
-        kname = "k_trace" if one else "k_primary"
+        kname = "k_trace" if one else ("k_reflect" if a.bounces else "k_primary")
         k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
         achieved = k_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
         shape = {"width": W, "height": H, "gpus": world, "inflight": a.inflight, "batch": a.batch,
-                 "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname}
-        pj = load_profile(a.profile_json, shape)
+                 "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname,
+                 "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera}
+        pj, pj_path = find_profile(a.profile_json, shape)
         frames_per_launch = pl / nlaunch
         dev_ms = dev_elapsed / steps * 1e3 if dev_elapsed else ms
         line = {
             "metric": METRIC,
-            # value: the device-resident frame interval (inputs and outputs in HBM, the task's
-            # contract); ms_per_step: BASELINE.md §3's ms/frame, the D2H to host memory included
-            "value": round(rays_per_frame / (dev_ms / 1e3) / 1e6, 3),
+            # value: BASELINE.md §3 / SURVEY.md §8(d) Mrays/s = rays per frame / ms per frame with
+            # the D2H of the assembled frame into host memory (ms_per_step); the device-resident
+            # rate (outputs left in HBM) is device_mrays_s
+            "value": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": steps,
@@ -421,22 +524,25 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), static frame-0 camera"
+            "data": ("synthetic: the reference's own example/scene.json (suzanne.obj, 968 tris, 3 lights), " + (
+                         "static frame-0 camera" if a.camera == "static" else
+                         f"camera orbiting the object {a.orbit_deg} deg per frame (a new camera every frame)")
                      if os.path.abspath(a.scene) == os.path.abspath(SCENE) else
                      f"synthetic: {os.path.relpath(a.scene, ROOT)} ({tris} tris, {nl} lights), the scene's camera"),
             "config": {"workload": workload_name(a, W, H, tris, nl), "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)",
-                       "d2h": "rgb8 + valid to pinned host memory inside the timed region" if d2h else "none (HBM)"},
+                       "d2h": "rgb8 + valid to pinned host memory inside the timed region" if d2h else "none (HBM)",
+                       "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera},
             "frames_in_flight": getattr(sh, "F", a.inflight),
             "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,
-            "value_basis": "rays_per_frame / device_ms_per_frame (outputs left in HBM); ms_per_step includes the "
-                           "D2H of the assembled rgb8 + valid frame into pinned host memory" if d2h else
-                           "rays_per_frame / ms_per_step (outputs left in HBM)",
+            "value_basis": "rays_per_frame / ms_per_step; ms_per_step includes the D2H of the assembled rgb8 + "
+                           "valid frame into pinned host memory (BASELINE.md §3)" if d2h else
+                           "rays_per_frame / ms_per_step (outputs left in HBM: --no-d2h)",
             "device_ms_per_frame": round(dev_ms, 4),
-            "mrays_s_with_d2h": round(rays_per_frame / (ms / 1e3) / 1e6, 3),
+            "device_mrays_s": round(rays_per_frame / (dev_ms / 1e3) / 1e6, 3),
             "frame_latency_ms": round(latency * 1e3, 4),
             "primary_mrays_s": round(primary / (dev_ms / 1e3) / 1e6, 3),
             "rays_per_frame": int(rays_per_frame),
@@ -449,14 +555,8 @@ def main():
                            "reflect": round(prof["reflect_ms_sum"] / nlaunch, 4),
                            "frame_device": round(prof["frame_ms_sum"] / nlaunch, 4)},
             "launches": launches,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pj["hbm_bytes_per_launch"] if pj else None,
-                         "kind": "algorithmic (north star): 72 B fp64 triangle record x ray-triangle tests performed "
-                                 "(device counter) per launch / mean HIP-event duration of the launch; the mesh is "
-                                 "LDS-resident, so these bytes never touch HBM (physical roofs: `roofs`)",
-                         "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
-                         "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(prim_ms, 4)},
+            "roofline": roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch,
+                                       prim_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES),
         }
         # north_star's own target: the brute-force work, bytes/tri-test x tris
         # x rays, over the frame interval, against >= 40% of the per-GPU HBM roofline.  Culling
@@ -471,11 +571,11 @@ def main():
         if pj:
             # physical roofs over the frame interval (counters of this exact command, profiles/)
             per_frame = lambda x: x / pj["frames_per_launch"]  # noqa: E731
-            iv = dev_ms / 1e3  # the device-resident frame interval (k_trace's counters)
+            iv = ms / 1e3  # the headline frame interval (ms_per_step)
             valu = per_frame(pj["sq_insts_valu_per_launch"])
             line["roofs"] = {
-                "source": os.path.relpath(a.profile_json, ROOT),
-                "frame_interval_ms": round(dev_ms, 4),
+                "source": os.path.relpath(pj_path, ROOT),
+                "frame_interval_ms": round(ms, 4),
                 "valu_issue_frac": round(valu / iv / VALU_ISSUE_PER_S, 4),
                 "valu_insts_per_frame": int(valu),
                 "salu_insts_per_frame": int(per_frame(pj["sq_insts_salu_per_launch"])),
@@ -491,7 +591,8 @@ def main():
             else:
                 fr = sh.frame
                 rgb8, valid = fr.rgb8.cpu().numpy(), fr.valid.cpu().numpy()
-            line["parity"] = parity_check(valid, rgb8, a.scene, W, H, a.bounces)
+            line["parity"] = parity_check(valid, rgb8, a.scene, W, H, a.bounces,
+                                          cams[(a.steps - 1) % len(cams)] if a.camera == "orbit" else None)
             line["parity"]["frame"] = "host copy (D2H)" if host_last is not None else "device framebuffer"
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.scene, W, H)
