@@ -43,7 +43,8 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"] if os.pa
 BYTES_PER_TRI_TEST = 72  # fp64 P1, E1, E2 read per ray-triangle test
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec, vector FP64 (FMA = 2 flops)
-VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions per second: 1024 SIMDs, 4 cycles each
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions per second at 4 cycles each (fp64 rate)
+SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9     # VALU-busy roof: 1024 SIMDs x 2.4 GHz
 HOST_CORES = 16  # the GPU box's CPU share for one GPU (os.cpu_count() shows the whole machine)
 
 
@@ -70,24 +71,25 @@ def find_profile(path: str, shape: dict):
 
 
 def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch, launch_ms,
-                   mesh_lds_resident):
+                   mesh_lds_resident, alg_kernel=None):
     """`roofline` of the bench line: the PHYSICAL binding roof of the frame kernel.  The
     kernels are fp64 VALU code whose mesh sits in LDS (suzanne) or streams from L2/HBM
-    (configs[3]); the committed PMC passes of this exact command (profiles/) show VALU issue as
-    the binding roof, so achieved = wave64 VALU instructions per frame (SQ_INSTS_VALU of the
-    frame kernel, from the committed PMC pass) / ms_per_step (the headline frame interval,
-    measured live), against the chip's wave64 issue rate (1,024 SIMDs x 2.4 GHz / 4 cycles).
-    traffic = HBM bytes per frame from the PMC passes ((2 FETCH_SIZE + WRITE_SIZE) x 1024).
-    The north star's algorithmic HBM figure (72 B x ray-triangle tests / launch duration) is
-    kept as `algorithmic`.  Without a committed profile of this command the algorithmic figure
-    is the roofline (and says so)."""
+    (configs[3]); the committed PMC passes of this exact command (profiles/) show the VALU as
+    the binding unit (HBM at ~10%), so achieved = VALU-busy SIMD cycles per frame (4 x
+    SQ_ACTIVE_INST_VALU of the frame kernel, the numerator of rocprof's VALUBusy) /
+    ms_per_step (the headline frame interval, measured live), against 1,024 SIMDs x 2.4 GHz.
+    `issue` keeps the instruction count (SQ_INSTS_VALU) at the fp64 issue rate; traffic = HBM
+    bytes per frame from the PMC passes ((2 FETCH_SIZE + WRITE_SIZE) x 1024); the north
+    star's algorithmic HBM figure (72 B x ray-triangle tests / launch duration) is kept as
+    `algorithmic`.  Without a committed profile of this command the algorithmic figure is the
+    roofline (and says so)."""
     alg = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4),
            "kind": "algorithmic (north star): 72 B fp64 triangle record x ray-triangle tests performed "
                    "(device counter) per launch / mean HIP-event duration of the launch" + (
                        "; the mesh is LDS-resident, so these bytes are LDS reads, not HBM traffic"
                        if mesh_lds_resident else "; the mesh is HBM-resident (scalar loads through L2/MALL)"),
-           "kernel": kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
+           "kernel": alg_kernel or kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
            "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(launch_ms, 4)}
     if not pj or "sq_insts_valu_per_launch" not in pj:
         out = dict(alg)
@@ -96,17 +98,32 @@ def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per
         return out
     fpl = pj["frames_per_launch"]
     valu = pj["sq_insts_valu_per_launch"] / fpl
-    ach = valu / (ms / 1e3) / 1e9
-    peak = VALU_ISSUE_PER_S / 1e9
     hbm = pj.get("hbm_bytes_per_launch")
-    return {"bound": "valu", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "G wave64-VALU-inst/s",
-            "frac": round(ach / peak, 4), "traffic": int(hbm / fpl) if hbm is not None else None,
-            "traffic_unit": "HBM bytes per frame (PMC)",
-            "kind": "physical: SQ_INSTS_VALU of " + kname + " per frame (committed PMC pass of this command) / "
-                    "ms_per_step, against 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction",
-            "kernel": kname, "valu_insts_per_frame": int(valu), "interval_ms": round(ms, 4),
-            "device_interval_frac": round(valu / (dev_ms / 1e3) / VALU_ISSUE_PER_S, 4),
-            "source": os.path.relpath(pj_path, ROOT), "algorithmic": alg}
+    issue = {"valu_insts_per_frame": int(valu),
+             "issue_frac_4cyc": round(valu / (ms / 1e3) / VALU_ISSUE_PER_S, 4),
+             "note": "wave64 VALU instructions per frame / ms_per_step against one instruction per 4 cycles per "
+                     "SIMD (fp64 rate); fp32 and integer ops issue in 2 on CDNA4's SIMD-32"}
+    common = {"traffic": int(hbm / fpl) if hbm is not None else None,
+              "traffic_unit": "HBM bytes per frame (PMC: (2 FETCH_SIZE + WRITE_SIZE) x 1024)", "kernel": kname,
+              "interval_ms": round(ms, 4), "source": os.path.relpath(pj_path, ROOT), "issue": issue, "algorithmic": alg}
+    if "valu_busy_simd_cycles_per_launch" in pj:
+        busy = pj["valu_busy_simd_cycles_per_launch"] / fpl
+        peak = SIMD_CYCLES_PER_S
+        out = {"bound": "valu", "achieved": round(busy / (ms / 1e3) / 1e9, 2), "peak": round(peak / 1e9, 1),
+               "unit": "G VALU-busy SIMD-cycles/s", "frac": round(busy / (ms / 1e3) / peak, 4),
+               "kind": "physical: VALU-busy SIMD cycles of " + kname + " per frame (4 x SQ_ACTIVE_INST_VALU, the "
+                       "committed PMC pass of this command) / ms_per_step, against 1024 SIMDs x 2.4 GHz",
+               "valu_busy_cycles_per_frame": int(busy), "lane_utilization": pj.get("valu_lane_utilization"),
+               "device_interval_frac": round(busy / (dev_ms / 1e3) / peak, 4)}
+        out.update(common)
+        return out
+    out = {"bound": "valu", "achieved": round(valu / (ms / 1e3) / 1e9, 2), "peak": round(VALU_ISSUE_PER_S / 1e9, 1),
+           "unit": "G wave64-VALU-inst/s", "frac": issue["issue_frac_4cyc"],
+           "kind": "physical: SQ_INSTS_VALU of " + kname + " per frame (committed PMC pass of this command) / "
+                   "ms_per_step, against 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction",
+           "device_interval_frac": round(valu / (dev_ms / 1e3) / VALU_ISSUE_PER_S, 4)}
+    out.update(common)
+    return out
 
 
 def parse():
@@ -501,8 +518,15 @@ def main():
         # longest of the three (profiles/r02_bench_config4.log: 2.67 of 3.81 ms)
         one = not a.split_kernels and not a.bounces
         kname = "k_trace" if one else ("k_reflect" if a.bounces else "k_primary")
-        k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
-        achieved = k_tests * BYTES_PER_TRI_TEST / (prim_ms / 1e3) / 1e9
+        if a.bounces:
+            # the algorithmic figure over the frame's three kernels: k_reflect's tests are counted
+            # with k_shadow's (one statistic), so the whole frame's tests / its device time
+            k_tests = (prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / nlaunch
+            alg_ms, alg_kernel = prof["frame_ms_sum"] / nlaunch, "k_primary + k_shadow + k_reflect"
+        else:
+            k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
+            alg_ms, alg_kernel = prim_ms, kname
+        achieved = k_tests * BYTES_PER_TRI_TEST / (alg_ms / 1e3) / 1e9
         shape = {"width": W, "height": H, "gpus": world, "inflight": a.inflight, "batch": a.batch,
                  "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname,
                  "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera}
@@ -556,7 +580,7 @@ def main():
                            "frame_device": round(prof["frame_ms_sum"] / nlaunch, 4)},
             "launches": launches,
             "roofline": roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch,
-                                       prim_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES),
+                                       alg_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES, alg_kernel=alg_kernel),
         }
         # north_star's own target: the brute-force work, bytes/tri-test x tris
         # x rays, over the frame interval, against >= 40% of the per-GPU HBM roofline.  Culling

@@ -648,6 +648,16 @@ extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
 #define MIRT_SHADOW_WIDE 0
 #endif
 #define MIRT_TRACE_KERNEL __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_WAVES_PER_EU)))
+// k_reflect keeps a whole bounce (ray, hit, normal) live through its shadow queries.  At 2
+// waves per SIMD (256 VGPRs, one 512-thread workgroup per CU) nothing spills (168 VGPRs),
+// but configs[4] ran 30% slower (1.28-1.31 vs 0.98-1.01 ms per frame, tools/ab_bench.sh):
+// the occupancy is worth more than the 17-77 spilled VGPRs (<= 160 B of scratch per lane,
+// mostly outside the traversal loops) it costs at 4.
+#ifndef MIRT_REFLECT_WAVES_PER_EU
+#define MIRT_REFLECT_WAVES_PER_EU 4
+#endif
+#define MIRT_REFLECT_KERNEL \
+    __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_REFLECT_WAVES_PER_EU)))
 
 // ---------------------------------------------------------------- wide traversal
 #ifndef MIRT_LEAF_LANE_TEST
@@ -2132,7 +2142,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
 // c_(k+1))), a miss contributing black, the deepest level (k = bounces) plain phong.
 // Level 0's phong comes from the shadow kernel (WorkArgs::ph0).
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ cnt_t red[kWG / 64][4];
     // RESIDENT implies one object and no MIRT_OPT_NO_SEGMENT (is_resident): a constant there
@@ -2155,7 +2165,9 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
             const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
             const HitRec rec = wa.hits[slot];
             const bool active = rec.obj != kNoHit;
-            RGB ph[MIRT_MAX_BOUNCES + 1], ks[MIRT_MAX_BOUNCES + 1];
+            // Only the current bounce is live; each level's phong and material go to
+            // WorkArgs::refl and are folded back innermost first below (a per-lane array of
+            // every level, indexed at run time, lived in scratch: 55-71 spilled VGPRs).
             V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
             uint32_t levels = 0;   // levels with a phong value
             bool missed = false;   // the chain ended on a miss (else on the depth limit)
@@ -2163,9 +2175,6 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
                 D = vload(wa.dir0 + 3 * slot);
                 hit = vload(rec.h);
                 N = vload(rec.n);
-                ph[0] = RGB{wa.ph0[3 * slot], wa.ph0[3 * slot + 1], wa.ph0[3 * slot + 2]};
-                const double* mt = fa.obj[rec.obj].m.mats + (size_t)rec.mat * 10;
-                ks[0] = RGB{mt[6], mt[7], mt[8]};
                 levels = 1;
             }
             bool on = active;
@@ -2207,10 +2216,13 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
                     ws.leaves += sv.leaves;
                     ws.overflow += sv.overflow;
                 }
-                if (on) {
-                    const double* mt = fa.obj[r.obj].m.mats + (size_t)r.mat * 10;
-                    ph[lv] = phong(fa, mt, r.hit, r.normal, lit);
-                    ks[lv] = RGB{mt[6], mt[7], mt[8]};
+                if (on) {  // the level's phong and material wait in WorkArgs::refl for the fold
+                    const RGB ph = phong(fa, fa.obj[r.obj].m.mats + (size_t)r.mat * 10, r.hit, r.normal, lit);
+                    double* const e = wa.refl + ((size_t)(lv - 1) * wa.refl_stride + slot) * kReflD;
+                    e[0] = ph.r;
+                    e[1] = ph.g;
+                    e[2] = ph.b;
+                    e[3] = bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
                     levels = lv + 1;
                     D = R;
                     hit = r.hit;
@@ -2218,10 +2230,30 @@ MIRT_TRACE_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPlane
                 }
             }
             if (active) {
+                // c_L = ph_L (a chain that ended on a miss: c_add(ph_L, c_mul(Ks_L, black))),
+                // then c_k = c_add(ph_k, c_mul(Ks_k, c_(k+1))) down to level 0
                 const uint32_t L = levels - 1;
-                RGB c = ph[L];
-                if (missed) c = c_add(ph[L], c_mul(ks[L], RGB{0, 0, 0}));  // c_reflected = black
-                for (int lv = (int)L - 1; lv >= 0; --lv) c = c_add(ph[lv], c_mul(ks[lv], c));
+                auto level = [&](uint32_t lv, RGB& ph, RGB& ks) {
+                    uint32_t obj = rec.obj, mat = rec.mat;
+                    if (lv == 0) {
+                        ph = RGB{wa.ph0[3 * slot], wa.ph0[3 * slot + 1], wa.ph0[3 * slot + 2]};
+                    } else {
+                        const double* e = wa.refl + ((size_t)(lv - 1) * wa.refl_stride + slot) * kReflD;
+                        ph = RGB{e[0], e[1], e[2]};
+                        const uint64_t om = dbits(e[3]);
+                        obj = (uint32_t)om;
+                        mat = (uint32_t)(om >> 32);
+                    }
+                    const double* mt = fa.obj[obj].m.mats + (size_t)mat * 10;
+                    ks = RGB{mt[6], mt[7], mt[8]};
+                };
+                RGB ph, ks;
+                level(L, ph, ks);
+                RGB c = missed ? c_add(ph, c_mul(ks, RGB{0, 0, 0})) : ph;  // c_reflected = black
+                for (int lv = (int)L - 1; lv >= 0; --lv) {
+                    level((uint32_t)lv, ph, ks);
+                    c = c_add(ph, c_mul(ks, c));
+                }
                 if (out.rgb) {
                     out.rgb[3 * rec.out] = c.r;
                     out.rgb[3 * rec.out + 1] = c.g;

@@ -96,6 +96,8 @@ struct Slot {
     size_t dir0_cap = 0;
     double* ph0 = nullptr;    // configs[4] reflections: phong of the primary hit per slot
     size_t ph0_cap = 0;
+    double* refl = nullptr;   // configs[4] reflections: per level and slot, phong + obj|mat
+    size_t refl_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
     size_t cost_cap = 0;
     cnt_t* counters = nullptr;
@@ -199,7 +201,7 @@ int slot_init(Slot* s) {
 
 void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0,
+    for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
                     (void*)s->d_frames, (void*)s->views, (void*)s->view_heads})
         if (p) (void)hipFree(p);
@@ -594,8 +596,11 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     if (wa.bounces) {
         if ((r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
         if ((r = dev_grow(sl->ph0, sl->ph0_cap, 3 * hit_slots)) != MIRT_OK) return r;
+        if ((r = dev_grow(sl->refl, sl->refl_cap, (size_t)kReflD * bounces * hit_slots)) != MIRT_OK) return r;
         wa.dir0 = sl->dir0;
         wa.ph0 = sl->ph0;
+        wa.refl = sl->refl;
+        wa.refl_stride = hit_slots;
     }
     if (one_launch && !getenv("MIRT_NO_COST_ORDER")) {
         const size_t cap0 = sl->cost_cap;
@@ -1538,13 +1543,22 @@ struct mirt_group {
     uint32_t* d_spans = nullptr;        // host output: per frame slot and column, the hit span the host holds
     // frames and batches
     uint32_t B = 1, FB = 1;
+    // Host run-ahead: batch records and events form a ring of HB = FB x runahead entries, so
+    // the host enqueues up to runahead x FB batches while the device runs FB at a time (one
+    // per stream).  With HB = FB the host waited for batch nb - FB before enqueueing batch nb
+    // and its stream sat idle from that batch's end until the host's launch reached it
+    // (~20 us per stream cycle in the kernel trace).  Device resources stay per stream
+    // (stream order protects them); run-ahead is off (1) for multi-frame batches, whose
+    // records are staged in pinned host memory per stream slot, and for tiled groups
+    // (per-slot trailer verdicts, transfers).
+    uint32_t HB = 1, runahead = 1;
     uint64_t nb = 0;                    // batches launched
     uint64_t k = 0;                     // frames enqueued
     uint32_t bn = 0;                    // frames in the open batch
     uint32_t bj[kMaxFrames] = {};
     FrameRec stage[kMaxFrames];         // the open batch's records (copied per share at launch)
     uint32_t bbounces = 0;
-    std::vector<BatchRec> binfo;        // per batch slot
+    std::vector<BatchRec> binfo;        // per host ring slot (HB)
     std::vector<uint64_t> slot_frame;   // per frame slot: the frame it holds (~0: none)
     // per frame slot: only [dirty0, dirty1) x [dirty_y0, dirty_y1) may hold non-miss pixels
     // (whole-screen planes); a narrow frame refills those columns before it traces its hit
@@ -1566,6 +1580,11 @@ uint64_t now_us() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                std::chrono::steady_clock::now().time_since_epoch())
         .count();
+}
+
+// The host ring (see mirt_group::HB): run-ahead only for one-frame batches of untiled groups.
+void group_ring(mirt_group* g) {
+    g->HB = g->FB * ((g->B == 1 && !g->tiled) ? g->runahead : 1u);
 }
 
 // Wait for a group event, within the group's deadline (0: no deadline).
@@ -2006,6 +2025,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->H = H;
     g->F = inflight;
     g->FB = inflight;  // one frame per launch until mirt_group_set_batch
+    const char* ra = getenv("MIRT_RUNAHEAD");
+    g->runahead = (uint32_t)std::min(std::max(ra ? atoi(ra) : 2, 1), 4);
     g->tile = tile;
     g->tile_h = tile_h;
     g->tiled = tile > 0;
@@ -2024,23 +2045,25 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     for (int q = 0; q < plan_world; ++q) g->members.push_back((uint32_t)q);
     g->my_index = rank;
     g->streams.assign(inflight, nullptr);
-    g->ev_traced.assign(inflight, nullptr);
-    g->ev_gathered.assign(inflight, nullptr);
-    g->ev_done.assign(inflight, nullptr);
+    const uint32_t ring = inflight * g->runahead;  // the largest HB this group can use
+    g->ev_traced.assign(ring, nullptr);
+    g->ev_gathered.assign(ring, nullptr);
+    g->ev_done.assign(ring, nullptr);
     // host output on reserved CUs (MIRT_D2H_CUS=n): the trace kernels fill every CU's VGPR
     // file, so a copy kernel sharing their CUs waits for a frame tail to start; n CUs kept
     // for the copy stream let each frame's D2H run beside the next frames' traces
     const char* dc = getenv("MIRT_D2H_CUS");
     g->d2h_cus = dc ? std::min(std::max(atoi(dc), 0), c->cus / 2) : 0;
-    for (uint32_t j = 0; j < inflight; ++j) {
-        HIP_TRY(stream_with_queue(c->cus, &g->streams[j], 0, c->cus - g->d2h_cus));
+    for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(stream_with_queue(c->cus, &g->streams[j], 0, c->cus - g->d2h_cus));
+    for (uint32_t j = 0; j < ring; ++j) {
         HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&g->ev_comm, hipEventDisableTiming));
     if (g->d2h_cus) HIP_TRY(stream_with_queue(c->cus, &g->copy_stream, c->cus - g->d2h_cus, c->cus));
-    g->binfo.assign(inflight, BatchRec());
+    g->binfo.assign(ring, BatchRec());
+    group_ring(g.get());
     g->slot_frame.assign(inflight, ~0ull);
     g->slot_bad.assign(inflight, 0);
     g->dirty0.assign(inflight, 0);  // the planes' first contents are unknown: the whole screen
@@ -2136,7 +2159,7 @@ int mirt_group_set_host_output(mirt_group* g, int enable) {
             hf.rect[2] = g->W;
             hf.rect[3] = g->H;
         }
-        for (uint32_t b = 0; b < g->F; ++b)  // every column's span: the whole column
+        for (uint32_t b = 0; b < g->HB; ++b)  // every column's span: the whole column
             HIP_TRY(hipStreamWaitEvent(g->streams[0], g->ev_done[b], 0));
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)g->d_spans, (int)(g->H << 16), (size_t)g->F * g->W, g->streams[0]));
         for (uint32_t b = 1; b < g->F; ++b) {
@@ -2244,12 +2267,13 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
 static int group_flush(mirt_group* g) {
     if (g->bn == 0) return MIRT_OK;
     mirt_ctx* c = g->c;
-    const uint32_t bs = (uint32_t)(g->nb % g->FB);
+    const uint32_t bs = (uint32_t)(g->nb % g->FB);  // the stream and its device slot
+    const uint32_t hs = (uint32_t)(g->nb % g->HB);  // the host ring slot: records and events
     hipStream_t s = g->streams[bs];
     const bool is_root = g->rank == 0;
     const uint32_t n = g->bn;
     g->bn = 0;
-    BatchRec& br = g->binfo[bs];
+    BatchRec& br = g->binfo[hs];
     br.n = n;
     br.first = g->k - n;
     br.checked = false;
@@ -2263,14 +2287,15 @@ static int group_flush(mirt_group* g) {
     HT(7);
     // a sender reuses its packed planes only after their previous batch's sends are done (the
     // root's stream already waited for that gather before its unpacks)
-    if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
+    if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB)
+        HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[(g->nb - g->FB) % g->HB], 0));
     // adaptive grid (MIRT_ADAPTIVE_GRID=1): the launches still running share the chip with
     // this one, ~wg_factor x CUs workgroups between them
     uint32_t max_wg_now = 0;
     if (g->adaptive_grid) {
         uint32_t running = 0;
         for (uint64_t b = g->nb > g->FB ? g->nb - g->FB + 1 : 0; b < g->nb; ++b)
-            if (hipEventQuery(g->ev_done[b % g->FB]) == hipErrorNotReady) ++running;
+            if (hipEventQuery(g->ev_done[b % g->HB]) == hipErrorNotReady) ++running;
         max_wg_now = std::max<uint32_t>(1, (uint32_t)(2 * kWgPerCu * (uint64_t)c->cus / (running + 1)));
     }
     // Blocks outside a frame's hit rectangle (every ray misses) are not traced: a share's
@@ -2356,8 +2381,8 @@ static int group_flush(mirt_group* g) {
     if (g->tiled && g->world > 1) {
         const Rccl& R = rccl();
         const uint32_t P = (uint32_t)g->members.size();
-        HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
-        HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[bs], 0));
+        HIP_TRY(hipEventRecord(g->ev_traced[hs], s));
+        HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->ev_traced[hs], 0));
         RCCL_TRY(R.group_start());
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t j = g->bj[i];
@@ -2371,8 +2396,8 @@ static int group_flush(mirt_group* g) {
             }
         }
         RCCL_TRY(R.group_end());
-        HIP_TRY(hipEventRecord(g->ev_gathered[bs], g->comm_stream));
-        if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[bs], 0));
+        HIP_TRY(hipEventRecord(g->ev_gathered[hs], g->comm_stream));
+        if (is_root) HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[hs], 0));
     }
     HT(4);
     if (g->tiled && is_root && !g->skip_unpack) {
@@ -2404,10 +2429,10 @@ static int group_flush(mirt_group* g) {
         } else if (cols && g->copy_stream) {
             // the batch's frames are final on stream s: copy them on the reserved CUs, and let
             // the batch complete (ev_done) only once they are in host memory
-            HIP_TRY(hipEventRecord(g->ev_traced[bs], s));
-            HIP_TRY(hipStreamWaitEvent(g->copy_stream, g->ev_traced[bs], 0));
+            HIP_TRY(hipEventRecord(g->ev_traced[hs], s));
+            HIP_TRY(hipStreamWaitEvent(g->copy_stream, g->ev_traced[hs], 0));
             HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, g->copy_stream));
-            HIP_TRY(hipEventRecord(g->ev_done[bs], g->copy_stream));
+            HIP_TRY(hipEventRecord(g->ev_done[hs], g->copy_stream));
             ++g->nb;
             return MIRT_OK;
         } else if (cols) {
@@ -2415,7 +2440,7 @@ static int group_flush(mirt_group* g) {
         }
     }
     HT(5);
-    HIP_TRY(hipEventRecord(g->ev_done[bs], s));
+    HIP_TRY(hipEventRecord(g->ev_done[hs], s));
     HT(6);
     ++g->nb;
     return MIRT_OK;
@@ -2430,6 +2455,7 @@ int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
         return fail(MIRT_E_INVALID, "several frames per launch need the single-kernel path (not MIRT_OPT_SPLIT_KERNELS)");
     g->B = frames_per_launch;
     g->FB = g->F / g->B;
+    group_ring(g);
     return MIRT_OK;
 }
 
@@ -2453,13 +2479,14 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     if (g->bn > 0 && (g->bbounces || f->max_bounces || (c->flags & MIRT_OPT_SPLIT_KERNELS) ||
                       !frames_batchable(g->stage[0], rec)))
         if ((r = group_flush(g)) != MIRT_OK) return r;
-    const uint32_t bs = (uint32_t)(g->nb % g->FB);
-    // back-pressure when a batch opens: batch nb - FB (the last user of this slot, and of
-    // every framebuffer this batch can touch) must have finished
-    if (g->bn == 0 && g->nb >= g->FB) {
-        if ((r = group_wait_event(g, g->ev_done[bs], "mirt_trace_frame back-pressure")) != MIRT_OK)
-            return group_timed_out(g, bs, r);
-        batch_fold(g, bs);
+    const uint32_t hs = (uint32_t)(g->nb % g->HB);
+    // back-pressure when a batch opens: batch nb - HB (the last user of this host ring slot)
+    // must have finished; batch nb - FB, the last user of this batch's stream, device slot and
+    // framebuffers, is ordered before it by the stream itself
+    if (g->bn == 0 && g->nb >= g->HB) {
+        if ((r = group_wait_event(g, g->ev_done[hs], "mirt_trace_frame back-pressure")) != MIRT_OK)
+            return group_timed_out(g, hs, r);
+        batch_fold(g, hs);
     }
     HT(0);
     g->stage[g->bn] = rec;
@@ -2479,7 +2506,7 @@ int mirt_group_wait(mirt_group* g, void* stream) {
     HIP_TRY(hipSetDevice(g->c->device));
     int r = group_flush(g);
     if (r != MIRT_OK) return r;
-    const uint64_t used = std::min<uint64_t>(g->nb, g->FB);
+    const uint64_t used = std::min<uint64_t>(g->nb, g->HB);
     for (uint64_t b = 0; b < used; ++b) {
         if (stream) {
             HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[b], 0));
@@ -2519,7 +2546,7 @@ int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
     int r;
     if (g->bn && index >= g->k - g->bn && (r = group_flush(g)) != MIRT_OK) return r;
     // the batch holding the frame: the latest launched batch whose slot lists j
-    for (uint32_t b = 0; b < g->FB; ++b) {
+    for (uint32_t b = 0; b < g->HB; ++b) {
         const BatchRec& br = g->binfo[b];
         if (br.n && index >= br.first && index < br.first + br.n) {
             if ((r = group_wait_event(g, g->ev_done[b], "mirt_group_frame_host")) != MIRT_OK)

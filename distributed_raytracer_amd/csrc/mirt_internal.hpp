@@ -273,6 +273,11 @@ struct WorkArgs {
     uint32_t bounces;      // configs[4] reflection extension (mirt_frame.max_bounces), 0 = off
     double* dir0;          // bounces: per hit slot, the primary ray direction (3 doubles)
     double* ph0;           // bounces: per hit slot, phong of the primary hit (3 doubles)
+    // bounces: levels 1..bounces of each slot's chain, level-major ([lv - 1][slot][kReflD]):
+    // the level's phong r, g, b and its obj | mat << 32 bits (k_reflect folds them innermost
+    // first)
+    double* refl;
+    uint64_t refl_stride;  // slots per level
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     FrustumArgs fr;
@@ -298,6 +303,7 @@ struct WorkArgs {
     uint32_t view_pad;
 };
 constexpr int kTimelineRec = 8;
+constexpr int kReflD = 4;  // doubles per slot and level of WorkArgs::refl
 // WorkArgs::dynamic: kernels whose waves take work items dynamically (primary: LDS tickets
 // within the workgroup; shadow / reflect: the sharded device queues).
 enum { kDynPrimary = 1, kDynShadow = 2, kDynReflect = 4 };

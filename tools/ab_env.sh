@@ -13,6 +13,6 @@ for v in "${VARS[@]}"; do
 import json
 d = json.loads([l for l in open('$LOG').read().splitlines() if l.startswith('{')][-1])
 print(json.dumps({'v': '$label', 'F': d['frames_in_flight'], 'B': d['frames_per_launch'], 'ms': d['ms_per_step'],
-                  'dev_ms': d['device_ms_per_frame'], 'lat_ms': d['frame_latency_ms'], 'launch_ms': d['roofline']['launch_ms'],
+                  'dev_ms': d['device_ms_per_frame'], 'lat_ms': d['frame_latency_ms'], 'launch_ms': d['roofline'].get('launch_ms', d['roofline'].get('algorithmic', {}).get('launch_ms')),
                   'tests': d['tri_tests_per_frame'], 'visits': d['bvh_visits_per_frame']}))"
 done

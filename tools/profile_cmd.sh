@@ -23,5 +23,10 @@ run pmc_fetch --pmc FETCH_SIZE
 run pmc_write --pmc WRITE_SIZE
 run pmc_sq --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES \
   SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+# VALU busy cycles and lane utilisation (VALUBusy / VALUUtilization), the instruction mix
+run pmc_valu --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 \
+  SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32
+run pmc_active --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU_CVT \
+  SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32
 echo "args: $ARGS" > "$OUT/args.txt"
 echo done
