@@ -2289,6 +2289,9 @@ static int group_flush(mirt_group* g) {
     // root's stream already waited for that gather before its unpacks)
     if (g->tiled && g->world > 1 && !is_root && g->nb >= g->FB)
         HIP_TRY(hipStreamWaitEvent(s, g->ev_gathered[(g->nb - g->FB) % g->HB], 0));
+    // host copies on copy_stream: batch nb - FB last used this batch's framebuffers; its copy
+    // must have read them before this batch's fill and trace rewrite them
+    if (g->copy_stream && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_done[(g->nb - g->FB) % g->HB], 0));
     // adaptive grid (MIRT_ADAPTIVE_GRID=1): the launches still running share the chip with
     // this one, ~wg_factor x CUs workgroups between them
     uint32_t max_wg_now = 0;
