@@ -1687,13 +1687,14 @@ template <bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u,
-                                            const ViewCache* vc = nullptr) {
+                                            const ViewCache* vc = nullptr, uint32_t lim = 64) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
     const uint64_t* w = (const uint64_t*)&wa.hits[slot];
     const uint64_t w7 = ld64(w + 7);
-    const bool active = (uint32_t)w7 != kNoHit;
+    // lim: the chunk's records (a bounce level's last chunk of a region is partial)
+    const bool active = lane < lim && (uint32_t)w7 != kNoHit;
     V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
     const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
     if (active) {
@@ -1744,10 +1745,11 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     const uint64_t oidx = ld64(w + 6);
     const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
     const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
-    if (wa.bounces) {  // the reflect kernel combines the levels and writes the pixel
-        wa.ph0[3 * slot] = col.r;
-        wa.ph0[3 * slot + 1] = col.g;
-        wa.ph0[3 * slot + 2] = col.b;
+    if (wa.bounces) {  // the level's phong: the reflection fold combines the levels and writes the pixel
+        double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot) * wa.ph_stride;
+        e[0] = col.r;
+        e[1] = col.g;
+        e[2] = col.b;
         return;
     }
     if (out.rgb) {
@@ -1864,10 +1866,11 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
     const ShardCursor sc;
     WaveStats ws{0, 0, 0, 0, 0};
     const uint32_t nl = max(fa.n_lights, 1u);
+    cnt_t* const qctr = wa.qcounters ? wa.qcounters : wa.counters;
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
+        const uint32_t nrec = *lo32(&qctr[cnt_hits(q)]), nch = (nrec + 63) / 64;
         const uint32_t items = nch * nl, peers = sc.peers();
-        cnt_t* qc = &wa.counters[cnt_queue(1, q)];
+        cnt_t* qc = &qctr[cnt_queue(1, q)];
         // item rank is this wave's (static); with the queue on, items peers + ticket follow,
         // each ticket taken while the previous item is traced
         const bool dyn = (wa.dynamic & kDynShadow) && items > peers;
@@ -1877,13 +1880,14 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
             shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
-                                          (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws);
+                                          (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, ~0u, nullptr,
+                                          min(64u, nrec - c * 64));
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
-    if (!wa.bounces) frame_fold(fa, wa);  // otherwise k_reflect is the frame's last kernel
+    if (!wa.bounces) frame_fold(fa, wa);  // otherwise the reflection fold is the frame's last kernel
 }
 
 // ---------------------------------------------------------------- one-launch frame
@@ -2277,6 +2281,134 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
     frame_fold(fa, wa);
 }
 
+// Reflections in waves of bounces (MIRT_OPT_REFLECT_WAVES; the default k_reflect above
+// follows each lane's whole chain).  Per level lv = 1..bounces: k_bounce traces one reflection ray
+// per record of level lv - 1 (R = D - 2 (D.N) N from hit + 1e-4 R, the nearest hit of
+// tracer.go:27-50) and packs the hits into level lv's records — region by region, each wave
+// appending its hits after one atomic, so a later wave of 64 records holds 64 live rays (the
+// chain kernel kept a lane per primary hit through every level: 41% of its lanes had a ray
+// at level 1, ~12% at level 4); k_shadow then traces level lv's shadow rays and stores its
+// phong at the origin slot; k_refl_fold combines the levels per pixel, innermost first.
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const BounceArgs ba) {
+    double* const lds = g_lds_mesh;
+    __shared__ cnt_t red[kWG / 64][4];
+    if (RESIDENT) {
+        stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const ShardCursor sc;
+    WaveStats ws{0, 0, 0, 0, 0};
+    cnt_t rays = 0, shadow_rays = 0;
+    const uint32_t lv = ba.level;
+    for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
+        const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
+        for (uint32_t k = sc.rank(); k < nch; k += sc.peers()) {
+            const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
+            const bool inb = k * 64 + lane < n;
+            const HitRec rec = ba.in[inb ? slot : (size_t)q * wa.hit_cap + (size_t)k * 64];
+            const bool active = inb && rec.obj != kNoHit;
+            const size_t origin = lv == 1 ? slot : (size_t)rec.out;
+            V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
+            if (active) {
+                D = vload(ba.in_dir + 3 * slot);
+                hit = vload(rec.h);
+                N = vload(rec.n);
+            }
+            const V3 R = sub(D, scale(N, 2 * dot(D, N)));
+            const V3 o = add(hit, scale(R, 0.0001));
+            Visits vis{0, 0, 0, 0};
+            const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, active, true, vis);
+            rays += __popcll(__ballot(active));
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
+            const bool got = active && r.ok;
+            if (active) ba.chain[origin] = got ? lv + 1 : (lv | 256u);  // levels with phong | missed
+            const uint64_t m = __ballot(got);
+            if (m) {
+                shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(lo32(&ba.out_cnt[cnt_hits(q)]), (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (got) {
+                    const size_t os = (size_t)q * wa.hit_cap + base + __popcll(m & ((1ull << lane) - 1ull));
+                    HitRec h;
+                    h.h[0] = r.hit.x, h.h[1] = r.hit.y, h.h[2] = r.hit.z;
+                    h.n[0] = r.normal.x, h.n[1] = r.normal.y, h.n[2] = r.normal.z;
+                    h.out = origin;
+                    h.obj = r.obj;
+                    h.mat = r.mat;
+                    ba.out[os] = h;
+                    vstore(ba.out_dir + 3 * os, R);
+                    ba.out_litw[os] = 0u;
+                    ba.out_blkdone[os / 64] = 0u;  // (every writer of the chunk: the same zero)
+                    wa.refl[((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD + 3] =
+                        bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
+                }
+            }
+        }
+    }
+    WaveStats extra{rays, (uint32_t)shadow_rays, 0, 0, 0};  // per wave: well below 2^32
+    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
+    __syncthreads();
+    stats_flush(wa.counters, red, kStatReflRays, kStatReflShadowRays, -1, -1, extra);
+}
+
+// The frame's last kernel on the bounce path: per primary hit slot, c_L = ph_L (a chain that
+// ended on a miss: c_add(ph_L, c_mul(Ks_L, black))), then c_k = c_add(ph_k, c_mul(Ks_k,
+// c_(k+1))) down to level 0 (rt_oracle.c shade_reflect), and the pixel's outputs.
+__global__ __launch_bounds__(256) void k_refl_fold(const FrameArgs fa, const WorkArgs wa, OutPlanes out,
+                                                   const uint32_t* __restrict__ chain) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    for (uint32_t q = 0; q < (uint32_t)kQShards; ++q) {
+        const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
+        for (uint32_t k = gw; k < nch; k += nw) {
+            const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
+            const HitRec& rec = wa.hits[slot];
+            if (rec.obj == kNoHit) continue;
+            const uint32_t st = chain[slot], L = (st & 0xffu) - 1;
+            auto level = [&](uint32_t l, RGB& ph, RGB& ks) {
+                uint32_t obj = rec.obj, mat = rec.mat;
+                if (l == 0) {
+                    ph = RGB{wa.ph0[3 * slot], wa.ph0[3 * slot + 1], wa.ph0[3 * slot + 2]};
+                } else {
+                    const double* e = wa.refl + ((size_t)(l - 1) * wa.refl_stride + slot) * kReflD;
+                    ph = RGB{e[0], e[1], e[2]};
+                    const uint64_t om = dbits(e[3]);
+                    obj = (uint32_t)om;
+                    mat = (uint32_t)(om >> 32);
+                }
+                const double* mt = fa.obj[obj].m.mats + (size_t)mat * 10;
+                ks = RGB{mt[6], mt[7], mt[8]};
+            };
+            RGB ph, ks;
+            level(L, ph, ks);
+            RGB c = (st >> 8) ? c_add(ph, c_mul(ks, RGB{0, 0, 0})) : ph;  // c_reflected = black
+            for (int l = (int)L - 1; l >= 0; --l) {
+                level((uint32_t)l, ph, ks);
+                c = c_add(ph, c_mul(ks, c));
+            }
+            const uint64_t oidx = rec.out;
+            if (out.rgb) {
+                out.rgb[3 * oidx] = c.r;
+                out.rgb[3 * oidx + 1] = c.g;
+                out.rgb[3 * oidx + 2] = c.b;
+            }
+            if (out.rgb8) {
+                out.rgb8[3 * oidx] = c_u8(c.r);
+                out.rgb8[3 * oidx + 1] = c_u8(c.g);
+                out.rgb8[3 * oidx + 2] = c_u8(c.b);
+            }
+            if (out.rgbv) out.rgbv[oidx] = pack_rgbv(c);
+        }
+    }
+    frame_fold(fa, wa);
+}
+
 // ---------------------------------------------------------------- arbitrary rays
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
@@ -2455,6 +2587,22 @@ hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
 #define K_REFLECT(P, B, R) hipLaunchKernelGGL((k_reflect<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, out)
     MIRT_DISPATCH(K_REFLECT);
 #undef K_REFLECT
+    return hipGetLastError();
+}
+
+hipError_t launch_bounce(const FrameArgs& fa, const WorkArgs& wa, const BounceArgs& ba, int grid, uint32_t opts,
+                         hipStream_t s) {
+    const bool resident = is_resident(fa);
+    const size_t dyn = resident ? mesh_lds_bytes(fa) : 0;
+#define K_BOUNCE(P, B, R) hipLaunchKernelGGL((k_bounce<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, fa, wa, ba)
+    MIRT_DISPATCH(K_BOUNCE);
+#undef K_BOUNCE
+    return hipGetLastError();
+}
+
+hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, const uint32_t* chain,
+                            int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_refl_fold, dim3(std::max(grid, 1)), dim3(256), 0, s, fa, wa, out, chain);
     return hipGetLastError();
 }
 

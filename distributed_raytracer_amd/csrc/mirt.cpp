@@ -98,6 +98,20 @@ struct Slot {
     size_t ph0_cap = 0;
     double* refl = nullptr;   // configs[4] reflections: per level and slot, phong + obj|mat
     size_t refl_cap = 0;
+    // configs[4] bounce waves (k_bounce): two level buffers used alternately, the levels'
+    // region counters, per origin slot the chain state
+    HitRec* lhits[2] = {nullptr, nullptr};
+    size_t lhits_cap[2] = {0, 0};
+    double* ldir[2] = {nullptr, nullptr};
+    size_t ldir_cap[2] = {0, 0};
+    uint32_t* llitw[2] = {nullptr, nullptr};
+    size_t llitw_cap[2] = {0, 0};
+    uint32_t* lblk[2] = {nullptr, nullptr};
+    size_t lblk_cap[2] = {0, 0};
+    cnt_t* lcnt = nullptr;    // [bounces][kCntN]
+    size_t lcnt_cap = 0;
+    uint32_t* chain = nullptr;
+    size_t chain_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
     size_t cost_cap = 0;
     cnt_t* counters = nullptr;
@@ -201,6 +215,9 @@ int slot_init(Slot* s) {
 
 void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (void* p : {(void*)s->lhits[0], (void*)s->lhits[1], (void*)s->ldir[0], (void*)s->ldir[1], (void*)s->llitw[0],
+                    (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
                     (void*)s->d_frames, (void*)s->views, (void*)s->view_heads})
@@ -601,6 +618,18 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         wa.ph0 = sl->ph0;
         wa.refl = sl->refl;
         wa.refl_stride = hit_slots;
+        wa.ph_out = sl->ph0;  // level 0 (k_shadow); the bounce levels set their own
+        wa.ph_stride = 3;
+        if (c->flags & MIRT_OPT_REFLECT_WAVES) {
+            for (int b = 0; b < 2; ++b) {
+                if ((r = dev_grow(sl->lhits[b], sl->lhits_cap[b], hit_slots)) != MIRT_OK) return r;
+                if ((r = dev_grow(sl->ldir[b], sl->ldir_cap[b], 3 * hit_slots)) != MIRT_OK) return r;
+                if ((r = dev_grow(sl->llitw[b], sl->llitw_cap[b], hit_slots)) != MIRT_OK) return r;
+                if ((r = dev_grow(sl->lblk[b], sl->lblk_cap[b], hit_slots / 64)) != MIRT_OK) return r;
+            }
+            if ((r = dev_grow(sl->lcnt, sl->lcnt_cap, (size_t)bounces * kCntN)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->chain, sl->chain_cap, hit_slots)) != MIRT_OK) return r;
+        }
     }
     if (one_launch && !getenv("MIRT_NO_COST_ORDER")) {
         const size_t cap0 = sl->cost_cap;
@@ -696,9 +725,39 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         // launched with no lights, to shade every hit with the ambient term
         HIP_TRY(launch_shadow(fa, wa, out, sgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
-        if (wa.bounces) {  // configs[4] extension: the frame's last kernel
+        if (wa.bounces && !(c->flags & MIRT_OPT_REFLECT_WAVES)) {  // configs[4] extension: the last kernel
             if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
             HIP_TRY(launch_reflect(fa, wa, out, sgrid, c->flags, s));
+        } else if (wa.bounces) {
+            // bounce waves: level lv's reflection rays (k_bounce), its shadow rays and phong
+            // (k_shadow on the level's records), then the fold of every chain (the last kernel)
+            HIP_TRY(hipMemsetAsync(sl->lcnt, 0, (size_t)wa.bounces * kCntN * sizeof(cnt_t), s));
+            for (uint32_t lv = 1; lv <= wa.bounces; ++lv) {
+                if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
+                const int ib = (int)(lv & 1u) ^ 1, ob = (int)(lv & 1u);  // level lv writes buffer lv % 2
+                BounceArgs ba{};
+                ba.in = lv == 1 ? sl->hits : sl->lhits[ib];
+                ba.in_dir = lv == 1 ? sl->dir0 : sl->ldir[ib];
+                ba.in_cnt = lv == 1 ? wa.counters : sl->lcnt + (size_t)(lv - 2) * kCntN;
+                ba.out = sl->lhits[ob];
+                ba.out_dir = sl->ldir[ob];
+                ba.out_cnt = sl->lcnt + (size_t)(lv - 1) * kCntN;
+                ba.out_litw = sl->llitw[ob];
+                ba.out_blkdone = sl->lblk[ob];
+                ba.chain = sl->chain;
+                ba.level = lv;
+                HIP_TRY(launch_bounce(fa, wa, ba, sgrid, c->flags, s));
+                WorkArgs wl = wa;
+                wl.hits = sl->lhits[ob];
+                wl.litw = sl->llitw[ob];
+                wl.blkdone = sl->lblk[ob];
+                wl.qcounters = ba.out_cnt;
+                wl.ph_out = sl->refl + (size_t)(lv - 1) * hit_slots * kReflD;
+                wl.ph_stride = kReflD;
+                wl.ph_by_origin = 1;
+                HIP_TRY(launch_shadow(fa, wl, out, sgrid, c->flags, s));
+            }
+            HIP_TRY(launch_refl_fold(fa, wa, out, sl->chain, (int)std::min<uint64_t>(4 * c->cus, 4096), s));
         }
     }
     sl->dirty = false;

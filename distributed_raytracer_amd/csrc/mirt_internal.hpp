@@ -278,6 +278,13 @@ struct WorkArgs {
     // first)
     double* refl;
     uint64_t refl_stride;  // slots per level
+    // bounces, k_shadow's phong: slot s's colour goes to ph_out + ps * ph_stride with ps = s, or
+    // ps = the record's `out` (the origin slot of a bounce level's record, ph_by_origin)
+    double* ph_out;
+    uint32_t ph_stride, ph_by_origin;
+    // k_shadow's region hit counts and queue tickets (cnt_hits, cnt_queue; nullptr: `counters`):
+    // a bounce level's records have counters of their own, its statistics go to `counters`
+    cnt_t* qcounters;
     cnt_t* counters;
     cnt_t* counters_next;  // the other set: zeroed by k_primary for the next frame
     FrustumArgs fr;
@@ -301,6 +308,23 @@ struct WorkArgs {
     uint16_t* block_cost;
     uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
     uint32_t view_pad;
+};
+// Reflections in waves of bounces (configs[4] extension, kernels.hip k_bounce): level lv's
+// hit records form region sets like the primary's (kQShards regions of hit_cap slots, region
+// q holding cnt_hits(q) records of its counters, packed from the front), each record's `out`
+// the origin slot (the primary hit slot whose chain it continues).
+struct BounceArgs {
+    const HitRec* in;       // level lv - 1 (lv == 1: the primary hit slots)
+    const double* in_dir;   // per input slot: the ray that reached the hit (3 doubles)
+    const cnt_t* in_cnt;    // the input's region counts (lv == 1: the frame's counters)
+    HitRec* out;            // level lv
+    double* out_dir;
+    cnt_t* out_cnt;         // zeroed before the launch
+    uint32_t* out_litw;
+    uint32_t* out_blkdone;
+    uint32_t* chain;        // per origin slot: levels with a phong value | missed << 8
+    uint32_t level;
+    uint32_t pad;
 };
 constexpr int kTimelineRec = 8;
 constexpr int kReflD = 4;  // doubles per slot and level of WorkArgs::refl
@@ -331,6 +355,10 @@ hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint3
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
+hipError_t launch_bounce(const FrameArgs& fa, const WorkArgs& wa, const BounceArgs& ba, int grid, uint32_t opts,
+                         hipStream_t s);
+hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, const uint32_t* chain,
+                            int grid, hipStream_t s);
 hipError_t read_diag_counters(uint64_t* out, uint32_t n);  // MIRT_DIAG builds (zeros otherwise)
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
 struct RectJobs {  // k_pack_rect / k_unpack_rect / k_check_regions: per frame of a batch

@@ -45,6 +45,30 @@ def test_reflections_full_frame_bit_exact(ctx, env, py_scene, bounces):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bounces", [1, 4])
+def test_reflection_waves_full_frame_bit_exact(ctx, env, py_scene, bounces):
+    """MIRT_OPT_REFLECT_WAVES (level by level, packed rays: k_bounce, k_shadow per level,
+    k_refl_fold) gives the chains' frames and ray counts bit for bit."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib as L
+    mut = dataclasses.replace(env.mutable(), max_bounces=bounces)
+    ctx.set_options(L.MIRT_OPT_REFLECT_WAVES)
+    try:
+        ctx.profile_enable(True)
+        fb = rt.draw(env, 320, 240, mut)
+        p = ctx.profile_read()
+        ctx.profile_enable(False)
+    finally:
+        ctx.set_options(0)
+    ref = _oracle(py_scene, bounces).frame(320, 240, nthreads=8)
+    assert np.array_equal(fb.valid, ref["valid"])
+    assert np.array_equal(fb.rgb, ref["rgb"]), f"{(fb.rgb != ref['rgb']).any(axis=1).sum()} pixels differ"
+    assert np.array_equal(fb.rgb8, ref["rgb8"])
+    assert p["reflection_rays"] == ref["stats"]["reflection_rays"]
+    assert p["shadow_rays"] == ref["stats"]["shadow_rays"] and p["stack_overflows"] == 0
+
+
+@pytest.mark.gpu
 def test_reflections_multi_object(ctx, py_scene):
     import distributed_raytracer_amd as rt
     from scenes import gpu_env, multi_object_scene
