@@ -1,5 +1,5 @@
 """The bench line's contract (the task's bench.py rules) on the committed
-bench lines of this round, and the consistency of the committed profile they cite.  CPU
+bench lines of this round, and the consistency of the committed profiles they cite.  CPU
 only: reads profiles/, runs nothing on a GPU."""
 import json
 import os
@@ -7,7 +7,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINES = ["profiles/r02_bench_driver_cmd.log", "profiles/r02_bench_default.log"]
+DRIVER = "profiles/r03_bench_driver_cmd.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
+LINES = [DRIVER, "profiles/r03_bench_default.log", "profiles/r03_bench_orbit.log"]
 
 
 def _line(path):
@@ -23,35 +24,59 @@ def _line(path):
 def test_bench_line_contract(path):
     d = _line(path)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
         assert k in d, k
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
     assert d["metric"] == base["metric"]
     assert d["unit"] == "Mrays/s" and d["higher_is_better"] is True and d["dtype"] == "f64"
     assert d["vs_baseline"] is None  # BASELINE.md publishes no number for this metric
     assert "workload" in d["config"] and "model" not in d["config"]
+    # value = rays per frame / ms per frame with the D2H
+    assert abs(d["value"] - d["rays_per_frame"] / d["ms_per_step"] / 1e3) / d["value"] < 2e-3
+    assert abs(d["device_mrays_s"] - d["rays_per_frame"] / d["device_ms_per_frame"] / 1e3) / d["value"] < 2e-3
     r = d["roofline"]
-    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "source", "algorithmic"):
         assert k in r, k
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
-    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
-    c = d["cpu_baseline"]
+    # the physical roof: VALU-busy SIMD cycles per frame (committed PMC of this command's shape)
+    assert r["bound"] == "valu" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert abs(r["achieved"] - r["valu_busy_cycles_per_frame"] / (d["ms_per_step"] * 1e-3) / 1e9) / r["achieved"] < 2e-3
+    assert os.path.exists(os.path.join(ROOT, r["source"])) and isinstance(r["traffic"], int)
+    a = r["algorithmic"]
+    assert a["bound"] == "hbm" and a["unit"] == "GB/s" and a["bytes_per_unit"] == 72
+    assert ("LDS-resident" in a["kind"]) == (d["config"]["triangles"] <= 1024)
+    assert d["parity"]["bit_exact"] is True and d["parity"]["pixels_checked"] == d["config"]["width"] * d["config"]["height"]
+
+
+def test_driver_line_cpu_baseline():
+    c = _line(DRIVER)["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
     assert c["kind"] in ("port", "reference") and c["cores"] >= 1
-    # value is the device-resident rate: rays per frame / device ms per frame
-    assert abs(d["value"] - d["rays_per_frame"] / d["device_ms_per_frame"] / 1e3) / d["value"] < 2e-3
-    assert d["parity"]["bit_exact"] is True and d["parity"]["pixels_checked"] == 1920 * 1080
 
 
-def test_driver_line_cites_the_committed_profile():
-    """The driver-command line's physical roofs come from profiles/r02_roofline.json of the
-    same launch shape, and the roofline recomputed from that file is within 5% of the line."""
-    d = _line(LINES[0])
-    prof = json.load(open(os.path.join(ROOT, "profiles", "r02_roofline.json")))
-    assert d["steps"] == prof["shape"]["steps"] and d["warmup"] == prof["shape"]["warmup"]
-    assert d["frames_in_flight"] == prof["shape"]["inflight"] and d["frames_per_launch"] == prof["shape"]["batch"]
-    assert d["roofs"]["source"] == "profiles/r02_roofline.json"
-    assert d["roofs"]["valu_insts_per_frame"] == int(prof["sq_insts_valu_per_launch"] / prof["frames_per_launch"])
+@pytest.mark.parametrize("path", LINES)
+def test_line_cites_the_committed_profile_of_its_shape(path):
+    """Each line's roofline comes from the profile of its own launch shape, and the fraction
+    recomputed from that file is within 5% of the line's."""
+    d = _line(path)
+    r = d["roofline"]
+    prof = json.load(open(os.path.join(ROOT, r["source"])))
+    sh = prof["shape"]
+    assert d["steps"] == sh["steps"] and d["warmup"] == sh["warmup"] and d["n_gpus"] == sh["gpus"]
+    assert d["frames_in_flight"] == sh["inflight"] and d["frames_per_launch"] == sh["batch"]
+    assert d["config"]["scene"] == sh["scene"] and d["config"]["camera"] == sh["camera"]
+    assert d["config"]["bounces"] == sh["bounces"] and d["config"]["options"] == sh["options"]
+    assert r["valu_busy_cycles_per_frame"] == int(prof["valu_busy_simd_cycles_per_launch"] / prof["frames_per_launch"])
     rt = prof["roofline_from_trace"]
-    assert abs(rt["frac"] - rt["bench_frac"]) / rt["frac"] < 0.05
+    assert abs(rt["frac_over_trace_ms_per_step"] - r["frac"]) / r["frac"] < 0.05
+    assert abs(rt["frac_over_timed_kernel_span"] - r["frac"]) / r["frac"] < 0.15
+
+
+def test_profiles_carry_per_region_kernel_summaries():
+    """profiles/<tag>_kernel_regions.csv: every frame kernel's launches per bench region."""
+    import csv
+    d = _line(DRIVER)
+    prof = json.load(open(os.path.join(ROOT, d["roofline"]["source"])))
+    rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", prof["tag"] + "_kernel_regions.csv"))))
+    regions = {r["region"]: int(r["launches"]) for r in rows if r["kernel"] == "k_trace"}
+    assert regions == {k: v for k, v in d["launches"].items() if v}
