@@ -35,6 +35,7 @@ MIRT_OPT_NO_FRUSTUM = 64
 MIRT_OPT_NO_OCTANT = 128
 MIRT_OPT_VIEWS = 256
 MIRT_OPT_REFLECT_WAVES = 512
+MIRT_OPT_NO_LIGHT_TABLE = 1024
 
 D3 = C.c_double * 3
 
@@ -151,6 +152,7 @@ SIGNATURES = {
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_debug_counters": (C.c_int, [_P, _P, C.c_uint32]),
+    "mirt_debug_light_table": (C.c_int, [_P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, _P]),
     "mirt_unpack_tiles_at_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "mirt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "mirt_scene_free": (None, [_P]),

@@ -268,16 +268,73 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
     return true;
 }
 
+// Shadow segments' fp32 pre-classification against a light table.  A
+// shadow ray runs along the line through its light L: o = L - lam d + eps, |eps| tiny.
+// For the triangle (P1, P1 + E1, P1 + E2) and V_i = P_i - L, the reference's barycentric
+// quotients are r_k = m_k / a with m_k = d . W_k (W_1 = V_2 x V_3, W_2 = V_3 x V_1,
+// W_3 = V_1 x V_2) and a = d . A, A = E1 x E2 (so inc = -a), and its t numerator is
+// nt = A . (o - P1) = ntL - lam a with ntL = A . (L - P1).  The light table holds W_1..3,
+// A, ntL and error bounds per (light, triangle) in fp32, computed on the host (mirt.cpp
+// light_records); the kernel forms m_k, a and nt with a few fp32 FMAs and rejects a lane
+// only when the bounds prove that the fp64 test of triangle.go:37-77 fails:
+//   |a| > Ea and some m_k certainly of the other sign (a barycentric < 0), or nt certainly
+//   of a's sign (t < 0);   E = |d|_inf cw, Ea = |d|_inf cA, Et = 2 |lam| |d|_inf cA + ctL
+//   (nt's error from lam a is at most 7 ulp of |lam| |d|_inf |A|_1; cA holds 10).
+// A wave whose lanes are all rejected skips the triangle; the others run the fp64 test
+// unchanged on the lanes not rejected, so the results are the same bits.
+struct SegPre {
+    float dx, dy, dz;  // d in fp32
+    float ninf;        // |d|_inf
+    float lam, lamn;   // lam = |L - hit| - 1e-4, 2 |lam| |d|_inf
+};
+__device__ __forceinline__ SegPre seg_pre(V3 d, double lh) {
+    SegPre p;
+    p.dx = (float)d.x;
+    p.dy = (float)d.y;
+    p.dz = (float)d.z;
+    p.ninf = fmaxf(fmaxf(fabsf(p.dx), fabsf(p.dy)), fabsf(p.dz));
+    p.lam = (float)(lh - 1e-4);
+    p.lamn = 2.0f * fabsf(p.lam) * p.ninf;
+    return p;
+}
+__device__ __forceinline__ float dot32(const float* w, const SegPre& p) {
+    return __builtin_fmaf(w[2], p.dz, __builtin_fmaf(w[1], p.dy, w[0] * p.dx));
+}
+// true: the fp64 test of this lane certainly fails (see SegPre).  w: the record in SGPRs.
+__device__ __forceinline__ bool seg_reject(const SegPre& p, const float* w) {
+    const float m1 = dot32(w, p), m2 = dot32(w + 3, p), m3 = dot32(w + 6, p), a = dot32(w + 9, p);
+    const float E = p.ninf * w[13], Ea = p.ninf * w[14];
+    const float nt = __builtin_fmaf(-p.lam, a, w[12]);
+    const float Et = __builtin_fmaf(p.lamn, w[14], w[15]);
+    const float lo = fminf(fminf(m1, m2), m3), hi = fmaxf(fmaxf(m1, m2), m3);
+    const bool pos = (a > Ea) & ((lo < -E) | (nt > Et));
+    const bool neg = (a < -Ea) & ((hi > E) | (nt < -Et));
+    return pos | neg;
+}
+
 // Test n triangles at positions pos0.. of the BVH-ordered arrays; `src` points at the
 // record of position pos0 (in LDS or in HBM).
+//   lt (shadow segments; NULL: none): the light table at position pos0 (kLtD floats per
+//   triangle), sp the lane's SegPre, live the lanes whose result still matters.
 template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
-                                           uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests) {
+                                           uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests,
+                                           const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
     if (MIRT_EXP_NO_TRI_TESTS || (MIRT_EXP_NO_SHADOW_TESTS && TPRE)) return;
-#pragma unroll 2
-    for (uint32_t i = 0; i < n; ++i) {
+    auto one = [&](uint32_t i) {
         const uint32_t k = pos0 + i;
+        bool maybe = true;
+        if (TPRE && PREFILTER && lt) {  // wave-uniform
+            const u32x16 a16 = ((cv16ptr)(lt + (size_t)i * kLtD))[0];  // one s_load_dwordx16
+            float w[kLtD];
+#pragma unroll
+            for (int q = 0; q < kLtD; ++q) w[q] = __uint_as_float(a16[q]);
+            maybe = live && !seg_reject(*sp, w);
+            diag(22);  // light-table classifications (shadow)
+            // every lane rejected: the wave skips the triangle (its fp64 record is not read)
+            if (__ballot(maybe) == 0) return;
+        }
         const auto t = src + (size_t)i * kTriD;
         V3 p1or = REL ? V3{t[0], t[1], t[2]} : sub(ro, V3{t[0], t[1], t[2]});
         V3 e1{t[3], t[4], t[5]};
@@ -285,10 +342,20 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         double tt;
         // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
         const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
-        if (mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt)) {
+        if (maybe && mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt)) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
         }
+    };
+    if (TPRE) {
+        // unrolled by two by hand: a loop holding a ballot is not runtime-unrolled
+        for (uint32_t i = 0; i < n; i += 2) {
+            one(i);
+            if (i + 1 < n) one(i + 1);
+        }
+    } else {
+#pragma unroll 2
+        for (uint32_t i = 0; i < n; ++i) one(i);
     }
 }
 
@@ -555,7 +622,8 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 // argument needs a bounded origin) enter every child.
 template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
-                                          Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true) {
+                                          Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true,
+                                          const float* lt = nullptr, const SegPre* sp = nullptr) {
     // LDS-resident meshes (the host guarantees depth <= kBvhShallowDepth) use a one-VGPR stack
     constexpr bool DEEP = !__is_same(SrcPtr, const double*);
     const Ray32 r = ray32(ro, d);
@@ -574,7 +642,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             ++vis.leaves;
             diag(SEG ? 14 : 6);
             test_range<REL, PREFILTER, SEG ? 8 : 0, SEG>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
-                                                    vis.tests);
+                                                    vis.tests, lt ? lt + (size_t)first * kLtD : nullptr, sp, live);
             if (SEG) {
                 live = live && !(b.has && b.d < resolve);
                 if (__ballot(live) == 0) break;
@@ -1008,8 +1076,8 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
 //   vt / vh (LDS-resident): the light's view table and header (view_sweep from the light).
 template <bool PREFILTER>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
-                                                  uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, bool lane_on,
-                                                  Visits& vis, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                                  uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, uint32_t li,
+                                                  bool lane_on, Visits& vis, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
                                                   const ViewHead* vh = nullptr) {
     const DevObject& ob = fa.obj[0];
     const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
@@ -1069,12 +1137,17 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
         view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b, vis,
                                     resolve, tmax);
-    } else if (resident) {
-        bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                          !(fa.flags & MIRT_OPT_NO_OCTANT));
     } else {
-        bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                          !(fa.flags & MIRT_OPT_NO_OCTANT));
+        // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
+        const float* lt = fa.ltab ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
+        SegPre sp;
+        if (lt) sp = seg_pre(d, lh);
+        if (resident)
+            bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                              !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
+        else
+            bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                              !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
     }
     if (b.has && b.d < resolve) return false;
     // the nearest candidate (not a NaN-distance first hit, which wins regardless) lies beyond
@@ -1717,7 +1790,7 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
             vh = view_lookup(wa, q, *vc);
             if (vh) vt = wa.views + (size_t)q * wa.view_leaves;
         }
-        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, active, vis, vt, wa.view_leaves,
+        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, vt, wa.view_leaves,
                                               vh);
     } else {
         Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis);
@@ -2209,7 +2282,7 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
                     Visits sv{0, 0, 0, 0};
                     bool is_lit;
                     if (segment) {
-                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, on, sv);
+                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, on, sv);
                     } else {
                         const Nearest sr = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, on, false, sv);
                         is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));

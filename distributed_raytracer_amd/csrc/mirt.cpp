@@ -58,6 +58,7 @@ struct MeshDev {
     uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
     Bvh8Node root{};     // host copy of the BVH root (frustum pre-test rectangles)
+    std::vector<double> htri;  // host copy of `tri` (light tables)
     bool has_normals = false;
     bool live = false;
 };
@@ -170,6 +171,17 @@ struct mirt_ctx {
     cnt_t* prof_acc = nullptr;     // kStatN device totals accumulated while profiling
     uint64_t* timeline = nullptr;  // MIRT_OPT_TIMELINE buffer (2 kernels x timeline_cap waves)
     uint32_t timeline_cap = 0;
+    // light tables of one-object frames (light_table), kept for the context's life: frames in
+    // flight may read any of them
+    struct LightTab {
+        uint32_t mesh, nl;
+        double pos[3];
+        double lpos[MIRT_MAX_LIGHTS][3];
+        float* d;
+    };
+    std::mutex lt_mu;
+    std::vector<LightTab> ltabs;
+    size_t ltab_bytes = 0;
 };
 
 namespace {
@@ -525,10 +537,108 @@ int check_tiles(uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n, uint
     return MIRT_OK;
 }
 
+// light_table's records (host only): nl lights x n triangles of T (kTriD doubles each).
+void light_records(const double* T, uint32_t n, double scale, const double pos[3], const double (*lpos)[3], uint32_t nl,
+                   float* out) {
+    auto n1 = [](const double* v) { return std::fabs(v[0]) + std::fabs(v[1]) + std::fabs(v[2]); };
+    auto cross = [](const double* a, const double* b, double* r) {
+        r[0] = a[1] * b[2] - a[2] * b[1];
+        r[1] = a[2] * b[0] - a[0] * b[2];
+        r[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    auto up = [](double x) { return std::nextafter((float)x, INFINITY); };
+    const double R = 2.0 * std::sqrt(3.0) * scale + 1.0;  // |hit| in object space, with slack
+    const double pinf = std::max(std::max(std::fabs(pos[0]), std::fabs(pos[1])), std::fabs(pos[2]));
+    for (uint32_t l = 0; l < nl; ++l) {
+        double Lo[3];
+        for (int q = 0; q < 3; ++q) Lo[q] = lpos[l][q] - pos[q];
+        const double Lh = std::sqrt(Lo[0] * Lo[0] + Lo[1] * Lo[1] + Lo[2] * Lo[2]) + R;  // >= |L - hit|
+        const double Mmax = 0x1p-36 * (2.0 + Lh + pinf + R);  // >= the kernel's M (shadow_lit_single)
+        for (uint32_t k = 0; k < n; ++k) {
+            const double* t = T + (size_t)k * kTriD;
+            double V[3][3], W[3][3], A[3], e21[3];
+            for (int q = 0; q < 3; ++q) {
+                V[0][q] = t[q] - Lo[q];
+                V[1][q] = V[0][q] + t[3 + q];
+                V[2][q] = V[0][q] + t[6 + q];
+                e21[q] = t[6 + q] - t[3 + q];
+            }
+            cross(V[1], V[2], W[0]);
+            cross(V[2], V[0], W[1]);
+            cross(V[0], V[1], W[2]);
+            cross(t + 3, t + 6, A);
+            const double ntL = -(A[0] * V[0][0] + A[1] * V[0][1] + A[2] * V[0][2]);
+            const double G = std::max(std::max(n1(V[0]), n1(V[1])), n1(V[2]));
+            const double Ed = std::max(std::max(n1(t + 3), n1(t + 6)), n1(e21));
+            const double Wm = std::max(std::max(n1(W[0]), n1(W[1])), n1(W[2]));
+            const double cw = 1.25 * (0x1p-21 * Wm + 0x1p-36 * (G + Lh) * (G + Ed) + 4.0 * Mmax * Ed) + 0x1p-100;
+            const double cA = 1.25 * (0x1p-21 * n1(A) + 0x1p-44 * Ed * Ed) + 0x1p-100;
+            const double ctL = 1.25 * (0x1p-22 * std::fabs(ntL) + n1(A) * Mmax + 0x1p-36 * (G + Lh) * Ed * Ed) + 0x1p-100;
+            float* r = out + ((size_t)l * n + k) * kLtD;
+            for (int w = 0; w < 3; ++w)
+                for (int q = 0; q < 3; ++q) r[3 * w + q] = (float)W[w][q];
+            for (int q = 0; q < 3; ++q) r[9 + q] = (float)A[q];
+            r[12] = (float)ntL;
+            r[13] = up(cw);
+            r[14] = up(cA);
+            r[15] = up(ctL);
+        }
+    }
+}
+
+// The light table of a one-object frame's shadow segments (kernels.hip SegPre, DESIGN.md
+// §4.3): per light l and BVH position k, with V_i = P_i - L (object space; P2 = P1 + E1,
+// P3 = P1 + E2 as the test sees them), the fp32 record
+//   W1 = V2 x V3, W2 = V3 x V1, W3 = V1 x V2, A = E1 x E2, ntL = A . (L - P1), cw, cA, ctL.
+// cw bounds, per unit |d|_inf, the error of every m_k = d . W_k the kernel forms in fp32
+// against the exact quotient numerators of the fp64 test (fp32 rounding of W, d and the dot:
+// at most 5 ulp of sum |d_i W_i|, bounded by 2^-21 = 8 ulp of |d|_inf |W|_1; the fp64 test's own rounding and the host's, 2^-36 (G + Lh)
+// (G + Ed); the shadow origin's distance from the line through L, |eps| <= M, and M's
+// bound over every hit on the mesh: 4 Mmax Ed), plus 2^-100 against underflow; cA the same
+// for a = d . A against -inc; ctL for nt's terms that do not scale with lam.  Rounded up.  Built on the host once per
+// (mesh, object position, lights) and kept for the context's life; past kLightTabBytes of
+// tables (scenes whose lights or object move every frame) new keys get NULL and trace
+// without the pre-classification.
+constexpr size_t kLightTabBytes = (size_t)2 << 30;
+const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) {
+    if (fa.n_objects != 1 || fa.n_lights == 0 ||
+        (fa.flags & (MIRT_OPT_NO_PREFILTER | MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_SEGMENT | MIRT_OPT_NO_LIGHT_TABLE)))
+        return nullptr;
+    const uint32_t mid = f->objects[0].mesh_id;
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (const auto& t : c->ltabs)
+        if (t.mesh == mid && t.nl == fa.n_lights && !memcmp(t.pos, fa.obj[0].pos, sizeof(t.pos)) &&
+            !memcmp(t.lpos, fa.lpos, sizeof(double) * 3 * fa.n_lights))
+            return t.d;
+    const MeshDev& m = c->meshes[mid];
+    const uint32_t n = m.ntri, nl = fa.n_lights;
+    if (n == 0 || m.htri.size() != (size_t)n * kTriD) return nullptr;
+    const size_t bytes = (size_t)nl * n * kLtD * sizeof(float);
+    if (c->ltab_bytes + bytes > kLightTabBytes) return nullptr;
+    std::vector<float> h((size_t)nl * n * kLtD);
+    light_records(m.htri.data(), n, m.scale, fa.obj[0].pos, fa.lpos, nl, h.data());
+    const double* pos = fa.obj[0].pos;
+    mirt_ctx::LightTab lt{};
+    lt.mesh = mid;
+    lt.nl = nl;
+    memcpy(lt.pos, pos, sizeof(lt.pos));
+    memcpy(lt.lpos, fa.lpos, sizeof(double) * 3 * nl);
+    if (hipSetDevice(c->device) != hipSuccess || hipMalloc((void**)&lt.d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(lt.d, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(lt.d);
+        return nullptr;
+    }
+    c->ltabs.push_back(lt);
+    c->ltab_bytes += bytes;
+    return lt.d;
+}
+
 // One frame's launch record: its arguments, output planes and frustum rectangles.
 void frame_record(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const OutPlanes& out, FrameRec& rec,
                   uint64_t& tris) {
     fill_args(c, f, W, H, rec.fa, tris);
+    rec.fa.ltab = light_table(const_cast<mirt_ctx*>(c), f, rec.fa);
+    rec.fa.ltab_n = rec.fa.ltab ? c->meshes[f->objects[0].mesh_id].ntri : 0;
     frustum_args(c, f, rec.fa, rec.fr);
     rec.out = out;
     rec.live[0] = rec.live[1] = 0;  // every block (a frame group narrows it to the hit rectangle)
@@ -824,6 +934,7 @@ void mirt_destroy(mirt_ctx* c) {
                 if (e) (void)hipEventDestroy(e);
         }
     for (auto& m : c->meshes) mesh_free(m);
+    for (auto& t : c->ltabs) (void)hipFree(t.d);
     if (c->timeline) (void)hipFree(c->timeline);
     if (c->prof_acc) (void)hipFree(c->prof_acc);
     delete c;
@@ -996,10 +1107,11 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         mesh_free(md);
         return r;
     }
+    md.htri = std::move(tri);
     md.live = true;
     std::lock_guard<std::mutex> g(c->mu);
     *mesh_id = (uint32_t)c->meshes.size();
-    c->meshes.push_back(md);
+    c->meshes.push_back(std::move(md));
     return MIRT_OK;
 }
 
@@ -1264,6 +1376,13 @@ int mirt_debug_timeline(mirt_ctx* c, uint64_t* out, uint32_t max_records) {
         ++n;
     }
     return (int)n;
+}
+
+int mirt_debug_light_table(const double* tri, uint32_t n, double scale, const double pos[3], const double* lights,
+                           uint32_t nl, float* out) {
+    if ((n && !tri) || !pos || (nl && !lights) || (n && nl && !out)) return fail(MIRT_E_INVALID, "NULL argument");
+    light_records(tri, n, scale, pos, (const double(*)[3])lights, nl, out);
+    return MIRT_OK;
 }
 
 int mirt_debug_counters(mirt_ctx* c, uint64_t* out, uint32_t n) {

@@ -21,6 +21,9 @@ constexpr int kWgPerCu = kWG >= 768 ? 1 : 2;
 constexpr int kBlk = 8;
 // Doubles per triangle record in HBM and LDS: P1, E1 = P2-P1, E2 = P3-P1 (72 B).
 constexpr int kTriD = 9;
+// Floats per light-table record (shadow segments, kernels.hip SegPre): W1, W2, W3, A, ntL,
+// cw, cA, ctL (64 B: one scalar load).
+constexpr int kLtD = 16;
 // Triangles one workgroup holds in LDS (73,728 B; two workgroups per CU fit in 160 KiB).
 // Meshes up to this size stay resident in LDS for the life of a persistent workgroup;
 // larger meshes stream through it in batches of this size.
@@ -152,6 +155,10 @@ struct FrameArgs {
     DevObject obj[MIRT_MAX_OBJECTS];
     double lpos[MIRT_MAX_LIGHTS][3];
     double lcol[MIRT_MAX_LIGHTS][3];
+    // shadow segments of one-object frames: obj[0]'s light table, kLtD floats per light and
+    // BVH position (kernels.hip SegPre, mirt.cpp light_table); NULL: no fp32 pre-classification
+    const float* ltab;
+    uint32_t ltab_n, ltab_pad;  // records per light (= obj[0]'s ntri)
 };
 
 struct TileDesc {

@@ -244,6 +244,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_NO_OCTANT 128u     /* generic child-box test (no sign-octant variants; same decisions) */
 #define MIRT_OPT_VIEWS 256u         /* per-frame view tables instead of the BVH walk (same results; slower) */
 #define MIRT_OPT_REFLECT_WAVES 512u /* reflections level by level with packed rays (k_bounce; same results; slower) */
+#define MIRT_OPT_NO_LIGHT_TABLE 1024u /* shadow segments without the fp32 light-table pre-classification (same results) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 /*
  * Launch shape of the frame kernel: every workgroup owns at least min_blocks_per_wg 8x8
@@ -287,9 +288,21 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
  * primary / nearest-hit sweeps, base 8: shadow segment sweeps) [base+0] triangle tests
  * entered, [+1] past inc != 0 and the r2 pre-reject, [+2] past the r2 range check,
  * [+3] past the r3 / r2+r3 / r1 checks, [+4] hits (t >= 0); [5] / [13] BVH node visits,
- * [6] / [14] leaves tested.  Synchronises the device; n <= 32.
+ * [6] / [14] leaves tested, [15] shadow tests past the t pre-test, [22] shadow tests
+ * pre-classified against a light table (those skipped by the wave: [22] - [8]).
+ * Synchronises the device; n <= 32.
  */
 int mirt_debug_counters(mirt_ctx *ctx, uint64_t *out, uint32_t n);
+
+/*
+ * Diagnostic (host only, no device): the light-table records the library builds for the
+ * shadow segments of a one-object frame (kernels.hip SegPre): for n triangles given as
+ * P1, E1 = P2 - P1, E2 = P3 - P1 (9 doubles each, the kernels' order), a mesh whose
+ * largest |coordinate| is scale, the object at pos and nl lights, writes nl * n records of
+ * 16 floats (W1, W2, W3, A, ntL, cw, cA, ctL) into out.  Lets host tests check the bounds.
+ */
+int mirt_debug_light_table(const double *tri, uint32_t n, double scale, const double pos[3], const double *lights,
+                           uint32_t nl, float *out);
 
 /*
  * Multi-GPU frames (one process per GPU of a box; SURVEY.md §8(b) mirt_trace_frame).  The

@@ -78,7 +78,7 @@ def _variants(ctx, fn):
                      rt._lib.MIRT_OPT_BRUTE_FORCE | rt._lib.MIRT_OPT_NO_PREFILTER,
                      rt._lib.MIRT_OPT_STATIC_SCHEDULE, rt._lib.MIRT_OPT_NO_SEGMENT,
                      rt._lib.MIRT_OPT_SPLIT_KERNELS, rt._lib.MIRT_OPT_SPLIT_KERNELS | rt._lib.MIRT_OPT_BRUTE_FORCE,
-                     rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_VIEWS):
+                     rt._lib.MIRT_OPT_NO_FRUSTUM, rt._lib.MIRT_OPT_VIEWS, rt._lib.MIRT_OPT_NO_LIGHT_TABLE):
             ctx.set_options(opts)
             out[opts] = fn()
     finally:
@@ -173,12 +173,60 @@ def test_shadow_segments_exact_with_lights_near_surfaces(ctx, env):
         mut = rt.EnvMutables(base.objects, lights, base.cam)
         res = {}
         for opts in (0, rt._lib.MIRT_OPT_BRUTE_FORCE, rt._lib.MIRT_OPT_NO_SEGMENT, rt._lib.MIRT_OPT_SPLIT_KERNELS,
-                     rt._lib.MIRT_OPT_VIEWS):
+                     rt._lib.MIRT_OPT_VIEWS, rt._lib.MIRT_OPT_NO_LIGHT_TABLE):
             ctx.set_options(opts)
             res[opts] = rt.draw(env, 320, 240, mut)
         ctx.set_options(0)
         assert res[0].valid.sum() > 1000
         _same_frames(res)
+
+
+def test_light_table_exact_for_light_placements(ctx, env):
+    """The shadow segments' fp32 light-table pre-classification (kernels.hip SegPre) never
+    changes a pixel: lights far away, on vertices, 1e-6 and 1e-3 off vertices and edge
+    midpoints, on the mesh's face planes, inside the mesh, and an object moved off the
+    origin; full 640x480 frames from two cameras, default vs MIRT_OPT_NO_LIGHT_TABLE vs
+    brute force, bit-exact."""
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    mesh = env.meshes[0]
+    rng = np.random.default_rng(23)
+    v = np.asarray(mesh.vertices, np.float64).reshape(-1, 3)
+    fv = np.asarray(mesh.face_v, np.int64).reshape(-1, 3)
+    obj_pos = np.asarray(base.objects[0].pos, np.float64)
+    col = (1.0, 200 / 255, 100 / 255)
+    for trial in range(6):
+        pts = []
+        f = fv[rng.integers(len(fv), size=4)]
+        a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+        nrm = np.cross(b - a, c - a)
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        pts.append(a[0])                                   # on a vertex
+        pts.append(0.5 * (a[1] + b[1]) + 1e-6 * nrm[1])    # just off an edge midpoint
+        pts.append((a[2] + b[2] + c[2]) / 3 + 1e-3 * nrm[2])
+        pts.append(a[3] + 2.0 * (b[3] - a[3]))             # in a face's plane, outside the face
+        pts.append(rng.normal(scale=0.2, size=3))          # inside / near the mesh
+        pts.append(rng.normal(scale=30.0, size=3))         # far away
+        objs = base.objects
+        if trial >= 4:  # the object off its scene position (object space != world space)
+            objs = [dataclasses_replace(o, pos=tuple(float(x) for x in obj_pos + rng.normal(scale=0.5, size=3)))
+                    for o in base.objects]
+        opos = np.asarray(objs[0].pos, np.float64)
+        lights = [rt.Light(tuple(float(x) for x in p + opos), col) for p in pts]
+        for cam in (base.cam, rt.Camera.new(tuple(opos + [2.5, 1.5, 2.0]), tuple(-np.array([2.5, 1.5, 2.0])), 0.9)):
+            mut = rt.EnvMutables(objs, lights, cam)
+            res = {}
+            for opts in (0, rt._lib.MIRT_OPT_NO_LIGHT_TABLE, rt._lib.MIRT_OPT_BRUTE_FORCE):
+                ctx.set_options(opts)
+                res[opts] = rt.draw(env, 640, 480, mut)
+            ctx.set_options(0)
+            assert res[0].valid.sum() > 1000
+            _same_frames(res)
+
+
+def dataclasses_replace(o, **kw):
+    import dataclasses
+    return dataclasses.replace(o, **kw)
 
 
 def test_view_tables_exact_for_light_and_camera_placements(ctx, env):

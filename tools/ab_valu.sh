@@ -1,15 +1,18 @@
 #!/bin/bash
 # VALU / SALU instructions per k_trace launch (one PMC pass of the driver's command per
 # library build; every launch traces the same static frame) and the bench line of each.
-#   tools/ab_valu.sh libA.so libB.so ...   (libs under distributed_raytracer_amd/)
+#   tools/ab_valu.sh libA.so libB.so@--bench-flag ...   (libs under distributed_raytracer_amd/;
+#   text after @: extra bench arguments of that variant)
 export TMPDIR=/tmp
 OUT=gpurun_out/ab_valu
 mkdir -p $OUT
-for L in "$@"; do
+for V in "$@"; do
+  L=${V%%@*}; X=""; [[ "$V" == *@* ]] && X=${V#*@}
+  N=$L${X// /}
   MIRT_LIB=distributed_raytracer_amd/$L timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU \
-    SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/$L -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 \
-    --no-cpu-baseline --no-parity > $OUT/$L.log 2>&1 || { echo "$L failed"; tail -5 $OUT/$L.log; exit 1; }
-  python3 - "$OUT/$L" "$L" <<'PY'
+    SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/$N -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+    --no-cpu-baseline --no-parity $X > $OUT/$N.log 2>&1 || { echo "$N failed"; tail -5 $OUT/$N.log; exit 1; }
+  python3 - "$OUT/$N" "$N" <<'PY'
 import csv, collections, json, sys
 d, name = sys.argv[1], sys.argv[2]
 per = collections.defaultdict(dict)

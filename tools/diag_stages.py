@@ -33,6 +33,7 @@ def main():
         print(kind, "  ".join(f"{nm}={c[base + i]:.0f}" for i, nm in enumerate(names)))
     print("k_trace: ready-wait spins", c[17], " idle spins", c[18], " shadow items", c[19], " primary blocks", c[20],
           " culled blocks", c[21])
+    print("shadow light-table classifications", c[22], " skipped by the wave", c[22] - c[8])
     g.close()
 
 
