@@ -1139,7 +1139,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
                                     resolve, tmax);
     } else {
         // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
-        const float* lt = fa.ltab ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
+        const float* lt = fa.ltab && li < fa.n_lights ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
         SegPre sp;
         if (lt) sp = seg_pre(d, lh);
         if (resident)

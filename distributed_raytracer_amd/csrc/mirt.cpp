@@ -715,7 +715,11 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, max_wg));
     // k_trace: workgroup w's hit region holds one chunk per block it owns
     wa.wg_cap = (uint32_t)((total + pgrid - 1) / pgrid * 64);
-    const uint64_t hit_slots = std::max<uint64_t>((uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap);
+    // sized for any grid up to kWgPerCu per CU (G ceil(total / G) <= total + G): a launch whose
+    // grid differs from the slot's last one (MIRT_ADAPTIVE_GRID) never regrows the buffers
+    // (hipFree synchronises the device)
+    const uint64_t hit_slots = std::max<uint64_t>({(uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap,
+                                                   (total + (uint64_t)kWgPerCu * c->cus) * 64});
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
@@ -1714,7 +1718,10 @@ struct mirt_group {
     bool skip_unpack = false;
     bool host_out = false;
     bool d2h_sdma = false;              // MIRT_D2H=sdma: copy-engine column ranges (default: zero-copy kernel)
-    bool adaptive_grid = false;         // MIRT_ADAPTIVE_GRID=1: size each launch by the launches still running
+    // launch grid by the launches still running (MIRT_ADAPTIVE_GRID): 0 (default) fixed; 1 the
+    // chip shared among them; 2 the whole chip for a launch issued when none is running (a
+    // lone frame, the first of a burst), the fixed grid otherwise
+    uint32_t adaptive_grid = 0;
     int d2h_cus = 0;                    // CUs reserved for the host copies (0: copies on the frame stream)
     hipStream_t copy_stream = nullptr;
     std::vector<HostFrame> hfb;
@@ -2211,7 +2218,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     const char* d2h = getenv("MIRT_D2H");
     g->d2h_sdma = d2h && !strcmp(d2h, "sdma");
     const char* ag = getenv("MIRT_ADAPTIVE_GRID");
-    g->adaptive_grid = ag && atoi(ag) > 0;
+    if (ag) g->adaptive_grid = (uint32_t)std::min(std::max(atoi(ag), 0), 2);
     // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
     // N-way deal (MIRT_GROUP_REHEARSE_RANK, default 0) and unpack all N regions, the others
     // stale: the root's per-frame GPU work at N GPUs without the transfers.  Results are
@@ -2470,14 +2477,18 @@ static int group_flush(mirt_group* g) {
     // host copies on copy_stream: batch nb - FB last used this batch's framebuffers; its copy
     // must have read them before this batch's fill and trace rewrite them
     if (g->copy_stream && g->nb >= g->FB) HIP_TRY(hipStreamWaitEvent(s, g->ev_done[(g->nb - g->FB) % g->HB], 0));
-    // adaptive grid (MIRT_ADAPTIVE_GRID=1): the launches still running share the chip with
-    // this one, ~wg_factor x CUs workgroups between them
+    // adaptive grid (MIRT_ADAPTIVE_GRID, see mirt_group): mode 1, the launches still running
+    // share the chip with this one; mode 2, a launch issued while none runs gets the chip
+    // (kWgPerCu per CU), any other the fixed grid
     uint32_t max_wg_now = 0;
     if (g->adaptive_grid) {
         uint32_t running = 0;
-        for (uint64_t b = g->nb > g->FB ? g->nb - g->FB + 1 : 0; b < g->nb; ++b)
+        for (uint64_t b = g->nb > g->HB ? g->nb - g->HB : 0; b < g->nb; ++b)
             if (hipEventQuery(g->ev_done[b % g->HB]) == hipErrorNotReady) ++running;
-        max_wg_now = std::max<uint32_t>(1, (uint32_t)(2 * kWgPerCu * (uint64_t)c->cus / (running + 1)));
+        if (g->adaptive_grid == 1)
+            max_wg_now = std::max<uint32_t>(1, (uint32_t)(2 * kWgPerCu * (uint64_t)c->cus / (running + 1)));
+        else if (running == 0)
+            max_wg_now = (uint32_t)(kWgPerCu * (uint64_t)c->cus);
     }
     // Blocks outside a frame's hit rectangle (every ray misses) are not traced: a share's
     // packed plane is only read inside the rectangle (k_pack_rect), and the whole-screen

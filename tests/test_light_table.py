@@ -127,7 +127,7 @@ def test_light_table_never_rejects_a_hit(seed):
     rec = _records(tri, scale, pos, np.array(lights))
     hits = rejected_miss = misses = 0
     for li, L in enumerate(lights):
-        ro, d, lh = _shadow_rays(V, F, pos, L, rng, 256)
+        ro, d, lh = _shadow_rays(V, F, pos, L, rng, 640)
         hit = _mt_hits(tri, ro, d)
         rej = _reject(rec[li], d, lh)
         bad = hit & rej
