@@ -159,6 +159,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
     ap.add_argument("--no-octant", action="store_true", help="ablation: generic (sorted) child-box test only")
+    ap.add_argument("--reflect-waves", action="store_true",
+                    help="variant (--bounces): reflections level by level, rays packed in block order (k_bounce/k_pack)")
     ap.add_argument("--no-light-table", action="store_true",
                     help="ablation: shadow segments without the fp32 light-table pre-classification")
     ap.add_argument("--views", action="store_true",
@@ -346,7 +348,8 @@ def main():
     opts = (rt._lib.MIRT_OPT_NO_OCTANT if a.no_octant else 0) | (rt._lib.MIRT_OPT_NO_PREFILTER if a.no_prefilter else 0) | (
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
-        rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0)
+        rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0) | (
+        rt._lib.MIRT_OPT_REFLECT_WAVES if a.reflect_waves else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses

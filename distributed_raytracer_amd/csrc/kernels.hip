@@ -1400,7 +1400,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
                                               bool frustum = false, const float4* __restrict__ frect = nullptr,
                                               const LocalChunks* lc = nullptr, uint32_t classified = 0,
                                               const ViewLeaf* vt = nullptr, uint32_t vn = 0,
-                                              const FrustumArgs* vfr = nullptr) {
+                                              const FrustumArgs* vfr = nullptr, uint32_t blk = ~0u) {
     pc.start();
     const uint32_t lane = threadIdx.x & 63;
     const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
@@ -1475,6 +1475,11 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
         const size_t slot = lc ? (size_t)(lc->base + (size_t)base * 64) + ln : (size_t)q * wa.hit_cap + base + lane;
+        // bounce waves: the block's hit chunk, for k_pack's walk in block order
+        if (!lc && wa.bmap && blk != ~0u && lane == 0) {
+            wa.bmap[blk] = (uint32_t)(((size_t)q * wa.hit_cap + base) / 64 + 1) << 7 | (uint32_t)__popcll(mask);
+            atomicAdd(&wa.bgcnt[blk / kPackGroup], (uint32_t)__popcll(mask));
+        }
         uint64_t* w = (uint64_t*)&wa.hits[slot];
         if (is_hit) {
             st64(w + 0, dbits(nh.hit.x));
@@ -1891,7 +1896,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
             const uint32_t b = blockIdx.x + (c0 + t) * G;
             ++taken;
             primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
-                                                      use_frustum, frect);
+                                                      use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b);
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -2375,6 +2380,9 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     WaveStats ws{0, 0, 0, 0, 0};
     cnt_t rays = 0, shadow_rays = 0;
     const uint32_t lv = ba.level;
+    // chunks per region of the input (k_pack fills regions in order, each but the last with
+    // the same number of chunks): input chunk (q, k) is source chunk q * cp + k of k_pack
+    const uint32_t cp = (*lo32((cnt_t*)&ba.in_cnt[cnt_hits(0)]) + 63) / 64;
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
         for (uint32_t k = sc.rank(); k < nch; k += sc.peers()) {
@@ -2382,7 +2390,7 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
             const bool inb = k * 64 + lane < n;
             const HitRec rec = ba.in[inb ? slot : (size_t)q * wa.hit_cap + (size_t)k * 64];
             const bool active = inb && rec.obj != kNoHit;
-            const size_t origin = lv == 1 ? slot : (size_t)rec.out;
+            const size_t origin = (size_t)rec.out;  // k_pack: the primary hit slot of the chain
             V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
             if (active) {
                 D = vload(ba.in_dir + 3 * slot);
@@ -2401,26 +2409,28 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
             const bool got = active && r.ok;
             if (active) ba.chain[origin] = got ? lv + 1 : (lv | 256u);  // levels with phong | missed
             const uint64_t m = __ballot(got);
-            if (m) {
-                shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(lo32(&ba.out_cnt[cnt_hits(q)]), (uint32_t)__popcll(m));
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (got) {
-                    const size_t os = (size_t)q * wa.hit_cap + base + __popcll(m & ((1ull << lane) - 1ull));
-                    HitRec h;
-                    h.h[0] = r.hit.x, h.h[1] = r.hit.y, h.h[2] = r.hit.z;
-                    h.n[0] = r.normal.x, h.n[1] = r.normal.y, h.n[2] = r.normal.z;
-                    h.out = origin;
-                    h.obj = r.obj;
-                    h.mat = r.mat;
-                    ba.out[os] = h;
-                    vstore(ba.out_dir + 3 * os, R);
-                    ba.out_litw[os] = 0u;
-                    ba.out_blkdone[os / 64] = 0u;  // (every writer of the chunk: the same zero)
-                    wa.refl[((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD + 3] =
-                        bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
-                }
+            shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
+            // the level's hits stay at the input's slots; k_pack compacts them in order
+            uint64_t* w = (uint64_t*)&ba.out[slot];
+            if (got) {
+                st64(w + 0, dbits(r.hit.x));
+                st64(w + 1, dbits(r.hit.y));
+                st64(w + 2, dbits(r.hit.z));
+                st64(w + 3, dbits(r.normal.x));
+                st64(w + 4, dbits(r.normal.y));
+                st64(w + 5, dbits(r.normal.z));
+                st64(w + 6, (uint64_t)origin);
+                st64(w + 7, (uint64_t)r.obj | ((uint64_t)r.mat << 32));
+                vstore(ba.out_dir + 3 * slot, R);
+                wa.refl[((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD + 3] =
+                    bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
+            } else {
+                st64(w + 7, (uint64_t)kNoHit);
+            }
+            if (lane == 0) {
+                const uint32_t j = q * cp + k;
+                ba.src[j] = (uint32_t)(((size_t)q * wa.hit_cap + (size_t)k * 64) / 64 + 1) << 7 | (uint32_t)__popcll(m);
+                if (m) atomicAdd(&ba.gcnt[j / kPackGroup], (uint32_t)__popcll(m));
             }
         }
     }
@@ -2430,6 +2440,99 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     stats_flush(wa.counters, red, kStatReflRays, kStatReflShadowRays, -1, -1, extra);
 }
 
+// k_pack (bounce waves): the records of a level compacted in source-chunk order — level 0
+// the primary hit blocks in block-table order (column-major 8x8 blocks: neighbours on the
+// screen), each later level in its input's order, so a wave of 64 records holds the rays of a
+// few adjacent blocks — and dealt evenly over the kQShards regions.  Every workgroup sums the
+// chunk counts before its range (and the total) itself: no scan kernel, no second launch.
+constexpr int kPackWG = 256;
+static_assert(kPackGroup == 64, "k_pack: one source chunk per lane of wave 0");
+__device__ __forceinline__ void pack_chunk(const WorkArgs& wa, const PackArgs& pa, uint32_t e, uint32_t off, uint32_t per,
+                                           uint32_t lane) {
+    if ((e & 127u) == 0) return;
+    const size_t cs = (size_t)((e >> 7) - 1) * 64;
+    const size_t from = cs + lane;
+    const uint64_t* w = (const uint64_t*)&pa.in[from];
+    const uint64_t w7 = ld64(w + 7);
+    const bool valid = (uint32_t)w7 != kNoHit;
+    const uint64_t m = __ballot(valid);
+    if (!valid) return;
+    const uint32_t p = off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t r = p / per, idx = p - r * per;
+    const size_t dst = (size_t)r * wa.hit_cap + idx;
+    uint64_t v[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) v[q] = ld64(w + q);
+    const V3 dir = vload(pa.in_dir + 3 * from);
+    uint64_t* d = (uint64_t*)&pa.out[dst];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) st64(d + q, v[q]);
+    st64(d + 6, pa.level0 ? (uint64_t)from : ld64(w + 6));
+    st64(d + 7, w7);
+    vstore(pa.out_dir + 3 * dst, dir);
+    st32(&pa.out_litw[dst], 0u);
+    st32(&pa.out_blkdone[dst / 64], 0u);  // (every record of the chunk: the same zero)
+}
+__global__ __launch_bounds__(kPackWG) void k_pack(const WorkArgs wa, const PackArgs pa) {
+    __shared__ uint32_t s_red[2][kPackWG / 64];
+    __shared__ uint32_t s_off[kPackGroup], s_src[kPackGroup];
+    __shared__ uint32_t s_nsrc;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) {
+        uint32_t n = pa.nsrc;
+        if (pa.in_cnt) {
+            n = 0;
+            for (int q = 0; q < kQShards; ++q) n += (*lo32((cnt_t*)&pa.in_cnt[cnt_hits(q)]) + 63) / 64;
+        }
+        s_nsrc = n;
+    }
+    __syncthreads();
+    // workgroup w packs source chunks [64 w, 64 w + 64); the records before them and in total
+    // come from the producers' per-group counts
+    const uint32_t nsrc = s_nsrc, ng = (nsrc + kPackGroup - 1) / kPackGroup;
+    const uint32_t j0 = min(nsrc, blockIdx.x * kPackGroup), j1 = min(nsrc, j0 + kPackGroup);
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t g = tid; g < ng; g += kPackWG) {
+        const uint32_t c = pa.gcnt[g];
+        tot += c;
+        if (g < blockIdx.x) pre += c;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        pre += __shfl_xor(pre, o);
+        tot += __shfl_xor(tot, o);
+    }
+    if (lane == 0) {
+        s_red[0][wave] = pre;
+        s_red[1][wave] = tot;
+    }
+    if (wave == 0) {  // the group's chunks: exclusive scan of their counts
+        const uint32_t e = j0 + lane < j1 ? pa.src[j0 + lane] : 0u, c = e & 127u;
+        uint32_t x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        s_off[lane] = x - c;
+        s_src[lane] = e;
+    }
+    __syncthreads();
+    pre = tot = 0;
+    for (int k = 0; k < kPackWG / 64; ++k) {
+        pre += s_red[0][k];
+        tot += s_red[1][k];
+    }
+    const uint32_t per = ((tot + 63) / 64 + kQShards - 1) / kQShards * 64;  // records per region
+    if (blockIdx.x == 0 && tid < (uint32_t)kQShards) {
+        const uint32_t a = tid * per;
+        *lo32(&pa.out_cnt[cnt_hits(tid)]) = tot > a ? min(per, tot - a) : 0u;
+    }
+    for (uint32_t t = wave; t < j1 - j0; t += kPackWG / 64) pack_chunk(wa, pa, s_src[t], pre + s_off[t], per, lane);
+}
+hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_pack, dim3(std::max(grid, 1)), dim3(kPackWG), 0, s, wa, pa);
+    return hipGetLastError();
+}
+
 // The frame's last kernel on the bounce path: per primary hit slot, c_L = ph_L (a chain that
 // ended on a miss: c_add(ph_L, c_mul(Ks_L, black))), then c_k = c_add(ph_k, c_mul(Ks_k,
 // c_(k+1))) down to level 0 (rt_oracle.c shade_reflect), and the pixel's outputs.
@@ -2437,9 +2540,21 @@ __global__ __launch_bounds__(256) void k_refl_fold(const FrameArgs fa, const Wor
                                                    const uint32_t* __restrict__ chain) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-    for (uint32_t q = 0; q < (uint32_t)kQShards; ++q) {
-        const uint32_t nch = *lo32(&wa.counters[cnt_hits(q)]) / 64;
-        for (uint32_t k = gw; k < nch; k += nw) {
+    // one walk over every region's chunks (a loop per region left most waves idle per region)
+    __shared__ uint32_t s_first[kQShards + 1];
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int q = 0; q < kQShards; ++q) {
+            s_first[q] = acc;
+            acc += *lo32(&wa.counters[cnt_hits(q)]) / 64;
+        }
+        s_first[kQShards] = acc;
+    }
+    __syncthreads();
+    for (uint32_t g = gw, q = 0; g < s_first[kQShards]; g += nw) {
+        while (g >= s_first[q + 1]) ++q;
+        const uint32_t k = g - s_first[q];
+        {
             const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
             const HitRec& rec = wa.hits[slot];
             if (rec.obj == kNoHit) continue;

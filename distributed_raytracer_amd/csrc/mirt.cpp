@@ -113,6 +113,18 @@ struct Slot {
     size_t lcnt_cap = 0;
     uint32_t* chain = nullptr;
     size_t chain_cap = 0;
+    // bounce waves: a level's hits at its input's slots (k_bounce), the chunk descriptors of
+    // k_pack's walk, and the block table's hit chunks (WorkArgs::bmap)
+    HitRec* shits = nullptr;
+    size_t shits_cap = 0;
+    double* sdir = nullptr;
+    size_t sdir_cap = 0;
+    uint32_t* ssrc = nullptr;
+    size_t ssrc_cap = 0;
+    uint32_t* bmap = nullptr;
+    size_t bmap_cap = 0;
+    uint32_t* gcnt = nullptr;  // [bounces + 1][groups]: records per group of kPackGroup source chunks
+    size_t gcnt_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
     size_t cost_cap = 0;
     cnt_t* counters = nullptr;
@@ -228,7 +240,8 @@ int slot_init(Slot* s) {
 void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->lhits[0], (void*)s->lhits[1], (void*)s->ldir[0], (void*)s->ldir[1], (void*)s->llitw[0],
-                    (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain})
+                    (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain,
+                    (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
@@ -741,8 +754,18 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
                 if ((r = dev_grow(sl->llitw[b], sl->llitw_cap[b], hit_slots)) != MIRT_OK) return r;
                 if ((r = dev_grow(sl->lblk[b], sl->lblk_cap[b], hit_slots / 64)) != MIRT_OK) return r;
             }
-            if ((r = dev_grow(sl->lcnt, sl->lcnt_cap, (size_t)bounces * kCntN)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->lcnt, sl->lcnt_cap, (size_t)(bounces + 1) * kCntN)) != MIRT_OK) return r;
             if ((r = dev_grow(sl->chain, sl->chain_cap, hit_slots)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->shits, sl->shits_cap, hit_slots)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->sdir, sl->sdir_cap, 3 * hit_slots)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->ssrc, sl->ssrc_cap, hit_slots / 64)) != MIRT_OK) return r;
+            if ((r = dev_grow(sl->bmap, sl->bmap_cap, (size_t)std::max<uint32_t>(sl->nblocks, 1))) != MIRT_OK) return r;
+            const size_t ng = (std::max<size_t>(sl->nblocks, hit_slots / 64) + kPackGroup - 1) / kPackGroup;
+            if ((r = dev_grow(sl->gcnt, sl->gcnt_cap, (size_t)(bounces + 1) * ng)) != MIRT_OK) return r;
+            wa.bmap = sl->bmap;
+            wa.bgcnt = sl->gcnt;
+            HIP_TRY(hipMemsetAsync(sl->bmap, 0, (size_t)sl->nblocks * sizeof(uint32_t), s));
+            HIP_TRY(hipMemsetAsync(sl->gcnt, 0, (size_t)(bounces + 1) * ng * sizeof(uint32_t), s));
         }
     }
     if (one_launch && !getenv("MIRT_NO_COST_ORDER")) {
@@ -843,29 +866,56 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
             HIP_TRY(launch_reflect(fa, wa, out, sgrid, c->flags, s));
         } else if (wa.bounces) {
-            // bounce waves: level lv's reflection rays (k_bounce), its shadow rays and phong
-            // (k_shadow on the level's records), then the fold of every chain (the last kernel)
-            HIP_TRY(hipMemsetAsync(sl->lcnt, 0, (size_t)wa.bounces * kCntN * sizeof(cnt_t), s));
+            // bounce waves: the primary hits packed in block order (k_pack, level 0), then per
+            // level lv the reflection rays of level lv - 1's records (k_bounce, hits left at the
+            // input's slots), those hits packed in order (k_pack), their shadow rays and phong
+            // (k_shadow on the packed records); then the fold of every chain (the last kernel)
+            HIP_TRY(hipMemsetAsync(sl->lcnt, 0, (size_t)(wa.bounces + 1) * kCntN * sizeof(cnt_t), s));
+            const size_t ng = (std::max<size_t>(sl->nblocks, hit_slots / 64) + kPackGroup - 1) / kPackGroup;
+            PackArgs p0{};
+            p0.in = sl->hits;
+            p0.in_dir = sl->dir0;
+            p0.src = sl->bmap;
+            p0.gcnt = sl->gcnt;
+            p0.nsrc = sl->nblocks;
+            p0.level0 = 1;
+            p0.out = sl->lhits[0];
+            p0.out_dir = sl->ldir[0];
+            p0.out_litw = sl->llitw[0];
+            p0.out_blkdone = sl->lblk[0];
+            p0.out_cnt = sl->lcnt;
+            HIP_TRY(launch_pack(wa, p0, (int)((sl->nblocks + kPackGroup - 1) / kPackGroup), s));
             for (uint32_t lv = 1; lv <= wa.bounces; ++lv) {
                 if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
-                const int ib = (int)(lv & 1u) ^ 1, ob = (int)(lv & 1u);  // level lv writes buffer lv % 2
+                const int ib = (int)((lv - 1) & 1u), ob = (int)(lv & 1u);  // level lv in buffer lv % 2
                 BounceArgs ba{};
-                ba.in = lv == 1 ? sl->hits : sl->lhits[ib];
-                ba.in_dir = lv == 1 ? sl->dir0 : sl->ldir[ib];
-                ba.in_cnt = lv == 1 ? wa.counters : sl->lcnt + (size_t)(lv - 2) * kCntN;
-                ba.out = sl->lhits[ob];
-                ba.out_dir = sl->ldir[ob];
-                ba.out_cnt = sl->lcnt + (size_t)(lv - 1) * kCntN;
-                ba.out_litw = sl->llitw[ob];
-                ba.out_blkdone = sl->lblk[ob];
+                ba.in = sl->lhits[ib];
+                ba.in_dir = sl->ldir[ib];
+                ba.in_cnt = sl->lcnt + (size_t)(lv - 1) * kCntN;
+                ba.out = sl->shits;
+                ba.out_dir = sl->sdir;
+                ba.src = sl->ssrc;
+                ba.gcnt = sl->gcnt + (size_t)lv * ng;
                 ba.chain = sl->chain;
                 ba.level = lv;
                 HIP_TRY(launch_bounce(fa, wa, ba, sgrid, c->flags, s));
+                PackArgs pk{};
+                pk.in = sl->shits;
+                pk.in_dir = sl->sdir;
+                pk.src = sl->ssrc;
+                pk.gcnt = ba.gcnt;
+                pk.in_cnt = ba.in_cnt;
+                pk.out = sl->lhits[ob];
+                pk.out_dir = sl->ldir[ob];
+                pk.out_litw = sl->llitw[ob];
+                pk.out_blkdone = sl->lblk[ob];
+                pk.out_cnt = sl->lcnt + (size_t)lv * kCntN;
+                HIP_TRY(launch_pack(wa, pk, (int)((hit_slots / 64 + kPackGroup - 1) / kPackGroup), s));
                 WorkArgs wl = wa;
                 wl.hits = sl->lhits[ob];
                 wl.litw = sl->llitw[ob];
                 wl.blkdone = sl->lblk[ob];
-                wl.qcounters = ba.out_cnt;
+                wl.qcounters = pk.out_cnt;
                 wl.ph_out = sl->refl + (size_t)(lv - 1) * hit_slots * kReflD;
                 wl.ph_stride = kReflD;
                 wl.ph_by_origin = 1;

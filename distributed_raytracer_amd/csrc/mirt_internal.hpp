@@ -315,23 +315,44 @@ struct WorkArgs {
     uint16_t* block_cost;
     uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
     uint32_t view_pad;
+    // bounce waves (MIRT_OPT_REFLECT_WAVES): per linear block of the table, its hit chunk
+    // ((slot / 64 + 1) << 7 | hits; 0: none), written by k_primary (zeroed per frame), and the
+    // hits per group of kPackGroup blocks (k_pack's prefix sums)
+    uint32_t* bmap;
+    uint32_t* bgcnt;
 };
+constexpr uint32_t kPackGroup = 64;  // source chunks per k_pack workgroup (and per counted group)
 // Reflections in waves of bounces (configs[4] extension, kernels.hip k_bounce): level lv's
 // hit records form region sets like the primary's (kQShards regions of hit_cap slots, region
 // q holding cnt_hits(q) records of its counters, packed from the front), each record's `out`
 // the origin slot (the primary hit slot whose chain it continues).
 struct BounceArgs {
-    const HitRec* in;       // level lv - 1 (lv == 1: the primary hit slots)
+    const HitRec* in;       // level lv - 1 in region layout (k_pack); `out` = the origin slot
     const double* in_dir;   // per input slot: the ray that reached the hit (3 doubles)
-    const cnt_t* in_cnt;    // the input's region counts (lv == 1: the frame's counters)
-    HitRec* out;            // level lv
+    const cnt_t* in_cnt;    // the input's region counts
+    HitRec* out;            // level lv's hits, at the input's slots (obj = kNoHit: none)
     double* out_dir;
-    cnt_t* out_cnt;         // zeroed before the launch
-    uint32_t* out_litw;
-    uint32_t* out_blkdone;
+    uint32_t* src;          // per input chunk j (region-major order): (slot / 64 + 1) << 7 | hits
+    uint32_t* gcnt;         // hits per group of kPackGroup input chunks (zeroed before)
     uint32_t* chain;        // per origin slot: levels with a phong value | missed << 8
     uint32_t level;
     uint32_t pad;
+};
+// k_pack: a bounce level's records compacted in source-chunk order (the screen's block
+// order), split evenly over the kQShards regions (region r: positions [r per, (r + 1) per)).
+struct PackArgs {
+    const HitRec* in;       // the source slots (level 0: the primary hit slots)
+    const double* in_dir;
+    const uint32_t* src;    // source chunks in order: (slot / 64 + 1) << 7 | records (0: none)
+    const uint32_t* gcnt;   // records per group of kPackGroup source chunks
+    const cnt_t* in_cnt;    // level >= 1: the region counts of the chunks' level (their number); else null
+    uint32_t nsrc;          // level 0: entries of src (the block table)
+    uint32_t level0;        // 1: records are primary hits (their origin = their slot)
+    HitRec* out;
+    double* out_dir;
+    uint32_t* out_litw;
+    uint32_t* out_blkdone;
+    cnt_t* out_cnt;         // region counts of the packed level (cnt_hits)
 };
 constexpr int kTimelineRec = 8;
 constexpr int kReflD = 4;  // doubles per slot and level of WorkArgs::refl
@@ -362,6 +383,7 @@ hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint3
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
+hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStream_t s);
 hipError_t launch_bounce(const FrameArgs& fa, const WorkArgs& wa, const BounceArgs& ba, int grid, uint32_t opts,
                          hipStream_t s);
 hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, const uint32_t* chain,
