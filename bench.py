@@ -159,8 +159,9 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-prefilter", action="store_true", help="ablation: always divide for r2")
     ap.add_argument("--no-octant", action="store_true", help="ablation: generic (sorted) child-box test only")
-    ap.add_argument("--reflect-waves", action="store_true",
-                    help="variant (--bounces): reflections level by level, rays packed in block order (k_bounce/k_pack)")
+    ap.add_argument("--reflect-chains", action="store_true",
+                    help="variant (--bounces): reflections as per-pixel chains in one kernel (k_reflect) instead of "
+                         "level by level with rays packed in block order (k_bounce / k_pack / k_shadow)")
     ap.add_argument("--no-light-table", action="store_true",
                     help="ablation: shadow segments without the fp32 light-table pre-classification")
     ap.add_argument("--views", action="store_true",
@@ -349,7 +350,7 @@ def main():
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
         rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0) | (
-        rt._lib.MIRT_OPT_REFLECT_WAVES if a.reflect_waves else 0)
+        rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses
@@ -518,16 +519,18 @@ def main():
         rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
         nlaunch = max(prof["launches"], 1)
         prim_ms = prof["primary_ms_sum"] / nlaunch
-        # the dominant kernel: k_trace (the whole frame, one launch); split frames: k_primary,
-        # and reflection frames (split, k_primary -> k_shadow -> k_reflect) k_reflect, the
-        # longest of the three (profiles/r02_bench_config4.log: 2.67 of 3.81 ms)
+        # the dominant kernel: k_trace (the whole frame, one launch); split frames: k_primary;
+        # reflection frames: k_shadow (level 0 and each bounce level: the most time per frame,
+        # profiles/r03config4_kernel_stats.csv), or k_reflect on the chain path (2.67 of 3.81 ms)
         one = not a.split_kernels and not a.bounces
-        kname = "k_trace" if one else ("k_reflect" if a.bounces else "k_primary")
+        kname = "k_trace" if one else (("k_reflect" if a.reflect_chains else "k_shadow") if a.bounces else "k_primary")
         if a.bounces:
-            # the algorithmic figure over the frame's three kernels: k_reflect's tests are counted
-            # with k_shadow's (one statistic), so the whole frame's tests / its device time
+            # the algorithmic figure over all the frame's kernels: the reflection levels' tests are
+            # counted with the shadow rays' (one statistic), so the whole frame's tests / its time
             k_tests = (prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / nlaunch
-            alg_ms, alg_kernel = prof["frame_ms_sum"] / nlaunch, "k_primary + k_shadow + k_reflect"
+            alg_ms = prof["frame_ms_sum"] / nlaunch
+            alg_kernel = ("k_primary + k_shadow + k_reflect" if a.reflect_chains else
+                          "k_primary + k_pack + k_bounce + k_shadow (levels 0..bounces) + k_refl_fold")
         else:
             k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
             alg_ms, alg_kernel = prim_ms, kname

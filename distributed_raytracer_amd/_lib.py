@@ -34,7 +34,7 @@ MIRT_OPT_SPLIT_KERNELS = 32
 MIRT_OPT_NO_FRUSTUM = 64
 MIRT_OPT_NO_OCTANT = 128
 MIRT_OPT_VIEWS = 256
-MIRT_OPT_REFLECT_WAVES = 512
+MIRT_OPT_REFLECT_CHAINS = 512
 MIRT_OPT_NO_LIGHT_TABLE = 1024
 
 D3 = C.c_double * 3

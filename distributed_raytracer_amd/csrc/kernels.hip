@@ -726,6 +726,11 @@ extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
 #endif
 #define MIRT_REFLECT_KERNEL \
     __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_REFLECT_WAVES_PER_EU)))
+// bounce waves: k_bounce also traces each level's shadow rays and phong (1: slower, DESIGN.md
+// §4.8), or leaves them to k_shadow on the packed records (0)
+#ifndef MIRT_BOUNCE_SHADE
+#define MIRT_BOUNCE_SHADE 0
+#endif
 
 // ---------------------------------------------------------------- wide traversal
 #ifndef MIRT_LEAF_LANE_TEST
@@ -2359,13 +2364,14 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
     frame_fold(fa, wa);
 }
 
-// Reflections in waves of bounces (MIRT_OPT_REFLECT_WAVES; the default k_reflect above
-// follows each lane's whole chain).  Per level lv = 1..bounces: k_bounce traces one reflection ray
-// per record of level lv - 1 (R = D - 2 (D.N) N from hit + 1e-4 R, the nearest hit of
-// tracer.go:27-50) and packs the hits into level lv's records — region by region, each wave
-// appending its hits after one atomic, so a later wave of 64 records holds 64 live rays (the
-// chain kernel kept a lane per primary hit through every level: 41% of its lanes had a ray
-// at level 1, ~12% at level 4); k_shadow then traces level lv's shadow rays and stores its
+// Reflections in waves of bounces (the default; MIRT_OPT_REFLECT_CHAINS runs k_reflect above,
+// which follows each lane's whole chain).  k_pack first lays the primary hits out in block
+// order; per level lv = 1..bounces k_bounce traces one reflection ray per record of level
+// lv - 1 (R = D - 2 (D.N) N from hit + 1e-4 R, the nearest hit of tracer.go:27-50) and leaves
+// its hits at the input's slots, k_pack compacts them in order, so a wave of 64 records holds
+// 64 live rays from a few neighbouring blocks (the chain kernel kept a lane per primary hit
+// through every level: 41% of its lanes had a ray at level 1, ~12% at level 4); k_shadow then
+// traces level lv's shadow rays and stores its
 // phong at the origin slot; k_refl_fold combines the levels per pixel, innermost first.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const BounceArgs ba) {
@@ -2410,6 +2416,40 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
             if (active) ba.chain[origin] = got ? lv + 1 : (lv | 256u);  // levels with phong | missed
             const uint64_t m = __ballot(got);
             shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
+            if (MIRT_BOUNCE_SHADE && m) {
+                // the level's shadow rays and phong in this wave (tracer.go:53-77 at the hit;
+                // the packed lanes are mostly live): no k_shadow launch per level
+                const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
+                uint32_t lit = 0;
+                for (uint32_t l = 0; l < fa.n_lights; ++l) {
+                    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+                    V3 so{0, 0, 0}, sd{1, 0, 0};
+                    if (got) {
+                        sd = norm(sub(lpos, r.hit));
+                        so = add(r.hit, scale(sd, 0.0001));
+                    }
+                    Visits sv{0, 0, 0, 0};
+                    bool is_lit;
+                    if (segment) {
+                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, got, sv);
+                    } else {
+                        const Nearest sr = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, got, false, sv);
+                        is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
+                    }
+                    lit |= (uint32_t)is_lit << l;
+                    ws.tests += (cnt_t)sv.tests * __popcll(m);
+                    ws.nodes += sv.nodes;
+                    ws.leaves += sv.leaves;
+                    ws.overflow += sv.overflow;
+                }
+                if (got) {
+                    const RGB ph = phong(fa, fa.obj[r.obj].m.mats + (size_t)r.mat * 10, r.hit, r.normal, lit);
+                    double* const e = wa.refl + ((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD;
+                    e[0] = ph.r;
+                    e[1] = ph.g;
+                    e[2] = ph.b;
+                }
+            }
             // the level's hits stay at the input's slots; k_pack compacts them in order
             uint64_t* w = (uint64_t*)&ba.out[slot];
             if (got) {
@@ -2528,6 +2568,7 @@ __global__ __launch_bounds__(kPackWG) void k_pack(const WorkArgs wa, const PackA
     }
     for (uint32_t t = wave; t < j1 - j0; t += kPackWG / 64) pack_chunk(wa, pa, s_src[t], pre + s_off[t], per, lane);
 }
+bool bounce_shades() { return MIRT_BOUNCE_SHADE != 0; }
 hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_pack, dim3(std::max(grid, 1)), dim3(kPackWG), 0, s, wa, pa);
     return hipGetLastError();

@@ -747,7 +747,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         wa.refl_stride = hit_slots;
         wa.ph_out = sl->ph0;  // level 0 (k_shadow); the bounce levels set their own
         wa.ph_stride = 3;
-        if (c->flags & MIRT_OPT_REFLECT_WAVES) {
+        if (!(c->flags & MIRT_OPT_REFLECT_CHAINS)) {
             for (int b = 0; b < 2; ++b) {
                 if ((r = dev_grow(sl->lhits[b], sl->lhits_cap[b], hit_slots)) != MIRT_OK) return r;
                 if ((r = dev_grow(sl->ldir[b], sl->ldir_cap[b], 3 * hit_slots)) != MIRT_OK) return r;
@@ -862,7 +862,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         // launched with no lights, to shade every hit with the ambient term
         HIP_TRY(launch_shadow(fa, wa, out, sgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[2], s));
-        if (wa.bounces && !(c->flags & MIRT_OPT_REFLECT_WAVES)) {  // configs[4] extension: the last kernel
+        if (wa.bounces && (c->flags & MIRT_OPT_REFLECT_CHAINS)) {  // configs[4] extension: the last kernel
             if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
             HIP_TRY(launch_reflect(fa, wa, out, sgrid, c->flags, s));
         } else if (wa.bounces) {
@@ -899,6 +899,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
                 ba.chain = sl->chain;
                 ba.level = lv;
                 HIP_TRY(launch_bounce(fa, wa, ba, sgrid, c->flags, s));
+                if (bounce_shades() && lv == wa.bounces) break;  // shaded in k_bounce, no next level
                 PackArgs pk{};
                 pk.in = sl->shits;
                 pk.in_dir = sl->sdir;
@@ -911,6 +912,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
                 pk.out_blkdone = sl->lblk[ob];
                 pk.out_cnt = sl->lcnt + (size_t)lv * kCntN;
                 HIP_TRY(launch_pack(wa, pk, (int)((hit_slots / 64 + kPackGroup - 1) / kPackGroup), s));
+                if (bounce_shades()) continue;
                 WorkArgs wl = wa;
                 wl.hits = sl->lhits[ob];
                 wl.litw = sl->llitw[ob];

@@ -315,7 +315,7 @@ struct WorkArgs {
     uint16_t* block_cost;
     uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
     uint32_t view_pad;
-    // bounce waves (MIRT_OPT_REFLECT_WAVES): per linear block of the table, its hit chunk
+    // bounce waves (reflection frames without MIRT_OPT_REFLECT_CHAINS): per linear block of the table, its hit chunk
     // ((slot / 64 + 1) << 7 | hits; 0: none), written by k_primary (zeroed per frame), and the
     // hits per group of kPackGroup blocks (k_pack's prefix sums)
     uint32_t* bmap;
@@ -384,6 +384,7 @@ hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t 
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStream_t s);
+bool bounce_shades();  // k_bounce traces each level's shadow rays itself (MIRT_BOUNCE_SHADE)
 hipError_t launch_bounce(const FrameArgs& fa, const WorkArgs& wa, const BounceArgs& ba, int grid, uint32_t opts,
                          hipStream_t s);
 hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, const uint32_t* chain,

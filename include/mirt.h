@@ -243,7 +243,7 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_NO_FRUSTUM 64u     /* no whole-block frustum pre-test of primary rays */
 #define MIRT_OPT_NO_OCTANT 128u     /* generic child-box test (no sign-octant variants; same decisions) */
 #define MIRT_OPT_VIEWS 256u         /* per-frame view tables instead of the BVH walk (same results; slower) */
-#define MIRT_OPT_REFLECT_WAVES 512u /* reflections level by level with packed rays (k_bounce; same results; slower) */
+#define MIRT_OPT_REFLECT_CHAINS 512u /* reflections as per-pixel chains in one kernel (k_reflect) instead of level by level (same results) */
 #define MIRT_OPT_NO_LIGHT_TABLE 1024u /* shadow segments without the fp32 light-table pre-classification (same results) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 /*

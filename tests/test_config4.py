@@ -46,13 +46,14 @@ def test_reflections_full_frame_bit_exact(ctx, env, py_scene, bounces):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bounces", [1, 4])
-def test_reflection_waves_full_frame_bit_exact(ctx, env, py_scene, bounces):
-    """MIRT_OPT_REFLECT_WAVES (level by level, packed rays: k_bounce, k_shadow per level,
-    k_refl_fold) gives the chains' frames and ray counts bit for bit."""
+def test_reflection_chains_full_frame_bit_exact(ctx, env, py_scene, bounces):
+    """MIRT_OPT_REFLECT_CHAINS (one k_reflect launch following each pixel's chain) gives the
+    level waves' frames (the default: k_pack, k_bounce, k_shadow per level, k_refl_fold) and
+    ray counts bit for bit."""
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd import _lib as L
     mut = dataclasses.replace(env.mutable(), max_bounces=bounces)
-    ctx.set_options(L.MIRT_OPT_REFLECT_WAVES)
+    ctx.set_options(L.MIRT_OPT_REFLECT_CHAINS)
     try:
         ctx.profile_enable(True)
         fb = rt.draw(env, 320, 240, mut)

@@ -26,7 +26,9 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FRAME_KERNELS = ("k_trace", "k_primary", "k_shadow", "k_reflect")  # launched once per bench "launch"
+# a bench "launch" (one frame's kernels) runs each once, or (reflection levels: k_shadow,
+# k_pack, k_bounce) a fixed number of times
+FRAME_KERNELS = ("k_trace", "k_primary", "k_shadow", "k_reflect", "k_pack", "k_bounce", "k_refl_fold")
 ORDER = ("warmup", "timed", "device_only", "profiled", "latency")
 
 
@@ -46,16 +48,18 @@ def kernel_of(name: str):
 
 
 def regions(dispatches, launches: dict, kernel: str = "k_trace"):
-    """dispatch ids (submission order) -> region name, by the bench's launch counts."""
+    """dispatch ids (submission order) -> region name, by the bench's launch counts (a kernel
+    dispatched m times per launch: m consecutive dispatches per launch)."""
     names = [r for r in ORDER if launches.get(r)]
     total = sum(launches[r] for r in names)
-    if len(dispatches) != total:
+    m = len(dispatches) // total if total else 0
+    if m < 1 or len(dispatches) != m * total:
         raise SystemExit(f"{len(dispatches)} {kernel} dispatches but the bench reports {total} launches {launches}")
     out, i = {}, 0
     for r in names:
-        for d in dispatches[i:i + launches[r]]:
+        for d in dispatches[i:i + m * launches[r]]:
             out[d] = r
-        i += launches[r]
+        i += m * launches[r]
     return out
 
 
@@ -127,6 +131,7 @@ def main():
     }
     # PMC passes: per-launch counters of every frame kernel, over the timed and profiled regions
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))  # (kernel) -> counter -> values
+    nl = {}  # kernel -> launches of the timed and profiled regions
     for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_valu", "pmc_active"):
         f = os.path.join(src, p, "run_counter_collection.csv")
         if not os.path.exists(f):
@@ -140,6 +145,7 @@ def main():
         for k, pk in per.items():
             ids = sorted(pk)
             preg = regions(ids, pl["launches"], k)
+            nl[k] = sum(pl["launches"].get(g, 0) for g in ("timed", "profiled"))
             for d in ids:
                 if preg[d] in ("timed", "profiled"):
                     for n, v in pk[d].items():
@@ -147,7 +153,8 @@ def main():
     mean = collections.defaultdict(float)  # summed over the frame kernels, per launch
     by_kernel = {}
     for k, cs in ctr.items():
-        by_kernel[k] = {n: sum(v) / len(v) for n, v in cs.items()}
+        # per launch: every dispatch of the kernel in those regions / their launches
+        by_kernel[k] = {n: sum(v) / nl[k] for n, v in cs.items()}
         for n, m in by_kernel[k].items():
             mean[n] += m
     out["pmc_per_launch_by_kernel"] = by_kernel
