@@ -93,6 +93,7 @@ def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per
            "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(launch_ms, 4)}
     if not pj or "sq_insts_valu_per_launch" not in pj:
         out = dict(alg)
+        out["kernel"], out["kernels"] = kname, alg["kernel"]  # the dominant kernel names the shape
         out["traffic"] = None
         out["note"] = "no committed PMC profile of this command's shape: algorithmic roofline only"
         return out

@@ -69,7 +69,10 @@ def main():
     dst = os.path.join(ROOT, "profiles")
     line = bench_line(os.path.join(src, "trace.log"))
     launches = line["launches"]
-    kname = line["roofline"]["kernel"]  # the dominant kernel (k_trace; k_reflect for reflection frames)
+    kname = line["roofline"]["kernel"]  # the dominant kernel (k_trace; k_shadow / k_reflect for reflection frames)
+    if kname not in FRAME_KERNELS:  # a line whose fallback roofline named the frame's kernel list
+        b, o = line["config"].get("bounces", 0), line["config"].get("options", 0)
+        kname = ("k_reflect" if o & 512 else "k_shadow") if b else "k_primary"
     alg = line["roofline"].get("algorithmic", line["roofline"])
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats_avg = {}
