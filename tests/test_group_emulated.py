@@ -81,6 +81,41 @@ def test_emulated_world_full_frames(ctx, views, world, tile, tile_h, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,tile,chains", [(4, 8, False), (2, 32, True), (1, None, False)])
+def test_emulated_world_reflections(ctx, env, world, tile, chains):
+    """configs[4] (3 bounces) through the frame group: each rank's share traced with the
+    reflection level waves (k_pack walks the share's own block table) or the chains, packed,
+    gathered and unpacked; frames equal the single-call draw() (itself checked against the
+    oracle in test_config4.py) on every pixel."""
+    import dataclasses
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib as L
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W2, H2 = 640, 360
+    mut = dataclasses.replace(env.mutable(), max_bounces=3)
+    ctx.set_options(L.MIRT_OPT_REFLECT_CHAINS if chains else 0)
+    try:
+        ref = rt.draw(env, W2, H2, mut)
+        assert ref.valid.sum() > 1000
+        g = NativeFrameGroup(ctx, W2, H2, 0, 1, tile, inflight=2, emulate=world if world > 1 else 0)
+        try:
+            for _ in range(3):
+                g.render(mut.to_frame())
+            g.wait()
+            torch.cuda.synchronize()
+            for k in range(2):
+                got = g.frames[k]
+                assert np.array_equal(got.valid.cpu().numpy(), ref.valid), f"frame {k}: valid differs"
+                assert np.array_equal(got.rgb8.cpu().numpy(), ref.rgb8), f"frame {k}: rgb8 differs"
+        finally:
+            g.close()
+            ctx.set_grid()
+    finally:
+        ctx.set_options(0)
+
+
+@pytest.mark.gpu
 def test_bench_path_full_frame(ctx, views):
     """The bench's own configuration (whole screen, 8 frames in flight, 2 frames per
     k_trace launch, frame records staged per launch): every pixel of each frame, valid,
