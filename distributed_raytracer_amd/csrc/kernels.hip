@@ -322,19 +322,9 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
                                            const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
     if (MIRT_EXP_NO_TRI_TESTS || (MIRT_EXP_NO_SHADOW_TESTS && TPRE)) return;
-    auto one = [&](uint32_t i) {
+    // the fp64 test of triangle i on the lanes `maybe` leaves
+    auto test = [&](uint32_t i, bool maybe) {
         const uint32_t k = pos0 + i;
-        bool maybe = true;
-        if (TPRE && PREFILTER && lt) {  // wave-uniform
-            const u32x16 a16 = ((cv16ptr)(lt + (size_t)i * kLtD))[0];  // one s_load_dwordx16
-            float w[kLtD];
-#pragma unroll
-            for (int q = 0; q < kLtD; ++q) w[q] = __uint_as_float(a16[q]);
-            maybe = live && !seg_reject(*sp, w);
-            diag(22);  // light-table classifications (shadow)
-            // every lane rejected: the wave skips the triangle (its fp64 record is not read)
-            if (__ballot(maybe) == 0) return;
-        }
         const auto t = src + (size_t)i * kTriD;
         V3 p1or = REL ? V3{t[0], t[1], t[2]} : sub(ro, V3{t[0], t[1], t[2]});
         V3 e1{t[3], t[4], t[5]};
@@ -347,15 +337,35 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
         }
     };
-    if (TPRE) {
-        // unrolled by two by hand: a loop holding a ballot is not runtime-unrolled
+    // light-table classification of triangle i from its record (in SGPRs)
+    auto classify = [&](const u32x16& a16) {
+        float w[kLtD];
+#pragma unroll
+        for (int q = 0; q < kLtD; ++q) w[q] = __uint_as_float(a16[q]);
+        diag(22);  // light-table classifications (shadow)
+        return live & !seg_reject(*sp, w);  // (no short circuit: straight-line code)
+    };
+    if (TPRE && PREFILTER && lt) {
+        // two triangles per step, both records loaded up front (one scalar-load wait per pair);
+        // a wave whose lanes all reject a triangle skips its fp64 record
         for (uint32_t i = 0; i < n; i += 2) {
-            one(i);
-            if (i + 1 < n) one(i + 1);
+            const bool two = i + 1 < n;
+            const u32x16 r0 = ((cv16ptr)(lt + (size_t)i * kLtD))[0];
+            const u32x16 r1 = ((cv16ptr)(lt + (size_t)(two ? i + 1 : i) * kLtD))[0];
+            const bool m0 = classify(r0);
+            const bool m1 = two & classify(r1);
+            if (__ballot(m0) != 0) test(i, m0);
+            if (__ballot(m1) != 0) test(i + 1, m1);
+        }
+    } else if (TPRE) {
+        // unrolled by two by hand, as the classified loop above
+        for (uint32_t i = 0; i < n; i += 2) {
+            test(i, true);
+            if (i + 1 < n) test(i + 1, true);
         }
     } else {
 #pragma unroll 2
-        for (uint32_t i = 0; i < n; ++i) one(i);
+        for (uint32_t i = 0; i < n; ++i) test(i, true);
     }
 }
 
