@@ -348,6 +348,16 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
     if (TPRE && PREFILTER && lt) {
         // two triangles per step, both records loaded up front (one scalar-load wait per pair);
         // a wave whose lanes all reject a triangle skips its fp64 record
+        if (n == 3) {  // the default leaf: all three records up front
+            const u32x16 r0 = ((cv16ptr)lt)[0];
+            const u32x16 r1 = ((cv16ptr)(lt + kLtD))[0];
+            const u32x16 r2 = ((cv16ptr)(lt + 2 * kLtD))[0];
+            const bool m0 = classify(r0), m1 = classify(r1), m2 = classify(r2);
+            if (__ballot(m0) != 0) test(0, m0);
+            if (__ballot(m1) != 0) test(1, m1);
+            if (__ballot(m2) != 0) test(2, m2);
+            return;
+        }
         for (uint32_t i = 0; i < n; i += 2) {
             const bool two = i + 1 < n;
             const u32x16 r0 = ((cv16ptr)(lt + (size_t)i * kLtD))[0];
