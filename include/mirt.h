@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 4
+#define MIRT_ABI_VERSION 5
 
 /* error codes */
 #define MIRT_OK 0
