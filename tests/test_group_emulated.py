@@ -116,6 +116,33 @@ def test_emulated_world_reflections(ctx, env, world, tile, chains):
 
 
 @pytest.mark.gpu
+def test_adaptive_grid_lone_and_burst_frames(ctx, views, monkeypatch):
+    """MIRT_ADAPTIVE_GRID=2: a frame issued while none runs gets the whole chip's grid, a
+    frame of a burst the fixed one; one slot sees both launch shapes in turn (its hit
+    buffers are sized for any grid) and every frame equals the oracle."""
+    import torch
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_ADAPTIVE_GRID", "2")
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=2)
+    try:
+        for k, name in enumerate(ORDER):
+            g.render(views[name][0])
+            if k % 3 == 0:  # a lone frame next: nothing left running
+                g.wait()
+                torch.cuda.synchronize()
+                got = g.frames[k % 2]
+                _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[name][1], f"frame {k} ({name})")
+        g.wait()
+        torch.cuda.synchronize()
+        for k in range(len(ORDER) - 2, len(ORDER)):
+            got = g.frames[k % 2]
+            _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[ORDER[k]][1], f"frame {k} ({ORDER[k]})")
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 def test_bench_path_full_frame(ctx, views):
     """The bench's own configuration (whole screen, 8 frames in flight, 2 frames per
     k_trace launch, frame records staged per launch): every pixel of each frame, valid,
