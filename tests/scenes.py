@@ -80,6 +80,77 @@ def box_mesh(size=1.0) -> PyMesh:
                   materials=np.array([DEFAULT_MATERIAL], np.float64))
 
 
+def triangle_soup(rng, n: int, spread: float = 1.0, with_normals: bool = True, nmat: int = 3) -> PyMesh:
+    """A seeded soup of n triangles in float32 vertices (as an OBJ parse gives them):
+    mostly small clustered triangles, some sharing a vertex with the previous one, some
+    long slivers, collinear and repeated-vertex (zero-area) faces, several materials."""
+    verts, fv = [], []
+
+    def vert(p):
+        verts.append(p)
+        return len(verts) - 1
+
+    for i in range(n):
+        c = rng.normal(scale=spread, size=3)
+        kind = rng.random()
+        if kind < 0.70:
+            idx = [vert(c + rng.normal(scale=0.15 * spread, size=3)) for _ in range(3)]
+            if fv and rng.random() < 0.3:
+                idx[0] = fv[-1][int(rng.integers(3))]  # shared vertex (connected faces)
+        elif kind < 0.85:  # sliver
+            a = c + rng.normal(scale=0.1 * spread, size=3)
+            b = a + rng.normal(scale=spread, size=3)
+            idx = [vert(a), vert(b), vert(a + 0.5 * (b - a) + rng.normal(scale=1e-3 * spread, size=3))]
+        elif kind < 0.93:  # collinear before the float32 rounding
+            a = c
+            d = rng.normal(scale=0.3 * spread, size=3)
+            idx = [vert(a), vert(a + d), vert(a + 2.5 * d)]
+        else:  # a repeated vertex: zero area
+            k = vert(c)
+            idx = [k, k, vert(c + rng.normal(scale=0.2 * spread, size=3))]
+        fv.append(idx)
+    V = f32(verts)
+    fv = np.array(fv, np.uint32)
+    mats = []
+    for _ in range(nmat):
+        ka = rng.uniform(0, 0.3, 3)
+        kd = rng.uniform(0, 1, 3)
+        ks = rng.uniform(0, 1, 3) * (rng.random() < 0.7)
+        mats.append(tuple(f32(np.concatenate([ka, kd, ks]))) + (float(rng.choice([0.0, 1.0, 10.0, 57.5])),))
+    if with_normals:
+        N = f32(rng.normal(size=(max(4, n // 2), 3)))
+        N = N / np.linalg.norm(N, axis=1, keepdims=True)
+        fn = rng.integers(len(N), size=(n, 3)).astype(np.uint32)
+    else:
+        N, fn = np.zeros((0, 3)), np.zeros((n, 3), np.uint32)
+    return PyMesh(vertices=V, normals=N, face_v=fv, face_n=fn,
+                  face_mat=rng.integers(nmat, size=n).astype(np.uint32), materials=np.array(mats, np.float64))
+
+
+def soup_scene(seed: int, ntri=(300, 700), vertex_light: bool = False) -> PyScene:
+    """Two soups (one without vertex normals) placed as 1-3 overlapping objects, 1-5 lights
+    (one inside the soups' extent; with vertex_light, one exactly on a vertex of the first
+    object), a camera looking at the middle."""
+    rng = np.random.default_rng(seed)
+    sc = PyScene()
+    sc.meshes = [triangle_soup(rng, ntri[0], 1.0, True), triangle_soup(rng, ntri[1], 1.5, False)]
+    nobj = int(rng.integers(1, 4))
+    sc.objects = [(k % 2, tuple(float(x) for x in rng.normal(scale=0.8, size=3))) for k in range(nobj)]
+    on_vertex = tuple(float(x) for x in sc.meshes[0].vertices[int(rng.integers(len(sc.meshes[0].vertices)))]
+                      + np.asarray(sc.objects[0][1]))
+    lights = [on_vertex if vertex_light else tuple(float(x) for x in rng.normal(scale=3.0, size=3)),
+              tuple(float(x) for x in rng.normal(scale=0.5, size=3))]
+    for _ in range(int(rng.integers(0, 4))):
+        lights.append(tuple(float(x) for x in rng.normal(scale=8.0, size=3)))
+    sc.lights = [(p, tuple(float(x) for x in rng.uniform(0, 1, 3))) for p in lights[:5]]
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    sc.cam_pos = tuple(float(x) for x in 6.0 * d)
+    sc.cam_dir = tuple(float(x) for x in -d + rng.normal(scale=0.05, size=3))
+    sc.fov = float(rng.uniform(0.6, 1.4))
+    return sc
+
+
 def multi_object_scene(suzanne: PyMesh) -> PyScene:
     """Two suzannes (one shadowing the other), a flat-shaded cube with the default
     material, and a sphere; four lights; an oblique camera."""
