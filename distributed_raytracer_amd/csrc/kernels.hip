@@ -1417,7 +1417,31 @@ struct LocalChunks {
     size_t base;
     uint8_t* frame_of;  // per chunk: its frame within the launch (k_trace)
     uint32_t frame;
+    uint32_t* ring;     // free positions of the hit-chunk ring (bit p: position p free)
+    uint16_t* pos;      // per chunk: its position in the region (< kHitRing: a ring position)
 };
+
+// Hit-chunk ring (k_trace): a chunk takes the lowest free one of kHitRing positions of the
+// workgroup's region and gives it back once shaded, so a frame's hit records dirty a few
+// ring positions per workgroup instead of one fresh 4 KB chunk per hit block (the L2
+// write-back of those lines was most of the frame's HBM writes).  A chunk that finds the
+// ring full takes position kHitRing + its index in the batch (never shared).
+__device__ __forceinline__ uint32_t ring_take(uint32_t* ring, uint32_t c) {
+    uint32_t p = kHitRing + c;
+    if (kHitRing > 0) {
+        uint32_t m = __hip_atomic_load(ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (m) {
+            const uint32_t b = __builtin_ctz(m), bit = 1u << b;
+            const uint32_t old = atomicAnd(ring, ~bit);
+            if (old & bit) {
+                p = b;
+                break;
+            }
+            m = old & ~bit;
+        }
+    }
+    return p;
+}
 template <bool REL, bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
@@ -1492,14 +1516,23 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
     const uint64_t mask = __ballot(is_hit);
     if (mask) {
         ws.hits += __popcll(mask);
-        uint32_t base = 0;
-        if (lane == 0) base = lc ? atomicAdd(lc->count, 1u) : atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
+        uint32_t base = 0, rp = 0;
+        if (lane == 0) {
+            if (lc) {
+                base = atomicAdd(lc->count, 1u);
+                rp = ring_take(lc->ring, base);
+                lc->pos[base] = (uint16_t)rp;  // LDS, in order before the ready flag
+            } else {
+                base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
+            }
+        }
         base = __builtin_amdgcn_readfirstlane(base);
+        rp = __builtin_amdgcn_readfirstlane(rp);
         // (the lane offset made here: base + lane hoisted out of the block loop stays live
         // across the traversal as a 64-bit pair, and k_trace spilled it to scratch)
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
-        const size_t slot = lc ? (size_t)(lc->base + (size_t)base * 64) + ln : (size_t)q * wa.hit_cap + base + lane;
+        const size_t slot = lc ? (size_t)(lc->base + (size_t)rp * 64) + ln : (size_t)q * wa.hit_cap + base + lane;
         // bounce waves: the block's hit chunk, for k_pack's walk in block order
         if (!lc && wa.bmap && blk != ~0u && lane == 0) {
             wa.bmap[blk] = (uint32_t)(((size_t)q * wa.hit_cap + base) / 64 + 1) << 7 | (uint32_t)__popcll(mask);
@@ -1790,7 +1823,8 @@ template <bool PREFILTER, bool BRUTE>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u,
-                                            const ViewCache* vc = nullptr, uint32_t lim = 64) {
+                                            const ViewCache* vc = nullptr, uint32_t lim = 64,
+                                            uint32_t* ring = nullptr, uint32_t rpos = ~0u) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
@@ -1842,30 +1876,44 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     uint32_t done = 0;
     if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
     done = __builtin_amdgcn_readfirstlane(done);
-    if (done != nl - 1 || !active) return;
-    const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
-    const V3 n{bitsd(ld64(w + 3)), bitsd(ld64(w + 4)), bitsd(ld64(w + 5))};
-    const uint64_t oidx = ld64(w + 6);
-    const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
-    const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
-    if (wa.bounces) {  // the level's phong: the reflection fold combines the levels and writes the pixel
-        double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot) * wa.ph_stride;
-        e[0] = col.r;
-        e[1] = col.g;
-        e[2] = col.b;
+    if (done != nl - 1) return;
+    auto shade = [&]() {
+        const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
+        const V3 n{bitsd(ld64(w + 3)), bitsd(ld64(w + 4)), bitsd(ld64(w + 5))};
+        const uint64_t oidx = ld64(w + 6);
+        const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
+        const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+        if (wa.bounces) {  // the level's phong: the reflection fold combines the levels and writes the pixel
+            double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot) * wa.ph_stride;
+            e[0] = col.r;
+            e[1] = col.g;
+            e[2] = col.b;
+            return;
+        }
+        if (out.rgb) {
+            out.rgb[3 * oidx] = col.r;
+            out.rgb[3 * oidx + 1] = col.g;
+            out.rgb[3 * oidx + 2] = col.b;
+        }
+        if (out.rgb8) {
+            out.rgb8[3 * oidx] = c_u8(col.r);
+            out.rgb8[3 * oidx + 1] = c_u8(col.g);
+            out.rgb8[3 * oidx + 2] = c_u8(col.b);
+        }
+        if (out.rgbv) out.rgbv[oidx] = pack_rgbv(col);
+    };
+    // ring (k_trace): the position goes back to the workgroup's ring once every access to
+    // the chunk has completed (the other lights' waves counted themselves done after theirs;
+    // this wave's own loads are waited for)
+    if (ring && rpos < kHitRing) {
+        if (active) shade();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) atomicOr(ring, 1u << rpos);
         return;
     }
-    if (out.rgb) {
-        out.rgb[3 * oidx] = col.r;
-        out.rgb[3 * oidx + 1] = col.g;
-        out.rgb[3 * oidx + 2] = col.b;
-    }
-    if (out.rgb8) {
-        out.rgb8[3 * oidx] = c_u8(col.r);
-        out.rgb8[3 * oidx + 1] = c_u8(col.g);
-        out.rgb8[3 * oidx + 2] = c_u8(col.b);
-    }
-    if (out.rgbv) out.rgbv[oidx] = pack_rgbv(col);
+    if (!active) return;
+    shade();
 }
 
 // ---------------------------------------------------------------- primary kernel
@@ -2035,7 +2083,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __shared__ uint32_t s_bucket[kQueueBuckets];
     __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
-    __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back;
+    __shared__ uint16_t chunk_pos[kBlkQ];  // each chunk's position in the region (ring_take)
+    __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back, s_ring;
     __shared__ ViewHead s_vhead[VIEWS ? kMaxViewTables : 1];
     __shared__ uint32_t s_vstate[VIEWS ? kMaxViewTables : 1];
     const ViewCache vc{s_vhead, s_vstate};
@@ -2071,7 +2120,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     uint32_t spins = 0;
     const uint32_t G = gridDim.x;
     const uint32_t mine = wa.nblocks > blockIdx.x ? (wa.nblocks - blockIdx.x + G - 1) / G : 0u;
-    size_t chunk0 = (size_t)blockIdx.x * wa.wg_cap;  // slot of this batch's chunk 0
+    const size_t chunk0 = (size_t)blockIdx.x * wa.wg_cap;  // slot of the region's position 0
     auto lds_ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto lds_inc = [](uint32_t* p) {
         uint32_t t = 0;
@@ -2148,12 +2197,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
             bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
             bq_frame[slot] = (uint8_t)qf;
         }
-        if (threadIdx.x == 0) s_prim = s_pdone = s_chunks = s_item = 0;
+        if (threadIdx.x == 0) {
+            s_prim = s_pdone = s_chunks = s_item = 0;
+            s_ring = kHitRing >= 32 ? ~0u : (1u << kHitRing) - 1u;  // every ring position free
+        }
         if (c0 == 0) clock.mark_staged();
         __syncthreads();
         // queued blocks: [0, s_front) and [s_back, nc); ticket q is entry q or q - nfront + s_back
         const uint32_t nfront = s_front, back0 = s_back, nq = nfront + (nc - back0);
-        LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0};
+        LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0, &s_ring, chunk_pos};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
         for (;;) {
             // 1. a shadow item of an allocated chunk
@@ -2172,8 +2224,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                 const WaveStats before = wsh;
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
                 const FrameRec& fr = frame_rec(frames, cf);
-                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)c * 64, l,
-                                              wsh, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr);
+                const uint32_t cp = __builtin_amdgcn_readfirstlane(chunk_pos[c]);
+                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64, l,
+                                              wsh, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring, cp);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -2227,8 +2280,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
             diag(18);
             __builtin_amdgcn_s_sleep(1);
         }
-        __syncthreads();  // every wave is done with this batch before it is restaged
-        chunk0 += (size_t)s_chunks * 64;
+        // every wave is done with this batch (each chunk shaded, its ring position free)
+        // before it is restaged; the next batch reuses the region from position 0
         __syncthreads();
     }
     if (mine == 0) clock.mark_staged();

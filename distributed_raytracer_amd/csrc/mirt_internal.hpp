@@ -360,6 +360,13 @@ constexpr int kReflD = 4;  // doubles per slot and level of WorkArgs::refl
 // within the workgroup; shadow / reflect: the sharded device queues).
 enum { kDynPrimary = 1, kDynShadow = 2, kDynReflect = 4 };
 constexpr int kBlkQ = 256;  // primary block descriptors staged in LDS per batch
+// k_trace hit-chunk ring positions per workgroup (kernels.hip ring_take; 0: every chunk of
+// a batch gets a fresh position); a workgroup's region holds kHitRing + its blocks' chunks.
+#ifndef MIRT_HIT_RING
+#define MIRT_HIT_RING 8
+#endif
+constexpr uint32_t kHitRing = MIRT_HIT_RING;
+static_assert(kHitRing <= 32, "the ring's free positions are one 32-bit LDS word");
 
 // Arbitrary-ray inputs/outputs for mirt_trace_rays.
 struct RayIO {
