@@ -1877,12 +1877,15 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
     done = __builtin_amdgcn_readfirstlane(done);
     if (done != nl - 1) return;
-    auto shade = [&]() {
+    // Phong of the lane's hit (tracer.go:53-76) once its lit word is complete, and its outputs
+    auto shade = [&](uint64_t& oidx) {
         const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
         const V3 n{bitsd(ld64(w + 3)), bitsd(ld64(w + 4)), bitsd(ld64(w + 5))};
-        const uint64_t oidx = ld64(w + 6);
+        oidx = ld64(w + 6);
         const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
-        const RGB col = phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+        return phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+    };
+    auto store = [&](uint64_t oidx, const RGB& col) {
         if (wa.bounces) {  // the level's phong: the reflection fold combines the levels and writes the pixel
             double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot) * wa.ph_stride;
             e[0] = col.r;
@@ -1902,18 +1905,24 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
         }
         if (out.rgbv) out.rgbv[oidx] = pack_rgbv(col);
     };
-    // ring (k_trace): the position goes back to the workgroup's ring once every access to
-    // the chunk has completed (the other lights' waves counted themselves done after theirs;
-    // this wave's own loads are waited for)
+    // ring (k_trace): the position goes back to the workgroup's ring once every access to the
+    // chunk has completed: the other lights' waves counted themselves done after theirs, and
+    // this wave's loads were consumed by phong (the wait has nothing else to wait for: the
+    // output stores are issued after the release)
     if (ring && rpos < kHitRing) {
-        if (active) shade();
+        RGB col{0, 0, 0};
+        uint64_t oidx = 0;
+        if (active) col = shade(oidx);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) atomicOr(ring, 1u << rpos);
+        if (active) store(oidx, col);
         return;
     }
     if (!active) return;
-    shade();
+    uint64_t oidx = 0;
+    const RGB col = shade(oidx);
+    store(oidx, col);
 }
 
 // ---------------------------------------------------------------- primary kernel
