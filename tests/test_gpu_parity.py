@@ -802,3 +802,32 @@ def test_1080p_frame_group_bench_path_matches_oracle(ctx, env, py_scene, infligh
         assert int(valid.sum()) == 209584
     finally:
         g.close()
+
+
+
+@pytest.mark.parametrize("max_wg", [1, 3])
+def test_hit_chunk_ring_many_batches_per_workgroup(ctx, env, oracle, max_wg):
+    """k_trace's hit-chunk ring (kernels.hip ring_take) under the heaviest
+    reuse: 1 or 3 workgroups for a 640x480 frame (4,800 blocks: up to 19 batches of 256 blocks
+    per workgroup, hundreds of hit chunks through 8 ring positions, and positions past the ring
+    whenever more than 8 chunks are live).  The default camera's frame must equal the oracle's;
+    a close camera (more hit blocks) must equal the default grid's frame."""
+    import distributed_raytracer_amd as rt
+    W, H = 640, 480
+    base = env.mutable()
+    c = base.cam
+    close = rt.EnvMutables(base.objects, base.lights, rt.Camera.new(tuple(np.asarray(c.pos) * 0.55), c.forward, c.fov))
+    ctx.set_grid(1, max_wg)
+    try:
+        fb = rt.draw(env, W, H)
+        fc = rt.draw(env, W, H, close)
+    finally:
+        ctx.set_grid()
+    ref = oracle.frame(W, H, nthreads=8)
+    assert np.array_equal(fb.valid, ref["valid"])
+    assert np.array_equal(fb.rgb, ref["rgb"])
+    assert np.array_equal(fb.rgb8, ref["rgb8"])
+    full = rt.draw(env, W, H, close)
+    assert int(full.valid.sum()) > int(fb.valid.sum())  # the close view hits more pixels
+    assert np.array_equal(fc.valid, full.valid) and np.array_equal(fc.rgb, full.rgb)
+    assert np.array_equal(fc.rgb8, full.rgb8)
