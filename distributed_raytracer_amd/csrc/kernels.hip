@@ -316,7 +316,7 @@ __device__ __forceinline__ bool seg_reject(const SegPre& p, const float* w) {
 // record of position pos0 (in LDS or in HBM).
 //   lt (shadow segments; NULL: none): the light table at position pos0 (kLtD floats per
 //   triangle), sp the lane's SegPre, live the lanes whose result still matters.
-template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, typename SrcPtr>
+template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, bool LT3 = true, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests,
                                            const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true) {
@@ -348,7 +348,7 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
     if (TPRE && PREFILTER && lt) {
         // two triangles per step, both records loaded up front (one scalar-load wait per pair);
         // a wave whose lanes all reject a triangle skips its fp64 record
-        if (n == 3) {  // the default leaf: all three records up front
+        if (LT3 && n == 3) {  // the default leaf: all three records up front
             const u32x16 r0 = ((cv16ptr)lt)[0];
             const u32x16 r1 = ((cv16ptr)(lt + kLtD))[0];
             const u32x16 r2 = ((cv16ptr)(lt + 2 * kLtD))[0];
@@ -640,7 +640,7 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 //   made); the walk ends when no live lane is left.
 // Packets with a lane whose object-space origin is beyond the cull limit (the inflation
 // argument needs a bounded origin) enter every child.
-template <bool REL, bool PREFILTER, bool SEG, typename SrcPtr>
+template <bool REL, bool PREFILTER, bool SEG, bool LT3 = true, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
                                           Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true,
                                           const float* lt = nullptr, const SegPre* sp = nullptr) {
@@ -661,7 +661,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
             diag(SEG ? 14 : 6);
-            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
+            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
                                                     vis.tests, lt ? lt + (size_t)first * kLtD : nullptr, sp, live);
             if (SEG) {
                 live = live && !(b.has && b.d < resolve);
@@ -1099,7 +1099,9 @@ __device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__
 // otherwise the nearest candidate found is the true nearest and the reference comparison
 // runs unchanged.  M bounds every fp64 rounding involved with a wide margin.
 //   vt / vh (LDS-resident): the light's view table and header (view_sweep from the light).
-template <bool PREFILTER>
+//   LT3: a three-face leaf loads its three light-table records at once (k_trace; the split
+//   k_shadow loads two per step, which spills fewer VGPRs there)
+template <bool PREFILTER, bool LT3 = true>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
                                                   uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, uint32_t li,
                                                   bool lane_on, Visits& vis, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
@@ -1168,10 +1170,10 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         SegPre sp;
         if (lt) sp = seg_pre(d, lh);
         if (resident)
-            bvh_sweep<false, PREFILTER, true>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
+            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
                                               !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
         else
-            bvh_sweep<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
+            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
                                               !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
     }
     if (b.has && b.d < resolve) return false;
@@ -1814,12 +1816,18 @@ __device__ __forceinline__ const ViewHead* view_lookup(const WorkArgs& wa, uint3
 
 
 
+// k_shadow (split kernels, reflection levels): three light-table records per leaf at once (1)
+// or two per step (0); see shadow_lit_single.
+#ifndef MIRT_SHADOW_LT3
+#define MIRT_SHADOW_LT3 0
+#endif
+
 // ---------------------------------------------------------------- shadow item
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
 // the wave that finishes the chunk's last light.  n_lights == 0: one pass that shades.
 //   vf: the chunk's frame within the launch (its view tables, k_trace), ~0u: none.
-template <bool PREFILTER, bool BRUTE>
+template <bool PREFILTER, bool BRUTE, bool LT3 = true>
 __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u,
@@ -1854,7 +1862,7 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
             vh = view_lookup(wa, q, *vc);
             if (vh) vt = wa.views + (size_t)q * wa.view_leaves;
         }
-        is_lit = shadow_lit_single<PREFILTER>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, vt, wa.view_leaves,
+        is_lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, vt, wa.view_leaves,
                                               vh);
     } else {
         Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis);
@@ -2039,7 +2047,7 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             const uint32_t nxt = dyn ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            shadow_item<PREFILTER, BRUTE>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
                                           (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, ~0u, nullptr,
                                           min(64u, nrec - c * 64));
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
