@@ -2235,6 +2235,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                     __builtin_amdgcn_s_sleep(1);
                 }
                 if (spins >= kSpinLimit) break;
+                // the chunk's LDS records (position, frame) are read after its ready flag: the
+                // producer wrote them first, and LDS operations complete in order
+                asm volatile("" ::: "memory");
                 ++taken;
                 diag(19);
                 ic.start();
