@@ -1806,6 +1806,7 @@ struct mirt_group {
     std::vector<uint64_t> slot_bad;     // per frame slot: deal indices whose transfer failed
     // fault handling (master/pool/pool.go:224-260, master/main.go:111-161)
     uint32_t timeout_ms = 0;
+    bool spin_wait = false;  // MIRT_WAIT=spin: poll completion events (no blocking wait)
     uint64_t failed_mask = 0;           // ranks (not deal indices) named by the last failure
     uint64_t pending_bad = 0;           // deal indices failed since the last mirt_group_wait
     uint64_t pending_bad_frame = ~0ull;
@@ -1827,20 +1828,26 @@ void group_ring(mirt_group* g) {
 }
 
 // Wait for a group event, within the group's deadline (0: no deadline).
+// Polling: the first kSpinWaitUs are a busy poll (a frame completes within tens of
+// microseconds, and a sleep would add the OS timer slack, ~50 us, to the wait), then 20 us
+// sleeps between polls.
+constexpr uint64_t kSpinWaitUs = 2000;
 int group_wait_event(mirt_group* g, hipEvent_t ev, const char* what) {
-    if (!g->timeout_ms) {
+    if (!g->timeout_ms && !g->spin_wait) {
         HIP_TRY(hipEventSynchronize(ev));
         return MIRT_OK;
     }
-    const uint64_t deadline = now_us() + (uint64_t)g->timeout_ms * 1000;
-    for (uint32_t spin = 0;; ++spin) {
+    const uint64_t t0 = now_us();
+    const uint64_t deadline = g->timeout_ms ? t0 + (uint64_t)g->timeout_ms * 1000 : UINT64_MAX;
+    for (;;) {
         const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return MIRT_OK;
         if (e != hipErrorNotReady) return hip_fail(e, what);
-        if (now_us() > deadline)
+        const uint64_t now = now_us();
+        if (now > deadline)
             return fail(MIRT_E_TIMEOUT, std::string(what) + ": no completion within " + std::to_string(g->timeout_ms) +
                                             " ms");
-        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (now - t0 > kSpinWaitUs) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
 
@@ -2273,6 +2280,8 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->d2h_sdma = d2h && !strcmp(d2h, "sdma");
     const char* ag = getenv("MIRT_ADAPTIVE_GRID");
     if (ag) g->adaptive_grid = (uint32_t)std::min(std::max(atoi(ag), 0), 2);
+    const char* wt = getenv("MIRT_WAIT");
+    if (wt) g->spin_wait = !strcmp(wt, "spin");
     // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
     // N-way deal (MIRT_GROUP_REHEARSE_RANK, default 0) and unpack all N regions, the others
     // stale: the root's per-frame GPU work at N GPUs without the transfers.  Results are
