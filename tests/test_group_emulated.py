@@ -167,13 +167,15 @@ def test_bench_path_full_frame(ctx, views):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile,emulate", [(None, 0), (8, 8)])
-def test_host_output_frames(ctx, views, tile, emulate):
+@pytest.mark.parametrize("tile,emulate,wait", [(None, 0, "sync"), (8, 8, "sync"), (None, 0, "spin"), (8, 8, "spin")])
+def test_host_output_frames(ctx, views, tile, emulate, wait, monkeypatch):
     """mirt_group_set_host_output: the assembled frame lands in pinned host memory (the copy
     kernel covers only each column's hit span and the slot's previous one); the host planes
     equal the oracle on every pixel while the rectangle moves and empties between frames,
-    and after host output was switched off and on again."""
+    and after host output was switched off and on again.  wait: the group's completion waits
+    (MIRT_WAIT, read at creation): blocking, or polled events."""
     from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_WAIT", wait)
     g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=2, batch=1, emulate=emulate, host_output=True)
     try:
         prev = None
