@@ -28,6 +28,7 @@ cpu_baseline.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -155,6 +156,11 @@ def parse():
                          "frame (the scene camera orbited about the first object, --orbit-deg per frame, "
                          "NewCamera per frame), as the reference master issues frames while the camera moves")
     ap.add_argument("--orbit-deg", type=float, default=1.0, help="orbit step per frame (degrees)")
+    ap.add_argument("--lights", choices=("static", "orbit"), default="static",
+                    help="static: the scene's lights every frame; orbit: every light moves every frame (orbited "
+                         "about the first object by --light-deg per frame), as EnvMutables diffs may carry "
+                         "(environment.go:65-69): a new light-table key every frame")
+    ap.add_argument("--light-deg", type=float, default=2.0, help="light orbit step per frame (degrees)")
     ap.add_argument("--no-d2h", action="store_true", help="leave the assembled frames in HBM (no host output)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -283,18 +289,39 @@ def orbit_cameras(cam_pos, cam_dir, fov, center, n: int, step_deg: float):
     return out
 
 
+def orbit_lights(lights, center, n: int, step_deg: float):
+    """n light sets: every light of the scene rotated about the world y axis through `center`
+    by step_deg x k in frame k (positions only; colours kept).  Frame data only."""
+    import math
+    c = np.asarray(center, np.float64)
+    out = []
+    for k in range(n):
+        a = math.radians(step_deg * k)
+        ca, sa = math.cos(a), math.sin(a)
+        ls = []
+        for lt in lights:
+            r = np.asarray(lt.pos, np.float64) - c
+            ls.append(dataclasses.replace(lt, pos=tuple(float(x) for x in
+                                                        c + np.array([ca * r[0] + sa * r[2], r[1], -sa * r[0] + ca * r[2]]))))
+        out.append(ls)
+    return out
+
+
 def parity_check(fb_valid: np.ndarray, fb_rgb8: np.ndarray, scene_path: str, W: int, H: int,
-                 bounces: int = 0, camera=None) -> dict:
+                 bounces: int = 0, camera=None, lights=None) -> dict:
     """Parity gate of the timed frames: EVERY pixel of the last timed
     frame against the oracle (R-tree restatement, 16 threads), valid mask and rgb8
     bit-exact; with the D2H on, the frame checked is the host copy."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
     sc = load_scene(scene_path)
-    if camera is not None:  # the moving-camera line's last timed frame
+    if camera is not None or lights is not None:  # a moving camera's / moving lights' last timed frame
         import copy
         sc = copy.copy(sc)
-        sc.cam_pos, sc.cam_dir, sc.fov = tuple(map(float, camera[0])), tuple(map(float, camera[1])), float(camera[2])
+        if camera is not None:
+            sc.cam_pos, sc.cam_dir, sc.fov = tuple(map(float, camera[0])), tuple(map(float, camera[1])), float(camera[2])
+        if lights is not None:
+            sc.lights = [(tuple(lt.pos), tuple(lt.col)) for lt in lights]
     orc = Oracle(sc, use_rtree=True)
     orc.set_bounces(bounces)
     ref = orc.frame(W, H, nthreads=HOST_CORES)
@@ -357,12 +384,21 @@ def main():
     import dataclasses
     base = dataclasses.replace(env.mutable(), max_bounces=a.bounces)
     cams = [None]
+    lsets = [None]
+    nseq = max(a.steps, a.warmup) if (a.camera == "orbit" or a.lights == "orbit") else 1
     if a.camera == "orbit":
         c = base.cam
-        cams = orbit_cameras(c.pos, c.forward, c.fov, base.objects[0].pos, max(a.steps, a.warmup), a.orbit_deg)
-        seq = [dataclasses.replace(base, cam=rt.Camera.new(*cam)).to_frame() for cam in cams]
-    else:
-        seq = [base.to_frame()]
+        cams = orbit_cameras(c.pos, c.forward, c.fov, base.objects[0].pos, nseq, a.orbit_deg)
+    if a.lights == "orbit":
+        lsets = orbit_lights(base.lights, base.objects[0].pos, nseq, a.light_deg)
+    seq = []
+    for k in range(nseq):
+        m = base
+        if a.camera == "orbit":
+            m = dataclasses.replace(m, cam=rt.Camera.new(*cams[k]))
+        if a.lights == "orbit":
+            m = dataclasses.replace(m, lights=lsets[k])
+        seq.append(m.to_frame())
 
     def frame_at(k):
         return seq[k % len(seq)]
@@ -539,6 +575,8 @@ def main():
         shape = {"width": W, "height": H, "gpus": world, "inflight": a.inflight, "batch": a.batch,
                  "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname,
                  "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera}
+        if a.lights != "static":
+            shape["lights"] = a.lights
         pj, pj_path = find_profile(a.profile_json, shape)
         frames_per_launch = pl / nlaunch
         dev_ms = dev_elapsed / steps * 1e3 if dev_elapsed else ms
@@ -561,13 +599,16 @@ def main():
                          "static frame-0 camera" if a.camera == "static" else
                          f"camera orbiting the object {a.orbit_deg} deg per frame (a new camera every frame)")
                      if os.path.abspath(a.scene) == os.path.abspath(SCENE) else
-                     f"synthetic: {os.path.relpath(a.scene, ROOT)} ({tris} tris, {nl} lights), the scene's camera"),
+                     f"synthetic: {os.path.relpath(a.scene, ROOT)} ({tris} tris, {nl} lights), the scene's camera") + (
+                     f"; lights orbiting the object {a.light_deg} deg per frame (a new light set every frame)"
+                     if a.lights == "orbit" else ""),
             "config": {"workload": workload_name(a, W, H, tris, nl), "width": W, "height": H, "triangles": tris,
                        "lights": nl, "parallelism": f"image tiles x{world}" + (f" ({a.tile}px, RCCL gather)"
                                                                                 if world > 1 else ""),
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)",
                        "d2h": "rgb8 + valid to pinned host memory inside the timed region" if d2h else "none (HBM)",
-                       "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera},
+                       "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera,
+                       "lights": a.lights},
             "frames_in_flight": getattr(sh, "F", a.inflight),
             "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,
@@ -588,6 +629,7 @@ def main():
                            "reflect": round(prof["reflect_ms_sum"] / nlaunch, 4),
                            "frame_device": round(prof["frame_ms_sum"] / nlaunch, 4)},
             "launches": launches,
+            "light_cache": ctx.light_cache_stats(),
             "roofline": roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch,
                                        alg_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES, alg_kernel=alg_kernel),
         }
@@ -625,7 +667,8 @@ def main():
                 fr = sh.frame
                 rgb8, valid = fr.rgb8.cpu().numpy(), fr.valid.cpu().numpy()
             line["parity"] = parity_check(valid, rgb8, a.scene, W, H, a.bounces,
-                                          cams[(a.steps - 1) % len(cams)] if a.camera == "orbit" else None)
+                                          cams[(a.steps - 1) % len(cams)] if a.camera == "orbit" else None,
+                                          lsets[(a.steps - 1) % len(lsets)] if a.lights == "orbit" else None)
             line["parity"]["frame"] = "host copy (D2H)" if host_last is not None else "device framebuffer"
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.scene, W, H)

@@ -36,6 +36,7 @@ MIRT_OPT_NO_OCTANT = 128
 MIRT_OPT_VIEWS = 256
 MIRT_OPT_REFLECT_CHAINS = 512
 MIRT_OPT_NO_LIGHT_TABLE = 1024
+MIRT_OPT_NO_BOX_GATE = 2048
 
 D3 = C.c_double * 3
 
@@ -153,6 +154,11 @@ SIGNATURES = {
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_debug_counters": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_debug_light_table": (C.c_int, [_P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, _P]),
+    "mirt_debug_light_table_gpu": (C.c_int, [_P, _P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, _P]),
+    "mirt_set_light_cache": (C.c_int, [_P, C.c_uint64]),
+    "mirt_light_cache_stats": (C.c_int, [_P, _P]),
+    "mirt_face_bounds": (None, [_P, _P, _P, _P]),
+    "mirt_object_bounds": (None, [_P, C.c_uint32, _P, _P]),
     "mirt_unpack_tiles_at_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "mirt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "mirt_scene_free": (None, [_P]),
@@ -192,6 +198,8 @@ def lib() -> C.CDLL:
                 f"There is no CPU fallback.")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("MIRT_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B (MIRT_LIB): entries it lacks stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -25,6 +25,8 @@
 // bit-identical to the CPU restatement (oracle/rt_oracle.c).
 #include "gomath.hpp"
 #include "mirt_internal.hpp"
+#include "diag.hpp"
+#include "lighttab.hpp"
 
 namespace mirt {
 
@@ -63,18 +65,6 @@ __device__ __forceinline__ bool r2_certainly_out(double n, double d) {
 // MIRT_DIAG (diagnostic builds only): wave-level event counts (how many waves reach each
 // stage of the triangle test, per query kind), read with mirt_debug_counters.  Counted by
 // the wave's first active lane into 8 shards.
-#ifndef MIRT_DIAG
-#define MIRT_DIAG 0
-#endif
-#ifndef MIRT_EXP_NO_PRIMARY_TRACE  // measurement builds only: every traced primary ray misses
-#define MIRT_EXP_NO_PRIMARY_TRACE 0
-#endif
-#ifndef MIRT_EXP_NO_TRI_TESTS  // measurement builds only: leaves are entered but never tested
-#define MIRT_EXP_NO_TRI_TESTS 0
-#endif
-#ifndef MIRT_EXP_NO_SHADOW_TESTS  // measurement builds only: shadow leaves entered, never tested (all lit)
-#define MIRT_EXP_NO_SHADOW_TESTS 0
-#endif
 constexpr int kDiagN = 32;
 __device__ unsigned long long g_diag[8 * kDiagN];
 __device__ __forceinline__ void diag(int k) {
@@ -91,9 +81,6 @@ __device__ __forceinline__ bool t_certainly_negative(double n, double d) {
     return n * __builtin_copysign(0x1p1000, d) < -__builtin_fabs(d);
 }
 
-#ifndef MIRT_TFIRST
-#define MIRT_TFIRST 0
-#endif
 // Möller–Trumbore exactly as triangle.go:37-77, on (p1or = O - P1, E1, E2), returning
 // only the hit decision and the ray parameter.  neg = D * -1 (triangle.go:38).
 //   DG: diagnostic counter base (MIRT_DIAG builds).
@@ -108,13 +95,9 @@ __device__ __forceinline__ bool mt_test(V3 p1or, V3 e1, V3 e2, V3 neg, double& t
     double inc = dot(e1, c);
     if (inc != 0.0) {
         double nt = 0.0;
-        if (MIRT_TFIRST && PREFILTER && TPRE) {  // the t pre-reject first (experiment)
-            nt = dot(e1, cross(e2, p1or));
-            if (t_certainly_negative(nt, inc)) return false;
-        }
         double n2 = dot(p1or, c);
         if (PREFILTER && r2_certainly_out(n2, inc)) return false;
-        if (!MIRT_TFIRST && PREFILTER && TPRE) {
+        if (PREFILTER && TPRE) {
             diag(DG + 7);
             nt = dot(e1, cross(e2, p1or));
             if (t_certainly_negative(nt, inc)) return false;
@@ -233,6 +216,7 @@ struct Best {
     uint32_t first;    // lowest original face index of any hit (0xffffffff: none)
     uint32_t first_pos;
     bool first_nan;    // that hit's distance is NaN
+    bool any_nan;      // some hit's distance is NaN (box_settle: the winner alone does not decide)
 };
 __device__ __forceinline__ void best_init(Best& b) {
     b.has = false;
@@ -241,9 +225,11 @@ __device__ __forceinline__ void best_init(Best& b) {
     b.first = 0xffffffffu;
     b.first_pos = 0;
     b.first_nan = false;
+    b.any_nan = false;
 }
 __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
     const bool isnan_d = dist != dist;
+    b.any_nan |= isnan_d;
     if (face < b.first) {
         b.first = face;
         b.first_pos = pos;
@@ -266,6 +252,48 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
         pos = b.pos;
     }
     return true;
+}
+
+// ---------------------------------------------------------------- the reference's box test
+// shared/geom/box.go:29-68 Box.Intersect of the ray (o, d) with a box given as NewBox's
+// corners bx = {MinCorner[3], MaxCorner[3]} (finite: the host builds them, mirt.cpp
+// face_box / object_box).  The reference ORs six planes; for the plane of normal +-e_A with
+// d_A != 0 it computes dirScale = (corner - o).n / d.n and checks the other two coordinates
+// of o + dirScale d against the rectangle.  With finite corners that is exactly
+//   ds = (corner_A - o_A) / d_A >= 0  and  lo_B <= o_B + ds d_B <= hi_B  (B != A):
+// x * 1 = x, (-a) / (-b) = a / b, and a zero-weighted term of the dot products is +-0 unless
+// a coordinate of o is not finite, where it is NaN and fails the plane — as the non-finite
+// coordinate of o + ds d fails the rectangle here.  (d.n != 0 is d_A != 0 for finite d; a NaN
+// d fails every plane both ways.)  The planes are pure tests, so any order gives the
+// reference's boolean.
+__device__ __forceinline__ double v3c(V3 v, int a) { return a == 0 ? v.x : a == 1 ? v.y : v.z; }
+// plane `hi` (MaxCorner, normal +e_a) or not (MinCorner, -e_a) of axis a (box.go:33-60)
+__device__ __forceinline__ bool box_plane(const double* bx, V3 o, V3 d, int a, bool hi) {
+    const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+    const double da = v3c(d, a);
+    const double ds = ((hi ? bx[3 + a] : bx[a]) - v3c(o, a)) / da;  // box.go:42
+    const double ib = v3c(o, b) + ds * v3c(d, b), ic = v3c(o, c) + ds * v3c(d, c);  // box.go:47
+    return da != 0.0 && ds >= 0.0 && bx[b] <= ib && ib <= bx[3 + b] && bx[c] <= ic && ic <= bx[3 + c];
+}
+// Box.Intersect for the lanes `on` (false on the others).  A ray that meets a box leaves it
+// through the far plane of some axis (+e_a for d_a > 0, -e_a for d_a < 0); the wave first
+// tries the far plane of the axis its first lane's direction leans on most (a wave-uniform
+// axis), and only the lanes that plane does not prove true go through the six planes, one
+// at a time (a short loop: this is the rare path).  Same boolean as the reference's.
+__device__ __forceinline__ bool box_gate(const double* bx, V3 o, V3 d, bool on) {
+    if (__ballot(on) == 0) return false;
+    const double ax = __builtin_fabs(d.x), ay = __builtin_fabs(d.y), az = __builtin_fabs(d.z);
+    const int lean = (ax >= ay && ax >= az) ? 0 : ay >= az ? 1 : 2;
+    const int a = __builtin_amdgcn_readfirstlane(lean);
+    bool r = false;
+    if (on) r = box_plane(bx, o, d, a, v3c(d, a) > 0.0);
+#pragma unroll 1
+    for (int q = 0; q < 6; ++q) {
+        const bool left = on && !r;
+        if (__ballot(left) == 0) break;
+        if (left) r = box_plane(bx, o, d, q >> 1, (q & 1) == 0);
+    }
+    return r;
 }
 
 // Shadow segments' fp32 pre-classification against a light table.  A
@@ -316,10 +344,13 @@ __device__ __forceinline__ bool seg_reject(const SegPre& p, const float* w) {
 // record of position pos0 (in LDS or in HBM).
 //   lt (shadow segments; NULL: none): the light table at position pos0 (kLtD floats per
 //   triangle), sp the lane's SegPre, live the lanes whose result still matters.
+//   fbox (non-null: a trace's second pass, trace_nearest / shadow_lit_single): a candidate
+//   counts only if its face box passes the reference's Box.Intersect (object.go:76).
 template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, bool LT3 = true, typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests,
-                                           const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true) {
+                                           const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true,
+                                           const double* fbox = nullptr) {
     wtests += n;  // wave-uniform: triangles this wave tests (x active lanes = tests)
     if (MIRT_EXP_NO_TRI_TESTS || (MIRT_EXP_NO_SHADOW_TESTS && TPRE)) return;
     // the fp64 test of triangle i on the lanes `maybe` leaves
@@ -332,7 +363,9 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         double tt;
         // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
         const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
-        if (maybe && mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt)) {
+        bool acc = maybe && mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt);
+        if (fbox) acc = box_gate(fbox + (size_t)k * kBoxD, ro, d, acc);  // wave-uniform branch
+        if (acc) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
         }
@@ -394,9 +427,6 @@ struct WaveStats {
 };
 // MIRT_PHASE_TIMING (diagnostic builds only): shader-clock cycles per phase of the primary
 // blocks, reported in the timeline record instead of the wave's start/end clocks.
-#ifndef MIRT_PHASE_TIMING
-#define MIRT_PHASE_TIMING 0
-#endif
 struct PhaseClock {
     uint64_t acc[4] = {0, 0, 0, 0};
     uint64_t t = 0;
@@ -640,10 +670,12 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 //   made); the walk ends when no live lane is left.
 // Packets with a lane whose object-space origin is beyond the cull limit (the inflation
 // argument needs a bounded origin) enter every child.
+//   fbox: candidates pass their face box first (test_range; a trace's second pass).
 template <bool REL, bool PREFILTER, bool SEG, bool LT3 = true, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
                                           Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true,
-                                          const float* lt = nullptr, const SegPre* sp = nullptr) {
+                                          const float* lt = nullptr, const SegPre* sp = nullptr,
+                                          const double* fbox = nullptr) {
     // LDS-resident meshes (the host guarantees depth <= kBvhShallowDepth) use a one-VGPR stack
     constexpr bool DEEP = !__is_same(SrcPtr, const double*);
     const Ray32 r = ray32(ro, d);
@@ -662,7 +694,7 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             ++vis.leaves;
             diag(SEG ? 14 : 6);
             test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
-                                                    vis.tests, lt ? lt + (size_t)first * kLtD : nullptr, sp, live);
+                                                    vis.tests, lt ? lt + (size_t)first * kLtD : nullptr, sp, live, fbox);
             if (SEG) {
                 live = live && !(b.has && b.d < resolve);
                 if (__ballot(live) == 0) break;
@@ -707,55 +739,17 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
 // launch, 72 B per face, after the kernel's static LDS (the launch passes 0 bytes otherwise).
 extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
 
-// Occupancy target of the tracing kernels (waves per SIMD) and LDS-resident meshes.
-#ifndef MIRT_WAVES_PER_EU
-#define MIRT_WAVES_PER_EU 4
-#endif
-#ifndef MIRT_LDS_MESH
-#define MIRT_LDS_MESH 1
-#endif
-#ifndef MIRT_BLOCK_FRUSTUM
-#define MIRT_BLOCK_FRUSTUM 1
-#endif
-#ifndef MIRT_EXP_NO_PHONG  // measurement builds only: ambient colour only
-#define MIRT_EXP_NO_PHONG 0
-#endif
-#ifndef MIRT_EXP_NO_SHADOW_TRACE  // measurement builds only: every light reaches every hit
-#define MIRT_EXP_NO_SHADOW_TRACE 0
-#endif
-#ifndef MIRT_SKIP_MISS_STORES  // measurement builds only (outputs left unwritten)
-#define MIRT_SKIP_MISS_STORES 0
-#endif
-// Traversal per kernel: 1 = wide cone traversal (shared-origin packets), 0 = per-lane
-// 8-child sweep with scalar node loads.  Measured on MI355X (suzanne 1080p): the sweep is
-// faster for both (profiles/r01_*); the wide walk stays for meshes where it wins.
-#ifndef MIRT_PRIMARY_WIDE
-#define MIRT_PRIMARY_WIDE 0
-#endif
-#ifndef MIRT_SHADOW_WIDE
-#define MIRT_SHADOW_WIDE 0
-#endif
+// (build-time switches: diag.hpp)
 #define MIRT_TRACE_KERNEL __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_WAVES_PER_EU)))
 // k_reflect keeps a whole bounce (ray, hit, normal) live through its shadow queries.  At 2
 // waves per SIMD (256 VGPRs, one 512-thread workgroup per CU) nothing spills (168 VGPRs),
 // but configs[4] ran 30% slower (1.28-1.31 vs 0.98-1.01 ms per frame, tools/ab_bench.sh):
 // the occupancy is worth more than the 17-77 spilled VGPRs (<= 160 B of scratch per lane,
 // mostly outside the traversal loops) it costs at 4.
-#ifndef MIRT_REFLECT_WAVES_PER_EU
-#define MIRT_REFLECT_WAVES_PER_EU 4
-#endif
 #define MIRT_REFLECT_KERNEL \
     __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_REFLECT_WAVES_PER_EU)))
-// bounce waves: k_bounce also traces each level's shadow rays and phong (1: slower, DESIGN.md
-// §4.8), or leaves them to k_shadow on the packed records (0)
-#ifndef MIRT_BOUNCE_SHADE
-#define MIRT_BOUNCE_SHADE 0
-#endif
 
 // ---------------------------------------------------------------- wide traversal
-#ifndef MIRT_LEAF_LANE_TEST
-#define MIRT_LEAF_LANE_TEST 1
-#endif
 // Wave reductions over 64 lanes (DPP row shifts + row broadcasts; every lane active,
 // lanes without data hold the identity).  Result read from lane 63: wave-uniform.
 template <bool MIN, int CTRL, int ROW_MASK, int BANK_MASK>
@@ -870,7 +864,7 @@ __device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t*
     uint32_t sp = 1;
     if (lane == 0) stk[0] = 0;  // root
     while (sp > 0) {
-        uint32_t k = ((int32_t)sp <= m.wide_thresh) ? min(sp, (uint32_t)kWideBatch) : 1u;
+        uint32_t k = ((int32_t)sp <= wide_thresh(m)) ? min(sp, (uint32_t)kWideBatch) : 1u;
         const uint32_t slot = lane >> 3, c = lane & 7;
         const bool on = slot < k;
         uint32_t node = 0;
@@ -1026,65 +1020,94 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   COMMON:   every lane's ray starts at o (primary rays): wide cone traversal.
 //   vt (one-object frames, LDS-resident, !REL): the camera's view table; (ls, lt) the lane's
 //   direction and crect the block's range of directions (view_sweep).
+//   The reference searches only objects whose box the ray meets (tracer.go:32) and only faces
+//   whose box it meets (object.go:76), by Box.Intersect (box.go:29-68) on the padded boxes of
+//   shared/state (rtreego's inner nodes are not replicated).  Pass 1 sweeps
+//   every candidate (the culling is exact) and applies the boxes to its outcome: an object
+//   box that fails removes the object; a winner whose face box passes, with no NaN distance
+//   around (whose first-hit rule could elect another face), is the nearest gated candidate
+//   itself.  Should some lane's winner fail its face box, the wave runs pass 2: every lane
+//   again, each candidate gated before it counts (test_range) — the same sweep code, so the
+//   rare path adds no register pressure to the common one.  MIRT_OPT_NO_BOX_GATE: no boxes
+//   (brute-force semantics).
 template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
-__device__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
+__device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
                                  bool lane_on, bool want_normal, Visits& vis, uint32_t* __restrict__ stk = nullptr,
                                  const ViewLeaf* vt = nullptr, uint32_t vn = 0, float ls = 0.0f, float lt = 0.0f,
                                  float4 crect = float4{0.0f, 0.0f, 0.0f, 0.0f}) {
     Nearest best;
-    best.ok = false;
-    best.obj = best.face = best.mat = 0;
-    best.hit = best.normal = V3{0, 0, 0};
-    double bestcd = 0;
-    V3 neg = scale(d, -1);  // triangle.go:38 rDir.Scale(-1)
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
-        const DevObject& ob = fa.obj[oi];
-        V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
-        Best b;
-        best_init(b);
-        const uint32_t ntri = ob.m.ntri;
-        if (BRUTE) {
-            if (resident)
-                test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
-            else  // every triangle straight from HBM (waves run independently: no LDS staging)
-                test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
-        } else if (COMMON) {
-            const Ray32 r = ray32(ro, d);
-            const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-            const bool force = !(far <= ob.m.cull_limit);
-            const Cone cone = make_cone(ro, r.ix, r.iy, r.iz, lane_on, force, 0.0f, __builtin_inff(), ob.m.cull_limit);
-            if (resident)
-                bvh_wide<REL, PREFILTER, false>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow);
-            else
-                bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
-                                                  vis.overflow);
-        } else if (resident && !REL && vt) {
-            view_sweep<PREFILTER, false>(ob.m, lds, vt, vn, ls, lt, false, crect.x, crect.y, crect.z, crect.w,
-                                         __builtin_inff(), ro, d, neg, lane_on, b, vis);
-        } else if (resident) {
-            bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
-                                             !(fa.flags & MIRT_OPT_NO_OCTANT));
-        } else {
-            bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
-                                               !(fa.flags & MIRT_OPT_NO_OCTANT));
-        }
-        uint32_t face, pos;
-        if (best_result(b, face, pos)) {
-            V3 world, normal{0, 0, 0};
-            uint32_t mat = 0;
-            winner(ob, pos, ro, d, neg, world, normal, mat, want_normal);
-            double cd = len(sub(world, cam));  // tracer.go:38
-            if (!best.ok || cd < bestcd) {
-                best.ok = true;
-                bestcd = cd;
-                best.obj = oi;
-                best.face = face;
-                best.mat = mat;
-                best.hit = world;
-                best.normal = normal;
+    const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
+    bool pass2 = false;  // wave-uniform
+#pragma unroll 1
+    for (;;) {
+        best.ok = false;
+        best.obj = best.face = best.mat = 0;
+        best.hit = best.normal = V3{0, 0, 0};
+        double bestcd = 0;
+        bool redo = false;
+        for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
+            const DevObject& ob = fa.obj[oi];
+            V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
+            V3 neg = scale(d, -1);  // triangle.go:38 rDir.Scale(-1)
+            Best b;
+            best_init(b);
+            const uint32_t ntri = ob.m.ntri;
+            const double* fgate = pass2 ? mesh_fbox(ob.m) : nullptr;
+            if (BRUTE) {
+                if (resident)
+                    test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests, nullptr, nullptr, true,
+                                               fgate);
+                else  // every triangle straight from HBM (waves run independently: no LDS staging)
+                    test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests, nullptr,
+                                                 nullptr, true, fgate);
+            } else if (COMMON && !pass2) {
+                const Ray32 r = ray32(ro, d);
+                const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+                const bool force = !(far <= ob.m.cull_limit);
+                const Cone cone = make_cone(ro, r.ix, r.iy, r.iz, lane_on, force, 0.0f, __builtin_inff(), ob.m.cull_limit);
+                if (resident)
+                    bvh_wide<REL, PREFILTER, false>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow);
+                else
+                    bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                                      vis.overflow);
+            } else if (resident && !REL && vt && !pass2) {
+                view_sweep<PREFILTER, false>(ob.m, lds, vt, vn, ls, lt, false, crect.x, crect.y, crect.z, crect.w,
+                                             __builtin_inff(), ro, d, neg, lane_on, b, vis);
+            } else if (resident) {
+                bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                                 !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr, fgate);
+            } else {
+                bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                                   !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr, fgate);
+            }
+            uint32_t face = 0, pos = 0;
+            bool got = lane_on && best_result(b, face, pos);
+            if (gating) {
+                got = box_gate(ob.box, o, d, got);  // tracer.go:32: the object's box
+                if (!pass2) {
+                    const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)pos * kBoxD, ro, d, got);  // object.go:76
+                    redo = redo || (got && (!fok || b.any_nan));
+                }
+            }
+            if (got) {
+                V3 world, normal{0, 0, 0};
+                uint32_t mat = 0;
+                winner(ob, pos, ro, d, neg, world, normal, mat, want_normal);
+                double cd = len(sub(world, cam));  // tracer.go:38
+                if (!best.ok || cd < bestcd) {
+                    best.ok = true;
+                    bestcd = cd;
+                    best.obj = oi;
+                    best.face = face;
+                    best.mat = mat;
+                    best.hit = world;
+                    best.normal = normal;
+                }
             }
         }
+        if (pass2 || __ballot(redo) == 0) break;
+        pass2 = true;
     }
     return best;
 }
@@ -1108,73 +1131,98 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
                                                   const ViewHead* vh = nullptr) {
     const DevObject& ob = fa.obj[0];
     const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
-    const V3 ro = sub(o, pos);  // object.go:71
-    const V3 neg = scale(d, -1);
     const double lh = len(sub(lpos, hit));
     const double mag = fmax(fmax(fmax(__builtin_fabs(o.x), __builtin_fabs(o.y)), __builtin_fabs(o.z)),
                             fmax(fmax(__builtin_fabs(pos.x), __builtin_fabs(pos.y)), __builtin_fabs(pos.z)));
     const double M = 0x1p-36 * (1.0 + lh + mag);
     const double resolve = lh - 1e-4 - M;
     const float tmax = (float)(lh + 1e-4 + M) * (1.0f + 0x1p-20f);
+    const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
     Best b;
-    best_init(b);
-    // Culling cone: the packet's rays walked backwards from the light, L + s * (-d), over
-    // s in [-(2e-4 + M), lh]: it covers o + t * d for t in [0, tmax] (o, L and d are
-    // collinear up to fp64 rounding, far inside the box inflation).
-    const Ray32 r = ray32(ro, d);
-    const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-    const bool force = !(far <= ob.m.cull_limit);
-    const float smin = -(float)(2e-4 + M) * (1.0f + 0x1p-20f);
-    const float smax = (float)lh * (1.0f + 0x1p-20f);
-    Cone cone;
-    if (MIRT_SHADOW_WIDE) cone = make_cone(sub(lpos, pos), -r.ix, -r.iy, -r.iz, lane_on, force, smin, smax, ob.m.cull_limit);
-    if (MIRT_SHADOW_WIDE) {
-        if (resident)
-            bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
-                                             tmax, resolve);
-        else
-            bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
-                                             vis.overflow, tmax, resolve);
-    } else if (resident && vt) {
-        // the lane's direction from the light: its hit point relative to the view point (every
-        // point of the segment short of the light lies in that direction)
-        const double* R0 = vh->R[0];
-        const double* R1 = vh->R[1];
-        const double* R2 = vh->R[2];
-        const V3 X = sub(sub(hit, pos), V3{vh->O[0], vh->O[1], vh->O[2]});
-        const double z = R0[0] * X.x + R0[1] * X.y + R0[2] * X.z;
-        const double mag = fmax(fmax(__builtin_fabs(X.x), __builtin_fabs(X.y)), __builtin_fabs(X.z));
-        const bool unb = !(z > 0x1p-20 * mag);
-        float ls = 0.0f, lt = 0.0f;
-        if (!unb) {
-            ls = (float)((R1[0] * X.x + R1[1] * X.y + R1[2] * X.z) / z);
-            lt = (float)((R2[0] * X.x + R2[1] * X.y + R2[2] * X.z) / z);
+    bool pass2 = false;  // wave-uniform: trace_nearest's two passes
+#pragma unroll 1
+    for (;;) {
+        best_init(b);
+        // (the sweep's inputs are made inside the loop: kept live across the box tests they
+        // would cost registers the sweep needs)
+        const V3 ro = sub(o, pos);  // object.go:71
+        const V3 neg = scale(d, -1);
+        // Culling cone: the packet's rays walked backwards from the light, L + s * (-d), over
+        // s in [-(2e-4 + M), lh]: it covers o + t * d for t in [0, tmax] (o, L and d are
+        // collinear up to fp64 rounding, far inside the box inflation).
+        const Ray32 r = ray32(ro, d);
+        const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+        const bool force = !(far <= ob.m.cull_limit);
+        const float smin = -(float)(2e-4 + M) * (1.0f + 0x1p-20f);
+        const float smax = (float)lh * (1.0f + 0x1p-20f);
+        Cone cone;
+        if (MIRT_SHADOW_WIDE) cone = make_cone(sub(lpos, pos), -r.ix, -r.iy, -r.iz, lane_on, force, smin, smax, ob.m.cull_limit);
+        if (MIRT_SHADOW_WIDE && !pass2) {
+            if (resident)
+                bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
+                                                 tmax, resolve);
+            else
+                bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                                 vis.overflow, tmax, resolve);
+        } else if (resident && vt && !pass2) {
+            // the lane's direction from the light: its hit point relative to the view point (every
+            // point of the segment short of the light lies in that direction)
+            const double* R0 = vh->R[0];
+            const double* R1 = vh->R[1];
+            const double* R2 = vh->R[2];
+            const V3 X = sub(sub(hit, pos), V3{vh->O[0], vh->O[1], vh->O[2]});
+            const double z = R0[0] * X.x + R0[1] * X.y + R0[2] * X.z;
+            const double mag = fmax(fmax(__builtin_fabs(X.x), __builtin_fabs(X.y)), __builtin_fabs(X.z));
+            const bool unb = !(z > 0x1p-20 * mag);
+            float ls = 0.0f, lt = 0.0f;
+            if (!unb) {
+                ls = (float)((R1[0] * X.x + R1[1] * X.y + R1[2] * X.z) / z);
+                lt = (float)((R2[0] * X.x + R2[1] * X.y + R2[2] * X.z) / z);
+            }
+            const bool any_unb = __ballot(lane_on && unb) != 0;
+            const float inf = __builtin_inff();
+            float cs0 = -inf, cs1 = inf, ct0 = -inf, ct1 = inf;
+            if (!any_unb) {
+                const bool on = lane_on;
+                cs0 = wave_reduce<true>(on ? ls : inf);
+                cs1 = wave_reduce<false>(on ? ls : -inf);
+                ct0 = wave_reduce<true>(on ? lt : inf);
+                ct1 = wave_reduce<false>(on ? lt : -inf);
+            }
+            // a candidate of the segment lies within |L - hit| of the light (or within near_r)
+            const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
+            view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b,
+                                        vis, resolve, tmax);
+        } else {
+            // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
+            const float* lt = fa.ltab && li < fa.n_lights ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
+            SegPre sp;
+            if (lt) sp = seg_pre(d, lh);
+            const double* fgate = pass2 ? mesh_fbox(ob.m) : nullptr;
+            if (resident)
+                bvh_sweep<false, PREFILTER, true, LT3>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                                      !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp, fgate);
+            else
+                bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                                      !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp, fgate);
         }
-        const bool any_unb = __ballot(lane_on && unb) != 0;
-        const float inf = __builtin_inff();
-        float cs0 = -inf, cs1 = inf, ct0 = -inf, ct1 = inf;
-        if (!any_unb) {
-            const bool on = lane_on;
-            cs0 = wave_reduce<true>(on ? ls : inf);
-            cs1 = wave_reduce<false>(on ? ls : -inf);
-            ct0 = wave_reduce<true>(on ? lt : inf);
-            ct1 = wave_reduce<false>(on ? lt : -inf);
-        }
-        // a candidate of the segment lies within |L - hit| of the light (or within near_r)
-        const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
-        view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b, vis,
-                                    resolve, tmax);
-    } else {
-        // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
-        const float* lt = fa.ltab && li < fa.n_lights ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
-        SegPre sp;
-        if (lt) sp = seg_pre(d, lh);
-        if (resident)
-            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                              !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
-        else
-            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                              !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
+        if (!gating) break;
+        // The reference's boxes (trace_nearest), applied to what the decision below rests on: a
+        // lane that retired rests on its candidate b.pos (a gated candidate nearer than
+        // `resolve` proves "not lit" whatever else the boxes remove); a lane whose candidates
+        // all lie beyond the light (no NaN distance) is lit under any gating; else it rests on
+        // the winner, which must pass with no NaN distance around.  An object box that fails
+        // leaves no candidate (lit).  A face box that fails: pass 2, every candidate gated.
+        uint32_t face = 0, p = 0;
+        const bool retired = b.has && b.d < resolve;
+        const bool far_lit = !retired && b.has && !b.any_nan && b.d > lh + 1e-4 + M;
+        const bool need = lane_on && best_result(b, face, p) && !far_lit;
+        const bool ok = box_gate(ob.box, o, d, need);  // tracer.go:32
+        if (need && !ok) best_init(b);
+        if (pass2) break;
+        const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)(retired ? b.pos : p) * kBoxD, ro, d, ok);  // object.go:76
+        if (__ballot(ok && (!fok || (!retired && b.any_nan))) == 0) break;
+        pass2 = true;
     }
     if (b.has && b.d < resolve) return false;
     // the nearest candidate (not a NaN-distance first hit, which wins regardless) lies beyond
@@ -1184,7 +1232,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     if (!best_result(b, face, p)) return true;
     V3 world, normal;
     uint32_t mat;
-    winner(ob, p, ro, d, neg, world, normal, mat, false);
+    winner(ob, p, sub(o, pos), d, scale(d, -1), world, normal, mat, false);
     return lh < len(sub(world, hit));
 }
 
@@ -1299,9 +1347,6 @@ struct WaveClock {
 // item of k_trace instead of one per wave — {kind, workgroup, start, end (100 MHz), start,
 // end (shader clock), wave tests, nodes | hits << 32} — appended through a counter held in
 // the buffer's first record (tools/item_trace.py).
-#ifndef MIRT_ITEM_TRACE
-#define MIRT_ITEM_TRACE 0
-#endif
 struct ItemClock {
     uint64_t real0 = 0, clk0 = 0;
     __device__ __forceinline__ void start() {
@@ -1665,7 +1710,8 @@ __device__ void build_view(const FrameRec& rec, uint32_t v, ViewLeaf* __restrict
         if (ok && v == 0) {
             ok = view_rows(fa.fwd, fa.left, fa.up, R);
         } else if (ok) {  // a light: look from it at the mesh's centre
-            double F[3] = {m.center[0] - O[0], m.center[1] - O[1], m.center[2] - O[2]};
+            const double* mc = mesh_center(m);
+            double F[3] = {mc[0] - O[0], mc[1] - O[1], mc[2] - O[2]};
             const double fl = sqrt(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]);
             if (fl > 0x1p-40 * (1.0 + far)) {
                 for (int k = 0; k < 3; ++k) F[k] /= fl;
@@ -1816,11 +1862,6 @@ __device__ __forceinline__ const ViewHead* view_lookup(const WorkArgs& wa, uint3
 
 
 
-// k_shadow (split kernels, reflection levels): three light-table records per leaf at once (1)
-// or two per step (0); see shadow_lit_single.
-#ifndef MIRT_SHADOW_LT3
-#define MIRT_SHADOW_LT3 0
-#endif
 
 // ---------------------------------------------------------------- shadow item
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
@@ -2837,6 +2878,11 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double r;
+    if (op == 4) {  // box.go:29-68 as the kernels evaluate it: ray i = a[6i..], box i = b[6i..]
+        const double* ray = a + 6 * (size_t)i;
+        out[i] = box_gate(b + 6 * (size_t)i, V3{ray[0], ray[1], ray[2]}, V3{ray[3], ray[4], ray[5]}, true) ? 1.0 : 0.0;
+        return;
+    }
     switch (op) {
         case 0: r = sqrt(a[i]); break;
         case 1: r = a[i] / b[i]; break;
@@ -3198,6 +3244,28 @@ __global__ __launch_bounds__(256) void k_stage_frames(const uint4* __restrict__ 
 hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s) {
     const uint32_t n16 = (uint32_t)(n * sizeof(FrameRec) / 16);
     hipLaunchKernelGGL(k_stage_frames, dim3(1), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst, n16);
+    return hipGetLastError();
+}
+
+// One light table, one thread per (light, triangle) record, on the stream of
+// the first frame that reads it (mirt.cpp lt_launch): lighttab.hpp's arithmetic, the host
+// builder's bits.
+__global__ __launch_bounds__(256) void k_light_table(const LightTabArgs a) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)a.n * a.nl) return;
+    const uint32_t l = (uint32_t)(i / a.n);
+    const size_t k = i - (size_t)l * a.n;
+    const LightGeom g = light_geom(a.lpos[l], a.pos, a.scale);
+    float r[kLtD];
+    light_record(a.tri + k * kTriD, g, r);
+    float4* o = (float4*)(a.out + i * kLtD);
+#pragma unroll
+    for (int q = 0; q < kLtD / 4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+}
+hipError_t launch_light_table(const LightTabArgs& a, hipStream_t s) {
+    const size_t n = (size_t)a.n * a.nl;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_light_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

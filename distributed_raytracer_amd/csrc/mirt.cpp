@@ -23,6 +23,7 @@
 #include "../../include/mirt.h"
 #include "gomath.hpp"
 #include "mirt_internal.hpp"
+#include "lighttab.hpp"
 #include "bvh.hpp"
 
 using namespace mirt;
@@ -58,7 +59,9 @@ struct MeshDev {
     uint32_t ntri = 0, nmat = 0, nnodes = 0, depth = 0;
     double scale = 1.0;  // max |coordinate| of the mesh (culling tolerances)
     Bvh8Node root{};     // host copy of the BVH root (frustum pre-test rectangles)
-    std::vector<double> htri;  // host copy of `tri` (light tables)
+    // Go math.Min / math.Max of every vertex coordinate (+inf / -inf without vertices): an
+    // object's box (object.go:31-59) is a function of its position and these (object_box)
+    double vmin[3] = {INFINITY, INFINITY, INFINITY}, vmax[3] = {-INFINITY, -INFINITY, -INFINITY};
     bool has_normals = false;
     bool live = false;
 };
@@ -183,17 +186,38 @@ struct mirt_ctx {
     cnt_t* prof_acc = nullptr;     // kStatN device totals accumulated while profiling
     uint64_t* timeline = nullptr;  // MIRT_OPT_TIMELINE buffer (2 kernels x timeline_cap waves)
     uint32_t timeline_cap = 0;
-    // light tables of one-object frames (light_table), kept for the context's life: frames in
-    // flight may read any of them
+    // Light tables of one-object frames (light_table): an LRU cache of device tables keyed by
+    // (mesh, object position, light set), built on the device on the stream of the first frame
+    // that reads them (lt_launch), evicted only once every stream that read them has passed
+    // an event recorded at eviction (lt_dead), their buffers reused for the next build.
     struct LightTab {
-        uint32_t mesh, nl;
-        double pos[3];
-        double lpos[MIRT_MAX_LIGHTS][3];
-        float* d;
+        uint32_t mesh = 0, nl = 0;
+        double pos[3] = {0, 0, 0};
+        double lpos[MIRT_MAX_LIGHTS][3] = {};
+        float* d = nullptr;
+        size_t bytes = 0;
+        bool built = false;             // k_light_table enqueued (on `built_on`)
+        hipStream_t built_on = nullptr;
+        hipEvent_t ready = nullptr;     // recorded after the build
+        bool ready_seen = false;        // `ready` has completed
+        uint64_t last_use = 0;          // lt_clock at the last light_table() returning it
+        // per stream whose frames read it: an event re-recorded after each such launch (the
+        // library owns the events, so a reader stream may be destroyed meanwhile)
+        std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    };
+    struct DeadTab {
+        float* d = nullptr;
+        size_t bytes = 0;
+        std::vector<hipEvent_t> evs;    // every reader stream's last launch that read it
     };
     std::mutex lt_mu;
-    std::vector<LightTab> ltabs;
-    size_t ltab_bytes = 0;
+    std::vector<std::unique_ptr<LightTab>> ltabs;
+    std::vector<DeadTab> lt_dead;
+    std::vector<hipEvent_t> lt_events;  // pool
+    size_t ltab_bytes = 0;              // live + dead tables
+    size_t lt_cap = (size_t)4 << 30;    // mirt_set_light_cache
+    uint64_t lt_clock = 0;
+    uint64_t lt_stat[6] = {0, 0, 0, 0, 0, 0};  // builds, hits, evictions, fallbacks, reused buffers, entries
 };
 
 namespace {
@@ -323,6 +347,49 @@ struct SlotGuard {
     }
 };
 
+// shared/state/util.go:7 boundEpsilon; rtreego.NewRect(p, len) keeps p and p + len, and
+// geom.NewBox (box.go:21-26) rebuilds MaxCorner as p + ((p + len) - p).
+constexpr double kBoundEpsilon = 0.0001;
+static void rect_corners(const double lo[3], const double hi[3], double out[6]) {
+    for (int k = 0; k < 3; ++k) {
+        const double len = go_max(hi[k] - lo[k], kBoundEpsilon);
+        const double q = lo[k] + len;
+        out[k] = lo[k];
+        out[3 + k] = lo[k] + (q - lo[k]);
+    }
+}
+// mesh.go:30-50 face.Bounds (math.Min(a, math.Min(b, c)) per axis), as NewBox corners
+static void face_box(const double* p1, const double* p2, const double* p3, double out[6]) {
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = go_min(p1[k], go_min(p2[k], p3[k]));
+        hi[k] = go_max(p1[k], go_max(p2[k], p3[k]));
+    }
+    rect_corners(lo, hi, out);
+}
+// object.go:31-59 Object.Bounds: min / max of pos and pos + v over the mesh's vertices.
+// Rounding is monotonic, so min_v fl(pos + v) = fl(pos + min_v v) (and the Go signed-zero
+// rule agrees: -0 + -0 is the only sum that is -0); the loop reduces to the mesh's vmin/vmax.
+static void object_box(const double pos[3], const double vmin[3], const double vmax[3], double out[6]) {
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = go_min(pos[k], pos[k] + vmin[k]);
+        hi[k] = go_max(pos[k], pos[k] + vmax[k]);
+    }
+    rect_corners(lo, hi, out);
+}
+static void vertex_minmax(const double* v, uint32_t nv, double vmin[3], double vmax[3]) {
+    for (int k = 0; k < 3; ++k) {
+        vmin[k] = INFINITY;
+        vmax[k] = -INFINITY;
+    }
+    for (uint32_t i = 0; i < nv; ++i)
+        for (int k = 0; k < 3; ++k) {
+            vmin[k] = go_min(vmin[k], v[3 * (size_t)i + k]);
+            vmax[k] = go_max(vmax[k], v[3 * (size_t)i + k]);
+        }
+}
+
 int check_frame(const mirt_ctx* c, const mirt_frame* f) {
     if (!f) return fail(MIRT_E_INVALID, "frame is NULL");
     if (f->n_objects > MIRT_MAX_OBJECTS)
@@ -337,6 +404,13 @@ int check_frame(const mirt_ctx* c, const mirt_frame* f) {
         uint32_t id = f->objects[i].mesh_id;
         if (id >= c->meshes.size() || !c->meshes[id].live)
             return fail(MIRT_E_INVALID, "object " + std::to_string(i) + " names unknown mesh id " + std::to_string(id));
+        // the kernels' Box.Intersect needs finite corners (an object box that overflows fp64
+        // would make the reference's zero-weighted dot-product terms inf * 0 = NaN)
+        double bx[6];
+        object_box(f->objects[i].pos, c->meshes[id].vmin, c->meshes[id].vmax, bx);
+        for (int k = 0; k < 6; ++k)
+            if (std::isinf(bx[k]))
+                return fail(MIRT_E_LIMIT, "object " + std::to_string(i) + "'s bounding box overflows fp64");
     }
     return MIRT_OK;
 }
@@ -372,16 +446,14 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         o.m.nodes = m.nodes;
         o.m.leaves = m.leaves;
         o.m.nleaves = m.nleaves;
-        for (int k = 0; k < 3; ++k) o.m.center[k] = m.center[k];
-        o.m.nnodes = m.nnodes;
         o.m.depth = m.depth;
         // culling needs bounded coordinates (fp32 slab arithmetic); beyond 2^40 never cull
         o.m.cull_limit = (m.scale <= 0x1p40) ? 256.0 * m.scale : -1.0;
-        o.m.wide_thresh = (int32_t)kBvhStack - 64 - 7 * (int32_t)m.depth;
         o.m.mats = m.mats;
         o.m.ntri = m.ntri;
         o.m.has_normals = m.has_normals ? 1u : 0u;
         for (int k = 0; k < 3; ++k) o.pos[k] = f->objects[i].pos[k];
+        object_box(o.pos, m.vmin, m.vmax, o.box);
         tris += m.ntri;
     }
     for (uint32_t l = 0; l < f->n_lights; ++l)
@@ -550,52 +622,13 @@ int check_tiles(uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n, uint
     return MIRT_OK;
 }
 
-// light_table's records (host only): nl lights x n triangles of T (kTriD doubles each).
+// light_table's records on the host (mirt_debug_light_table): nl lights x n triangles of T
+// (kTriD doubles each), lighttab.hpp's arithmetic (the device builder's, k_light_table).
 void light_records(const double* T, uint32_t n, double scale, const double pos[3], const double (*lpos)[3], uint32_t nl,
                    float* out) {
-    auto n1 = [](const double* v) { return std::fabs(v[0]) + std::fabs(v[1]) + std::fabs(v[2]); };
-    auto cross = [](const double* a, const double* b, double* r) {
-        r[0] = a[1] * b[2] - a[2] * b[1];
-        r[1] = a[2] * b[0] - a[0] * b[2];
-        r[2] = a[0] * b[1] - a[1] * b[0];
-    };
-    auto up = [](double x) { return std::nextafter((float)x, INFINITY); };
-    const double R = 2.0 * std::sqrt(3.0) * scale + 1.0;  // |hit| in object space, with slack
-    const double pinf = std::max(std::max(std::fabs(pos[0]), std::fabs(pos[1])), std::fabs(pos[2]));
     for (uint32_t l = 0; l < nl; ++l) {
-        double Lo[3];
-        for (int q = 0; q < 3; ++q) Lo[q] = lpos[l][q] - pos[q];
-        const double Lh = std::sqrt(Lo[0] * Lo[0] + Lo[1] * Lo[1] + Lo[2] * Lo[2]) + R;  // >= |L - hit|
-        const double Mmax = 0x1p-36 * (2.0 + Lh + pinf + R);  // >= the kernel's M (shadow_lit_single)
-        for (uint32_t k = 0; k < n; ++k) {
-            const double* t = T + (size_t)k * kTriD;
-            double V[3][3], W[3][3], A[3], e21[3];
-            for (int q = 0; q < 3; ++q) {
-                V[0][q] = t[q] - Lo[q];
-                V[1][q] = V[0][q] + t[3 + q];
-                V[2][q] = V[0][q] + t[6 + q];
-                e21[q] = t[6 + q] - t[3 + q];
-            }
-            cross(V[1], V[2], W[0]);
-            cross(V[2], V[0], W[1]);
-            cross(V[0], V[1], W[2]);
-            cross(t + 3, t + 6, A);
-            const double ntL = -(A[0] * V[0][0] + A[1] * V[0][1] + A[2] * V[0][2]);
-            const double G = std::max(std::max(n1(V[0]), n1(V[1])), n1(V[2]));
-            const double Ed = std::max(std::max(n1(t + 3), n1(t + 6)), n1(e21));
-            const double Wm = std::max(std::max(n1(W[0]), n1(W[1])), n1(W[2]));
-            const double cw = 1.25 * (0x1p-21 * Wm + 0x1p-36 * (G + Lh) * (G + Ed) + 4.0 * Mmax * Ed) + 0x1p-100;
-            const double cA = 1.25 * (0x1p-21 * n1(A) + 0x1p-44 * Ed * Ed) + 0x1p-100;
-            const double ctL = 1.25 * (0x1p-22 * std::fabs(ntL) + n1(A) * Mmax + 0x1p-36 * (G + Lh) * Ed * Ed) + 0x1p-100;
-            float* r = out + ((size_t)l * n + k) * kLtD;
-            for (int w = 0; w < 3; ++w)
-                for (int q = 0; q < 3; ++q) r[3 * w + q] = (float)W[w][q];
-            for (int q = 0; q < 3; ++q) r[9 + q] = (float)A[q];
-            r[12] = (float)ntL;
-            r[13] = up(cw);
-            r[14] = up(cA);
-            r[15] = up(ctL);
-        }
+        const LightGeom g = light_geom(lpos[l], pos, scale);
+        for (uint32_t k = 0; k < n; ++k) light_record(T + (size_t)k * kTriD, g, out + ((size_t)l * n + k) * kLtD);
     }
 }
 
@@ -608,42 +641,182 @@ void light_records(const double* T, uint32_t n, double scale, const double pos[3
 // at most 5 ulp of sum |d_i W_i|, bounded by 2^-21 = 8 ulp of |d|_inf |W|_1; the fp64 test's own rounding and the host's, 2^-36 (G + Lh)
 // (G + Ed); the shadow origin's distance from the line through L, |eps| <= M, and M's
 // bound over every hit on the mesh: 4 Mmax Ed), plus 2^-100 against underflow; cA the same
-// for a = d . A against -inc; ctL for nt's terms that do not scale with lam.  Rounded up.  Built on the host once per
-// (mesh, object position, lights) and kept for the context's life; past kLightTabBytes of
-// tables (scenes whose lights or object move every frame) new keys get NULL and trace
-// without the pre-classification.
-constexpr size_t kLightTabBytes = (size_t)2 << 30;
+// for a = d . A against -inc; ctL for nt's terms that do not scale with lam.  Rounded up
+// (lighttab.hpp, the arithmetic the device builder k_light_table runs).
+//
+// The cache (mirt_ctx::LightTab): a key (mesh, object position, lights) found is reused; a new
+// key reserves a buffer (a dead table's of the same size once its readers are done, else
+// hipMalloc) and is built by k_light_table on the stream of the first frame that reads it
+// (lt_launch) — no host work proportional to the mesh on the issue path.  Past the cap
+// (mirt_set_light_cache, default 4 GiB) the least recently used table whose last use is more
+// than kLtPinUses calls old is evicted: the events re-recorded after every launch that read it
+// (one per reader stream, lt_after) mark the point after which its buffer is free.  Only when
+// nothing is evictable (every table in use
+// by the frames being issued) does a frame trace without a table; the fallbacks are counted
+// (mirt_light_cache_stats), so a disabled prefilter is never silent.
+// tables returned by the last kLtPinUses calls may belong to frames not launched yet (a
+// group's open batch holds at most kMaxFrames; one-call paths launch at once)
+constexpr uint64_t kLtPinUses = 2 * kMaxFrames;
+hipEvent_t lt_event(mirt_ctx* c) {
+    if (!c->lt_events.empty()) {
+        hipEvent_t e = c->lt_events.back();
+        c->lt_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+}
+// Dead tables whose readers are all done: freed, or kept for a build of `want` bytes (returned).
+float* lt_reap(mirt_ctx* c, size_t want) {
+    float* got = nullptr;
+    for (size_t i = 0; i < c->lt_dead.size();) {
+        mirt_ctx::DeadTab& t = c->lt_dead[i];
+        bool done = true;
+        for (hipEvent_t e : t.evs) done = done && hipEventQuery(e) == hipSuccess;
+        if (!done) {
+            ++i;
+            continue;
+        }
+        for (hipEvent_t e : t.evs) c->lt_events.push_back(e);
+        if (!got && want && t.bytes == want) {
+            got = t.d;
+            ++c->lt_stat[4];
+        } else {
+            (void)hipFree(t.d);
+        }
+        c->ltab_bytes -= t.bytes;
+        c->lt_dead[i] = c->lt_dead.back();
+        c->lt_dead.pop_back();
+    }
+    return got;
+}
+// Retire table i: its buffer is free once every launch that read it (or built it) is done.
+void lt_evict(mirt_ctx* c, size_t i) {
+    mirt_ctx::LightTab& t = *c->ltabs[i];
+    mirt_ctx::DeadTab dt;
+    dt.d = t.d;
+    dt.bytes = t.bytes;
+    for (auto& u : t.uses) dt.evs.push_back(u.second);
+    if (t.ready) dt.evs.push_back(t.ready);
+    c->lt_dead.push_back(std::move(dt));
+    c->ltabs[i] = std::move(c->ltabs.back());
+    c->ltabs.pop_back();
+    ++c->lt_stat[2];
+}
+void lt_drop_mesh(mirt_ctx* c, uint32_t mesh) {  // the device is idle (mirt_mesh_release)
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (size_t i = 0; i < c->ltabs.size();) {
+        if (c->ltabs[i]->mesh != mesh) {
+            ++i;
+            continue;
+        }
+        lt_evict(c, i);
+    }
+    (void)lt_reap(c, 0);
+}
 const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) {
     if (fa.n_objects != 1 || fa.n_lights == 0 ||
         (fa.flags & (MIRT_OPT_NO_PREFILTER | MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_SEGMENT | MIRT_OPT_NO_LIGHT_TABLE)))
         return nullptr;
     const uint32_t mid = f->objects[0].mesh_id;
     std::lock_guard<std::mutex> g(c->lt_mu);
-    for (const auto& t : c->ltabs)
-        if (t.mesh == mid && t.nl == fa.n_lights && !memcmp(t.pos, fa.obj[0].pos, sizeof(t.pos)) &&
-            !memcmp(t.lpos, fa.lpos, sizeof(double) * 3 * fa.n_lights))
-            return t.d;
+    const uint64_t now = ++c->lt_clock;
+    for (auto& t : c->ltabs)
+        if (t->mesh == mid && t->nl == fa.n_lights && !memcmp(t->pos, fa.obj[0].pos, sizeof(t->pos)) &&
+            !memcmp(t->lpos, fa.lpos, sizeof(double) * 3 * fa.n_lights)) {
+            t->last_use = now;
+            ++c->lt_stat[1];
+            return t->d;
+        }
     const MeshDev& m = c->meshes[mid];
     const uint32_t n = m.ntri, nl = fa.n_lights;
-    if (n == 0 || m.htri.size() != (size_t)n * kTriD) return nullptr;
+    if (n == 0) return nullptr;
     const size_t bytes = (size_t)nl * n * kLtD * sizeof(float);
-    if (c->ltab_bytes + bytes > kLightTabBytes) return nullptr;
-    std::vector<float> h((size_t)nl * n * kLtD);
-    light_records(m.htri.data(), n, m.scale, fa.obj[0].pos, fa.lpos, nl, h.data());
-    const double* pos = fa.obj[0].pos;
-    mirt_ctx::LightTab lt{};
-    lt.mesh = mid;
-    lt.nl = nl;
-    memcpy(lt.pos, pos, sizeof(lt.pos));
-    memcpy(lt.lpos, fa.lpos, sizeof(double) * 3 * nl);
-    if (hipSetDevice(c->device) != hipSuccess || hipMalloc((void**)&lt.d, bytes) != hipSuccess) return nullptr;
-    if (hipMemcpy(lt.d, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(lt.d);
-        return nullptr;
+    float* buf = lt_reap(c, bytes);
+    // make room: least recently used first, never a table of the last kLtPinUses calls
+    while (!buf && c->ltab_bytes + bytes > c->lt_cap) {
+        size_t best = c->ltabs.size();
+        for (size_t i = 0; i < c->ltabs.size(); ++i)
+            if (now - c->ltabs[i]->last_use > kLtPinUses &&
+                (best == c->ltabs.size() || c->ltabs[i]->last_use < c->ltabs[best]->last_use))
+                best = i;
+        if (best == c->ltabs.size()) break;
+        lt_evict(c, best);
+        buf = lt_reap(c, bytes);
     }
-    c->ltabs.push_back(lt);
-    c->ltab_bytes += bytes;
-    return lt.d;
+    if (!buf) {
+        if (c->ltab_bytes + bytes > c->lt_cap || hipSetDevice(c->device) != hipSuccess ||
+            hipMalloc((void**)&buf, bytes) != hipSuccess) {
+            ++c->lt_stat[3];  // this frame traces without the pre-classification (counted)
+            return nullptr;
+        }
+        c->ltab_bytes += bytes;
+    }
+    auto lt = std::make_unique<mirt_ctx::LightTab>();
+    lt->mesh = mid;
+    lt->nl = nl;
+    memcpy(lt->pos, fa.obj[0].pos, sizeof(lt->pos));
+    memcpy(lt->lpos, fa.lpos, sizeof(double) * 3 * nl);
+    lt->d = buf;
+    lt->bytes = bytes;
+    lt->last_use = now;
+    c->ltabs.push_back(std::move(lt));
+    return buf;
+}
+// Before frames reading `tab` launch on stream s: build it there if nobody has (stream order
+// then covers this stream; other streams wait for its `ready` event until it has completed),
+// and remember s as a reader for eviction.
+int lt_launch(mirt_ctx* c, const float* tab, hipStream_t s) {
+    if (!tab) return MIRT_OK;
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (auto& tp : c->ltabs) {
+        mirt_ctx::LightTab& t = *tp;
+        if (t.d != tab) continue;
+        if (!t.built) {
+            const MeshDev& m = c->meshes[t.mesh];
+            LightTabArgs a{};
+            a.tri = m.tri;
+            a.n = m.ntri;
+            a.nl = t.nl;
+            a.scale = m.scale;
+            memcpy(a.pos, t.pos, sizeof(a.pos));
+            memcpy(a.lpos, t.lpos, sizeof(double) * 3 * t.nl);
+            a.out = t.d;
+            HIP_TRY(launch_light_table(a, s));
+            t.ready = lt_event(c);
+            if (!t.ready) return fail(MIRT_E_DEVICE, "hipEventCreate (light table)");
+            HIP_TRY(hipEventRecord(t.ready, s));
+            t.built = true;
+            t.built_on = s;
+            ++c->lt_stat[0];
+        } else if (!t.ready_seen && s != t.built_on) {
+            if (hipEventQuery(t.ready) == hipSuccess)
+                t.ready_seen = true;
+            else
+                HIP_TRY(hipStreamWaitEvent(s, t.ready, 0));
+        }
+        return MIRT_OK;
+    }
+    return fail(MIRT_E_INVALID, "light table not in the cache");  // cannot happen (pinned by kLtPinUses)
+}
+// After the frames reading `tab` were enqueued on s: the table's event for s marks their end.
+int lt_after(mirt_ctx* c, const float* tab, hipStream_t s) {
+    if (!tab) return MIRT_OK;
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (auto& tp : c->ltabs) {
+        if (tp->d != tab) continue;
+        hipEvent_t e = nullptr;
+        for (auto& u : tp->uses)
+            if (u.first == s) e = u.second;
+        if (!e) {
+            if (!(e = lt_event(c))) return fail(MIRT_E_DEVICE, "hipEventCreate (light table)");
+            tp->uses.emplace_back(s, e);
+        }
+        HIP_TRY(hipEventRecord(e, s));
+        return MIRT_OK;
+    }
+    return MIRT_OK;
 }
 
 // One frame's launch record: its arguments, output planes and frustum rectangles.
@@ -697,6 +870,10 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     if (nf > 1 && !one_launch) return fail(MIRT_E_INVALID, "several frames per launch need the single-kernel path");
     const FrameArgs& fa = sl->h_frames[0].fa;
     const OutPlanes out = sl->h_frames[0].out;
+    for (uint32_t k = 0; k < nf; ++k)  // the frames' light tables: built / waited for on s
+        if ((k == 0 || sl->h_frames[k].fa.ltab != sl->h_frames[k - 1].fa.ltab) &&
+            (r = lt_launch(c, sl->h_frames[k].fa.ltab, s)) != MIRT_OK)
+            return r;
     if ((r = blocks_prepare(sl, W, H, tiles, n, s)) != MIRT_OK) return r;
     HT(9);
     uint64_t pixels = 0;
@@ -936,6 +1113,10 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         std::lock_guard<std::mutex> g(c->mu);
         c->prof_pending.push_back(pr);
     }
+    for (uint32_t k = 0; k < nf; ++k)  // the light tables' reader events
+        if ((k == 0 || sl->h_frames[k].fa.ltab != sl->h_frames[k - 1].fa.ltab) &&
+            (r = lt_after(c, sl->h_frames[k].fa.ltab, s)) != MIRT_OK)
+            return r;
     if (!sl->dedicated) {
         HIP_TRY(hipEventRecord(sl->done, s));
         sl->pending = true;
@@ -991,8 +1172,18 @@ void mirt_destroy(mirt_ctx* c) {
             for (auto e : r.ev)
                 if (e) (void)hipEventDestroy(e);
         }
+    (void)hipDeviceSynchronize();
     for (auto& m : c->meshes) mesh_free(m);
-    for (auto& t : c->ltabs) (void)hipFree(t.d);
+    for (auto& t : c->ltabs) {
+        (void)hipFree(t->d);
+        if (t->ready) (void)hipEventDestroy(t->ready);
+        for (auto& u : t->uses) (void)hipEventDestroy(u.second);
+    }
+    for (auto& t : c->lt_dead) {
+        (void)hipFree(t.d);
+        for (hipEvent_t e : t.evs) (void)hipEventDestroy(e);
+    }
+    for (hipEvent_t e : c->lt_events) (void)hipEventDestroy(e);
     if (c->timeline) (void)hipFree(c->timeline);
     if (c->prof_acc) (void)hipFree(c->prof_acc);
     delete c;
@@ -1062,6 +1253,15 @@ double mirt_go_minmax(int op, double a, double b) {
     return op == 0 ? go_min(a, b) : op == 1 ? go_max(a, b) : op == 2 ? go_min1(a) : go_max0(a);
 }
 
+void mirt_face_bounds(const double p1[3], const double p2[3], const double p3[3], double out[6]) {
+    face_box(p1, p2, p3, out);
+}
+void mirt_object_bounds(const double* v, uint32_t nv, const double pos[3], double out[6]) {
+    double vmin[3], vmax[3];
+    vertex_minmax(v, nv, vmin, vmax);
+    object_box(pos, vmin, vmax, out);
+}
+
 int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn, uint32_t nn, const uint32_t* fv,
                      const uint32_t* fn, const uint32_t* fmat, uint32_t nf, const mirt_material* mats, uint32_t nm,
                      uint32_t* mesh_id) {
@@ -1094,6 +1294,8 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     // P1, E1 = P2 - P1, E2 = P3 - P1 (triangle.go:38: single fp64 subtractions, so the
     // precomputed edges are bit-identical to the per-test ones of the reference).
     std::vector<double> tri((size_t)nf * kTriD), vnrm(has_n ? (size_t)nf * kTriD : 0), mt((size_t)nm * 10);
+    // the device copy of `tri` continues with the face boxes and the centre (mesh_fbox)
+    std::vector<double> fbox((size_t)nf * kBoxD);
     std::vector<uint32_t> fm(nf);
     for (uint32_t pos = 0; pos < nf; ++pos) {
         const uint32_t f = bvh.order[pos];
@@ -1106,6 +1308,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
             t[3 + k] = p2[k] - p1[k];
             t[6 + k] = p3[k] - p1[k];
         }
+        face_box(p1, p2, p3, &fbox[(size_t)pos * kBoxD]);
         if (has_n)
             for (int q = 0; q < 3; ++q)
                 for (int k = 0; k < 3; ++k) vnrm[(size_t)pos * kTriD + 3 * q + k] = vn[3 * (size_t)fn[3 * f + q] + k];
@@ -1139,6 +1342,10 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     MeshDev md;
     md.nleaves = (uint32_t)leaves.size();
     for (int a = 0; a < 3; ++a) md.center[a] = md.nleaves ? 0.5 * (blo[a] + bhi[a]) : 0.0;
+    vertex_minmax(v, nv, md.vmin, md.vmax);
+    std::vector<double> dtri(tri);
+    dtri.insert(dtri.end(), fbox.begin(), fbox.end());
+    dtri.insert(dtri.end(), md.center, md.center + 3);
     md.ntri = nf;
     md.nmat = nm;
     md.has_normals = has_n;
@@ -1155,7 +1362,7 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         return MIRT_OK;
     };
     int r;
-    if ((r = upload((void**)&md.tri, tri.data(), tri.size() * 8)) != MIRT_OK ||
+    if ((r = upload((void**)&md.tri, dtri.data(), dtri.size() * 8)) != MIRT_OK ||
         (r = upload((void**)&md.vnrm, vnrm.data(), vnrm.size() * 8)) != MIRT_OK ||
         (r = upload((void**)&md.fmat, fm.data(), (size_t)nf * 4)) != MIRT_OK ||
         (r = upload((void**)&md.fidx, bvh.order.data(), (size_t)nf * 4)) != MIRT_OK ||
@@ -1165,7 +1372,6 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
         mesh_free(md);
         return r;
     }
-    md.htri = std::move(tri);
     md.live = true;
     std::lock_guard<std::mutex> g(c->mu);
     *mesh_id = (uint32_t)c->meshes.size();
@@ -1179,7 +1385,50 @@ int mirt_mesh_release(mirt_ctx* c, uint32_t id) {
     if (id >= c->meshes.size() || !c->meshes[id].live) return fail(MIRT_E_INVALID, "unknown mesh id");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
+    lt_drop_mesh(c, id);  // the mesh's light tables go with it (the device is idle)
     mesh_free(c->meshes[id]);
+    return MIRT_OK;
+}
+
+int mirt_set_light_cache(mirt_ctx* c, uint64_t max_bytes) {
+    if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    c->lt_cap = (size_t)max_bytes;
+    return MIRT_OK;
+}
+
+int mirt_light_cache_stats(mirt_ctx* c, uint64_t out[8]) {
+    if (!c || !out) return fail(MIRT_E_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (int k = 0; k < 5; ++k) out[k] = c->lt_stat[k];
+    out[5] = c->ltabs.size();
+    out[6] = c->ltab_bytes;
+    out[7] = c->lt_cap;
+    return MIRT_OK;
+}
+
+int mirt_debug_light_table_gpu(mirt_ctx* c, const double* tri, uint32_t n, double scale, const double pos[3],
+                               const double* lights, uint32_t nl, float* out) {
+    if (!c || (n && !tri) || !pos || (nl && !lights) || (n && nl && !out)) return fail(MIRT_E_INVALID, "NULL argument");
+    if (nl > MIRT_MAX_LIGHTS) return fail(MIRT_E_LIMIT, "nl > MIRT_MAX_LIGHTS");
+    if ((size_t)n * nl == 0) return MIRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t tb = (size_t)n * kTriD * sizeof(double), ob = (size_t)n * nl * kLtD * sizeof(float);
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, tb + ob));
+    LightTabArgs a{};
+    a.tri = (const double*)d;
+    a.n = n;
+    a.nl = nl;
+    a.scale = scale;
+    memcpy(a.pos, pos, sizeof(a.pos));
+    memcpy(a.lpos, lights, sizeof(double) * 3 * nl);
+    a.out = (float*)((char*)d + tb);
+    hipError_t e = hipMemcpy(d, tri, tb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_light_table(a, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, a.out, ob, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "mirt_debug_light_table_gpu");
     return MIRT_OK;
 }
 
@@ -1452,15 +1701,17 @@ int mirt_debug_counters(mirt_ctx* c, uint64_t* out, uint32_t n) {
 }
 
 int mirt_debug_fp64(mirt_ctx* c, int op, uint32_t n, const double* a, const double* b, double* out) {
-    if (!c || !a || !b || !out || op < 0 || op > 3) return fail(MIRT_E_INVALID, "bad argument");
+    if (!c || !a || !b || !out || op < 0 || op > 4) return fail(MIRT_E_INVALID, "bad argument");
     if (n == 0) return MIRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    const size_t w = op == 4 ? 6 : 1;  // op 4: six doubles per ray and per box
     double* d = nullptr;
-    HIP_TRY(hipMalloc((void**)&d, (size_t)n * 24));
-    hipError_t e = hipMemcpy(d, a, (size_t)n * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d + n, b, (size_t)n * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_debug_fp64(op, n, d, d + n, d + 2 * (size_t)n, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * (size_t)n, (size_t)n * 8, hipMemcpyDeviceToHost);
+    HIP_TRY(hipMalloc((void**)&d, (size_t)n * 8 * (2 * w + 1)));
+    hipError_t e = hipMemcpy(d, a, (size_t)n * 8 * w, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + w * n, b, (size_t)n * 8 * w, hipMemcpyHostToDevice);
+    double* o = d + 2 * w * (size_t)n;
+    if (e == hipSuccess) e = launch_debug_fp64(op, n, d, d + w * n, o, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, o, (size_t)n * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "mirt_debug_fp64");
     return MIRT_OK;

@@ -85,8 +85,10 @@ struct LeafBox {
     uint32_t ref, pad;
 };
 
+// `tri` is one allocation: [ntri * 9 tri][ntri * 6 face boxes][3 centre] (mesh_fbox,
+// mesh_center), so the face boxes cost no kernel-argument bytes.
 struct DevMesh {
-    const double* tri;       // ntri * 9 : P1, E1, E2
+    const double* tri;       // ntri * 9 : P1, E1, E2; then the face boxes and the centre
     const double* vnrm;      // ntri * 9 : N1, N2, N3 (normalised) if has_normals
     const uint32_t* fmat;    // ntri     : material index
     const uint32_t* fidx;    // ntri     : original face index
@@ -95,14 +97,20 @@ struct DevMesh {
     const LeafBox* leaves;   // nleaves BVH leaves (view tables)
     uint32_t ntri;
     uint32_t has_normals;
-    uint32_t nnodes;
     uint32_t depth;
-    int32_t wide_thresh;     // wide traversal batches nodes only while sp <= this (< 0: never)
     uint32_t nleaves;
     double cull_limit;       // rays whose object-space origin has a coordinate beyond this
                              // are never culled (tolerance scales with |origin|)
-    double center[3];        // centre of the mesh's bounding box (light views look at it)
 };
+// Per BVH position: face.Bounds (mesh.go:30-50) as NewBox corners {MinCorner, MaxCorner}.
+constexpr int kBoxD = 6;
+__host__ __device__ inline const double* mesh_fbox(const DevMesh& m) { return m.tri + (size_t)m.ntri * kTriD; }
+// centre of the mesh's bounding box (light views look at it)
+__host__ __device__ inline const double* mesh_center(const DevMesh& m) {
+    return m.tri + (size_t)m.ntri * (kTriD + kBoxD);
+}
+// wide traversal batches nodes only while the stack holds <= this many entries (< 0: never)
+__host__ __device__ inline int32_t wide_thresh(const DevMesh& m) { return (int32_t)kBvhStack - 64 - 7 * (int32_t)m.depth; }
 
 // View tables (one-object frames with an LDS-resident mesh).  A view is a point every ray
 // of a packet passes through: the camera for primary rays, a light for shadow rays (a
@@ -143,6 +151,7 @@ enum TraceMode { kModeBvh = 0, kModeBrute = 1 };
 struct DevObject {
     DevMesh m;
     double pos[3];
+    double box[kBoxD];  // Object.Bounds (object.go:31-59) as NewBox corners, world space
 };
 
 // Everything per frame travels by value in the kernel-argument block (s_load'ed).
@@ -380,6 +389,16 @@ struct RayIO {
     uint32_t n;
 };
 
+// Device builder of one light table (kernels.hip k_light_table; lighttab.hpp records).
+struct LightTabArgs {
+    const double* tri;  // the mesh's P1, E1, E2 records in BVH order
+    uint32_t n, nl;     // triangles, lights
+    double scale;       // the mesh's largest |coordinate|
+    double pos[3];      // the object's position
+    double lpos[MIRT_MAX_LIGHTS][3];
+    float* out;         // nl * n * kLtD floats, light-major
+};
+hipError_t launch_light_table(const LightTabArgs& a, hipStream_t s);
 hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s);
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);

@@ -135,6 +135,27 @@ class Context:
         L.check(L.lib().mirt_debug_fp64(self.handle, op, len(a), a.ctypes.data, b.ctypes.data, out.ctypes.data))
         return out
 
+    def light_cache_stats(self) -> dict:
+        """mirt_light_cache_stats: the light-table cache's counters (mirt.h)."""
+        out = np.zeros(8, np.uint64)
+        L.check(L.lib().mirt_light_cache_stats(self.handle, out.ctypes.data))
+        return dict(zip(("builds", "hits", "evictions", "no_room", "reused_buffers", "tables", "bytes", "cap"),
+                        (int(x) for x in out)))
+
+    def set_light_cache(self, max_bytes: int) -> None:
+        L.check(L.lib().mirt_set_light_cache(self.handle, int(max_bytes)))
+
+    def debug_box_intersect(self, origins, dirs, boxes) -> np.ndarray:
+        """box.go:29-68 Box.Intersect as the kernels evaluate it (mirt_debug_fp64 op 4):
+        ray i (origins[i], dirs[i]) against box i ({MinCorner, MaxCorner}, 6 doubles)."""
+        rays = np.ascontiguousarray(np.concatenate([np.reshape(origins, (-1, 3)), np.reshape(dirs, (-1, 3))], 1),
+                                    np.float64)
+        bx = np.ascontiguousarray(np.reshape(boxes, (-1, 6)), np.float64)
+        assert len(rays) == len(bx)
+        out = np.zeros(len(rays), np.float64)
+        L.check(L.lib().mirt_debug_fp64(self.handle, 4, len(rays), rays.ctypes.data, bx.ctypes.data, out.ctypes.data))
+        return out != 0.0
+
     def debug_timeline(self, max_records: int = 1 << 16) -> np.ndarray:
         """Per-wave stamps of the last frame traced with MIRT_OPT_TIMELINE (mirt.h)."""
         out = np.zeros((max_records, 8), np.uint64)

@@ -143,12 +143,21 @@ func main() {
 		}
 	}
 
+	// One GPU context for the process's life (mirt_create sets up the device workspaces and
+	// streams once); while the device cannot be opened the worker keeps retrying, as the
+	// reference keeps retrying its registration (worker/distributed/main.go:131-185).
+	var w *gpu.Worker
 	for {
-		// one GPU context per registration: a re-registered worker may get another scene
-		w, err := gpu.New(device)
-		if err != nil {
-			log.Fatalf("GPU %d: %v.\n", device, err)
+		if w, err = gpu.New(device); err == nil {
+			break
 		}
+		log.Printf("GPU %d: %v.\n", device, err)
+		time.Sleep(time.Millisecond * time.Duration(registerFrequency))
+	}
+	defer w.Close()
+
+	for {
+		// a failed registration costs one RPC; only a successful one uploads meshes
 		tracer, err := register(masterAddr, uint32(orderPort), w)
 		if err == nil {
 			server := grpc.NewServer()
@@ -177,7 +186,8 @@ func main() {
 		} else {
 			log.Printf("Failed to register: %v.\n", err)
 		}
-		w.Close()
+		// the next registration may bring another scene: drop this one's meshes
+		w.ReleaseMeshes()
 		time.Sleep(time.Millisecond * time.Duration(registerFrequency))
 	}
 }

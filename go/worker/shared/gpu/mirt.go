@@ -57,6 +57,15 @@ func (w *Worker) Close() {
 	}
 }
 
+// ReleaseMeshes frees every uploaded mesh: a worker that registers again may receive another
+// scene.  The context (device workspaces, streams) stays open for the process's life.
+func (w *Worker) ReleaseMeshes() {
+	for path, id := range w.meshes {
+		C.mirt_mesh_release(w.ctx, id)
+		delete(w.meshes, path)
+	}
+}
+
 // UploadScene uploads every mesh of the scene the master sent at registration
 // (worker/distributed/main.go:115-126; shared/state/mesh.go:100-106).  Meshes are
 // immutable for the worker's life: frames only carry EnvMutables diffs.

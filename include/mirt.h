@@ -245,6 +245,8 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_VIEWS 256u         /* per-frame view tables instead of the BVH walk (same results; slower) */
 #define MIRT_OPT_REFLECT_CHAINS 512u /* reflections as per-pixel chains in one kernel (k_reflect) instead of level by level (same results) */
 #define MIRT_OPT_NO_LIGHT_TABLE 1024u /* shadow segments without the fp32 light-table pre-classification (same results) */
+#define MIRT_OPT_NO_BOX_GATE 2048u  /* ablation: skip the reference's Box.Intersect of the face and object boxes
+                                       (box.go:29-68), i.e. brute-force semantics; DESIGN.md §4.2 */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 /*
  * Launch shape of the frame kernel: every workgroup owns at least min_blocks_per_wg 8x8
@@ -267,6 +269,9 @@ int mirt_stream_destroy(mirt_ctx *ctx, void *stream);
  * Diagnostic: evaluate one fp64 primitive of the kernels on the device for n inputs
  * (host buffers) so tests can pin device arithmetic against the host bit-for-bit.
  *   op 0: sqrt(a)   op 1: a / b   op 2: Go math.Pow(a, b)   op 3: Go math.Max(a, b)
+ *   op 4: box.go:29-68 Box.Intersect as the kernels evaluate it: a holds n rays (origin,
+ *         direction: 6 doubles each), b n boxes ({MinCorner, MaxCorner}: 6 doubles each),
+ *         out[i] = 1.0 if ray i meets box i, else 0.0
  */
 int mirt_debug_fp64(mirt_ctx *ctx, int op, uint32_t n, const double *a, const double *b, double *out);
 
@@ -303,6 +308,34 @@ int mirt_debug_counters(mirt_ctx *ctx, uint64_t *out, uint32_t n);
  */
 int mirt_debug_light_table(const double *tri, uint32_t n, double scale, const double pos[3], const double *lights,
                            uint32_t nl, float *out);
+/* The same records built on the device (k_light_table, the builder the cache uses). */
+int mirt_debug_light_table_gpu(mirt_ctx *ctx, const double *tri, uint32_t n, double scale, const double pos[3],
+                               const double *lights, uint32_t nl, float *out);
+
+/*
+ * The light-table cache of one-object frames: tables keyed by (mesh, object
+ * position, light set), built on the device on the stream of the first frame that reads them,
+ * least recently used evicted past max_bytes (default 4 GiB) once the streams that read them
+ * have moved on.  A frame finding no room traces without a table (same results, slower) and is
+ * counted.  stats: out[0] builds, [1] hits, [2] evictions, [3] frames without a table (no room),
+ * [4] builds that reused an evicted buffer, [5] live tables, [6] bytes held (live + being
+ * retired), [7] the cap.
+ */
+int mirt_set_light_cache(mirt_ctx *ctx, uint64_t max_bytes);
+int mirt_light_cache_stats(mirt_ctx *ctx, uint64_t out[8]);
+
+/*
+ * Diagnostic (host only, no device): the padded boxes the reference culls with, as NewBox
+ * (box.go:21-26) turns the rtreego rect into corners, written as {MinCorner, MaxCorner}:
+ *   mirt_face_bounds    face.Bounds (shared/state/mesh.go:30-50) of the triangle p1 p2 p3;
+ *   mirt_object_bounds  Object.Bounds (shared/state/object.go:31-59) of an object at pos
+ *                       whose mesh has the nv vertices v (nv*3 doubles).
+ * MaxCorner = p + ((p + len) - p) with len = max(extent, boundEpsilon): the rtreego rect stores
+ * p + len and NewBox subtracts p again.  The kernels gate every candidate face and object
+ * with Box.Intersect on exactly these corners.
+ */
+void mirt_face_bounds(const double p1[3], const double p2[3], const double p3[3], double out[6]);
+void mirt_object_bounds(const double *v, uint32_t nv, const double pos[3], double out[6]);
 
 /*
  * Multi-GPU frames (one process per GPU of a box; SURVEY.md §8(b) mirt_trace_frame).  The

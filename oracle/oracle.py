@@ -72,6 +72,10 @@ def lib():
                                      C.POINTER(OrStats)]
         L.or_trace_rays.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_rtree_audit.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 4
+        L.or_face_box.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+        L.or_object_box.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.or_box_intersect.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_triangle_intersection.argtypes = [C.c_void_p] * 7
         L.or_go_tan.restype = C.c_double
         L.or_go_tan.argtypes = [C.c_double]
@@ -86,10 +90,24 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data if a is not None and a.size else 0
 
 
-class Oracle:
-    """Holds the C oracle context for one scene (brute force or R-tree culling)."""
+CULL_MODES = {"brute": 0, "rtree": 1, "boxes": 2}
 
-    def __init__(self, scene: PyScene, use_rtree: bool = False):
+
+class Oracle:
+    """Holds the C oracle context for one scene.
+
+    culling (rt_oracle.c OR_CULL_*):
+      "brute"  every face and object, no box test;
+      "rtree"  the reference's rtreego search (object.go:76, tracer.go:32), DFS order;
+      "boxes"  every face / object gated by Box.Intersect on its own padded box only —
+               the reference's leaf-level test without rtreego's inner nodes; the set the
+               GPU computes.
+    use_rtree=True is the old spelling of culling="rtree"."""
+
+    def __init__(self, scene: PyScene, use_rtree: bool = False, culling: str | None = None):
+        if culling is None:
+            culling = "rtree" if use_rtree else "brute"
+        self.culling = culling
         self._keep = []
         L = lib()
         meshes = (OrMesh * max(1, len(scene.meshes)))()
@@ -109,7 +127,7 @@ class Oracle:
         self._sc = OrScene(meshes, len(scene.meshes), objs, len(scene.objects), lights, len(scene.lights),
                            (C.c_double * 3)(*scene.cam_pos), (C.c_double * 3)(*scene.cam_dir), scene.fov)
         self._keep.extend([meshes, objs, lights])
-        self._ctx = L.or_build(C.byref(self._sc), 1 if use_rtree else 0)
+        self._ctx = L.or_build(C.byref(self._sc), CULL_MODES[culling])
         if not L.or_camera_ok(self._ctx):
             raise ValueError("camera dir is parallel to the global up vector (camera.go:37)")
 
@@ -161,6 +179,44 @@ class Oracle:
         obj = np.zeros(n, np.int32)
         lib().or_trace_rays(self._ctx, n, _ptr(o), _ptr(d), _ptr(ok), _ptr(hit), _ptr(nrm), _ptr(face), _ptr(obj))
         return dict(ok=ok, hit=hit, normal=nrm, face=face, obj=obj)
+
+
+    def rtree_audit(self, origins: np.ndarray, dirs: np.ndarray):
+        """Per ray (culling="rtree" only): (veto, ties) — candidates rtreego's inner nodes
+        prune although their own box passes, and objects with two accepted faces at the same
+        minimum distance (rt_oracle.c or_rtree_audit)."""
+        o = np.ascontiguousarray(origins, np.float64).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, np.float64).reshape(-1, 3)
+        veto = np.zeros(len(o), np.uint32)
+        ties = np.zeros(len(o), np.uint32)
+        if lib().or_rtree_audit(self._ctx, len(o), _ptr(o), _ptr(d), _ptr(veto), _ptr(ties)) != 0:
+            raise ValueError("rtree_audit needs culling='rtree'")
+        return veto, ties
+
+
+    def face_box(self, mesh: int, face: int) -> np.ndarray:
+        """{MinCorner, MaxCorner} of face.Bounds as NewBox makes them (mesh.go:30-50)."""
+        out = np.zeros(6, np.float64)
+        if lib().or_face_box(self._ctx, mesh, face, _ptr(out)) != 0:
+            raise IndexError("no such face")
+        return out
+
+    def object_box(self, obj: int) -> np.ndarray:
+        """{MinCorner, MaxCorner} of Object.Bounds as NewBox makes them (object.go:31-59)."""
+        out = np.zeros(6, np.float64)
+        if lib().or_object_box(self._ctx, obj, _ptr(out)) != 0:
+            raise IndexError("no such object")
+        return out
+
+
+def box_intersect(box, origins, dirs) -> np.ndarray:
+    """box.go:29-68 Box.Intersect of each ray with a box given as NewBox corners."""
+    b = np.ascontiguousarray(box, np.float64)
+    o = np.ascontiguousarray(origins, np.float64).reshape(-1, 3)
+    d = np.ascontiguousarray(dirs, np.float64).reshape(-1, 3)
+    out = np.zeros(len(o), np.uint8)
+    lib().or_box_intersect(_ptr(b), len(o), _ptr(o), _ptr(d), _ptr(out))
+    return out.astype(bool)
 
 
 def triangle_intersection(p1, p2, p3, o, d):

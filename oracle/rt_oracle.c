@@ -366,10 +366,7 @@ static void rtree_init(rtree *t) { t->root = node_new(NULL, 1, 1); t->size = 0; 
 
 /* box.go:21-26 NewBox + box.go:29-68 Box.Intersect */
 static const vec3 BOX_NORMALS[6] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
-static int box_intersect(const rect *bb, vec3 o, vec3 d) {
-    vec3 mn = v_make(bb->p[0], bb->p[1], bb->p[2]);
-    vec3 mx = v_make(bb->p[0] + (bb->q[0] - bb->p[0]), bb->p[1] + (bb->q[1] - bb->p[1]),
-                     bb->p[2] + (bb->q[2] - bb->p[2]));
+static int corners_intersect(vec3 mn, vec3 mx, vec3 o, vec3 d) {
     for (int k = 0; k < 6; k++) {
         vec3 sn = BOX_NORMALS[k];
         if (v_dot(d, sn) != 0.0) {
@@ -389,6 +386,12 @@ static int box_intersect(const rect *bb, vec3 o, vec3 d) {
     }
     return 0;
 }
+static int box_intersect(const rect *bb, vec3 o, vec3 d) {
+    vec3 mn = v_make(bb->p[0], bb->p[1], bb->p[2]);
+    vec3 mx = v_make(bb->p[0] + (bb->q[0] - bb->p[0]), bb->p[1] + (bb->q[1] - bb->p[1]),
+                     bb->p[2] + (bb->q[2] - bb->p[2]));
+    return corners_intersect(mn, mx, o, d);
+}
 
 /* ------------------------------------------------------------------ context */
 #define BOUND_EPSILON 0.0001 /* shared/state/util.go:7 */
@@ -396,12 +399,24 @@ static int box_intersect(const rect *bb, vec3 o, vec3 d) {
 typedef struct {
     const or_mesh *m;
     rtree faces;
+    rect *fbox;           /* OR_CULL_BOXES: face.Bounds per face (mesh.go:30-50) */
 } mesh_rt;
+/* Culling modes (or_build):
+ *   OR_CULL_BRUTE  every face and object, ascending index (no box test at all);
+ *   OR_CULL_RTREE  the reference: rtreego SearchCondition over the face and object trees,
+ *                  Box.Intersect on every inner-node and leaf-entry box (DFS order);
+ *   OR_CULL_BOXES  every face and object in ascending index, each gated by Box.Intersect on
+ *                  its OWN padded box only (face.Bounds / Object.Bounds) — the reference's
+ *                  leaf-level test without rtreego's inner nodes, whose shape depends on the
+ *                  unvendored tree's insertion order and split.  The GPU
+ *                  computes exactly this set. */
+enum { OR_CULL_BRUTE = 0, OR_CULL_RTREE = 1, OR_CULL_BOXES = 2 };
 typedef struct {
     or_scene s;
     mesh_rt *meshes;
     rtree objs;           /* top-level object tree (EnvMutables.Objs) */
-    int use_rtree;
+    rect *obox;           /* OR_CULL_BOXES: Object.Bounds per object (object.go:31-59) */
+    int use_rtree;        /* the culling mode (OR_CULL_*) */
     vec3 cam_pos, cam_fwd, cam_left, cam_up;
     double fov;
     int cam_ok;
@@ -465,15 +480,23 @@ or_ctx *or_build(const or_scene *s, int use_rtree) {
     c->meshes = (mesh_rt *)calloc(s->n_meshes ? s->n_meshes : 1, sizeof(mesh_rt));
     for (uint32_t i = 0; i < s->n_meshes; i++) {
         c->meshes[i].m = &s->meshes[i];
-        if (use_rtree) {
+        if (use_rtree == OR_CULL_RTREE) {
             rtree_init(&c->meshes[i].faces);
             for (uint32_t f = 0; f < s->meshes[i].n_faces; f++)
                 rtree_insert(&c->meshes[i].faces, face_bounds(&s->meshes[i], f), (int32_t)f);
         }
+        if (use_rtree != OR_CULL_BRUTE) {  /* BOXES, and the RTREE mode's veto audit */
+            c->meshes[i].fbox = (rect *)malloc(sizeof(rect) * (s->meshes[i].n_faces + 1));
+            for (uint32_t f = 0; f < s->meshes[i].n_faces; f++) c->meshes[i].fbox[f] = face_bounds(&s->meshes[i], f);
+        }
     }
-    if (use_rtree) {
+    if (use_rtree == OR_CULL_RTREE) {
         rtree_init(&c->objs);
         for (uint32_t o = 0; o < s->n_objects; o++) rtree_insert(&c->objs, object_bounds(c, o), (int32_t)o);
+    }
+    if (use_rtree != OR_CULL_BRUTE) {
+        c->obox = (rect *)malloc(sizeof(rect) * (s->n_objects + 1));
+        for (uint32_t o = 0; o < s->n_objects; o++) c->obox[o] = object_bounds(c, o);
     }
     c->cam_pos = v_make(s->cam_pos[0], s->cam_pos[1], s->cam_pos[2]);
     double f[3], l[3], u[3];
@@ -487,10 +510,12 @@ or_ctx *or_build(const or_scene *s, int use_rtree) {
 int or_camera_ok(const or_ctx *c) { return c->cam_ok; }
 void or_free(or_ctx *c) {
     if (!c) return;
-    if (c->use_rtree) {
+    if (c->use_rtree == OR_CULL_RTREE) {
         for (uint32_t i = 0; i < c->s.n_meshes; i++) node_free(c->meshes[i].faces.root);
         node_free(c->objs.root);
     }
+    for (uint32_t i = 0; i < c->s.n_meshes; i++) free(c->meshes[i].fbox);
+    free(c->obox);
     free(c->meshes);
     free(c);
 }
@@ -564,7 +589,8 @@ static void object_intersection(const or_ctx *c, uint32_t oi, vec3 ro, vec3 rd, 
         const or_mesh *m = c->meshes[ob->mesh].m;
         uint32_t ncand;
         const uint32_t *cand = NULL;
-        if (c->use_rtree) {
+        const rect *fbox = c->use_rtree == OR_CULL_BOXES ? c->meshes[ob->mesh].fbox : NULL;
+        if (c->use_rtree == OR_CULL_RTREE) {
             searchq q = {ro, rd, sc->stack_face, 0, &sc->box_tests};
             rt_search(c->meshes[ob->mesh].faces.root, &q);
             ncand = q.n; cand = sc->stack_face;
@@ -574,6 +600,10 @@ static void object_intersection(const or_ctx *c, uint32_t oi, vec3 ro, vec3 rd, 
         int has_normals = m->n_normals > 0;
         for (uint32_t k = 0; k < ncand; k++) {
             uint32_t f = cand ? cand[k] : k;
+            if (fbox) {  /* OR_CULL_BOXES: the face's own box (object.go:76, box.go:29-68) */
+                sc->box_tests++;
+                if (!box_intersect(&fbox[f], ro, rd)) continue;
+            }
             vec3 p1 = mesh_vertex(m, m->face_v[3 * f]), p2 = mesh_vertex(m, m->face_v[3 * f + 1]),
                  p3 = mesh_vertex(m, m->face_v[3 * f + 2]);
             vec3 ip; double bc[3];
@@ -610,7 +640,7 @@ static hitrec trace(const or_ctx *c, vec3 ro, vec3 rd, scratch *sc) {
     double bestd = 0;
     uint32_t cands[64];
     uint32_t *cl = NULL; uint32_t nc;
-    if (c->use_rtree) {
+    if (c->use_rtree == OR_CULL_RTREE) {
         cl = c->s.n_objects <= 64 ? cands : (uint32_t *)malloc(sizeof(uint32_t) * c->s.n_objects);
         searchq q = {ro, rd, cl, 0, &sc->box_tests};
         rt_search(c->objs.root, &q);
@@ -620,6 +650,10 @@ static hitrec trace(const or_ctx *c, vec3 ro, vec3 rd, scratch *sc) {
     }
     for (uint32_t k = 0; k < nc; k++) {
         uint32_t oi = cl ? cl[k] : k;
+        if (c->use_rtree == OR_CULL_BOXES) {  /* the object's own box (tracer.go:32) */
+            sc->box_tests++;
+            if (!box_intersect(&c->obox[oi], ro, rd)) continue;
+        }
         hitrec h;
         object_intersection(c, oi, ro, rd, &h, sc);
         if (h.ok) {
@@ -833,5 +867,99 @@ int or_trace_rays(const or_ctx *c, uint32_t n, const double *orig, const double 
         obj[r] = h.ok ? (int32_t)h.obj : -1;
     }
     free(sc.stack_face);
+    return 0;
+}
+
+/*
+ * Audit of the R-tree mode against OR_CULL_BOXES, per ray (OR_CULL_RTREE contexts only):
+ *   veto[r]  candidates the rtreego tree prunes although their OWN box passes Box.Intersect
+ *            and they would count: faces Möller–Trumbore accepts whose leaf entry passes but
+ *            an ancestor inner-node box fails, plus objects whose own box passes, with such
+ *            a face, pruned by the object tree;
+ *   ties[r]  objects on the ray where two distinct accepted faces share the minimum
+ *            distance (the R-tree's DFS order and the ascending index may pick different
+ *            winners: object.go:97's strict `<` keeps the first visited).
+ * The two culling modes can only differ on a ray where one of the two is non-zero.
+ */
+static int face_accepts(const or_mesh *m, uint32_t f, vec3 ro, vec3 rd, double *dist) {
+    vec3 p1 = mesh_vertex(m, m->face_v[3 * f]), p2 = mesh_vertex(m, m->face_v[3 * f + 1]),
+         p3 = mesh_vertex(m, m->face_v[3 * f + 2]);
+    vec3 ip; double bc[3];
+    if (!tri_intersection(p1, p2, p3, ro, rd, &ip, bc)) return 0;
+    *dist = v_len(v_sub(ro, ip));
+    return 1;
+}
+int or_rtree_audit(const or_ctx *c, uint32_t n, const double *orig, const double *dir, uint32_t *veto,
+                   uint32_t *ties) {
+    if (c->use_rtree != OR_CULL_RTREE) return -1;
+    uint32_t maxf = 0;
+    for (uint32_t i = 0; i < c->s.n_meshes; i++) if (c->s.meshes[i].n_faces > maxf) maxf = c->s.meshes[i].n_faces;
+    uint32_t *cand = (uint32_t *)malloc(sizeof(uint32_t) * (maxf + 1));
+    uint8_t *mark = (uint8_t *)malloc(maxf + 1);
+    uint32_t *ocand = (uint32_t *)malloc(sizeof(uint32_t) * (c->s.n_objects + 1));
+    uint8_t *omark = (uint8_t *)malloc(c->s.n_objects + 1);
+    uint64_t bt = 0;
+    for (uint32_t r = 0; r < n; r++) {
+        vec3 o = v_make(orig[3 * r], orig[3 * r + 1], orig[3 * r + 2]);
+        vec3 d = v_make(dir[3 * r], dir[3 * r + 1], dir[3 * r + 2]);
+        uint32_t nv = 0, nt = 0;
+        searchq oq = {o, d, ocand, 0, &bt};
+        rt_search(c->objs.root, &oq);
+        memset(omark, 0, c->s.n_objects + 1);
+        for (uint32_t k = 0; k < oq.n; k++) omark[ocand[k]] = 1;
+        for (uint32_t oi = 0; oi < c->s.n_objects; oi++) {
+            const or_object *ob = &c->s.objects[oi];
+            if (ob->mesh >= c->s.n_meshes) continue;
+            const or_mesh *m = c->meshes[ob->mesh].m;
+            vec3 ro = v_sub(o, v_make(ob->pos[0], ob->pos[1], ob->pos[2]));
+            const rect *fbox = c->meshes[ob->mesh].fbox;
+            /* both modes skip an object whose own box fails (its leaf entry is that box) */
+            if (!box_intersect(&c->obox[oi], o, d)) continue;
+            const int pruned = !omark[oi];
+            searchq fq = {ro, d, cand, 0, &bt};
+            rt_search(c->meshes[ob->mesh].faces.root, &fq);
+            memset(mark, 0, m->n_faces + 1);
+            for (uint32_t k = 0; k < fq.n; k++) mark[cand[k]] = 1;
+            int has = 0, tie = 0; double best = 0;
+            for (uint32_t f = 0; f < m->n_faces; f++) {
+                double dist;
+                if (!box_intersect(&fbox[f], ro, d) || !face_accepts(m, f, ro, d, &dist)) continue;
+                if (!mark[f] || pruned) nv++;  /* pruned above its own box */
+                if (!mark[f] || pruned) continue;
+                if (!has || dist < best) { has = 1; best = dist; tie = 0; }
+                else if (dist == best) tie = 1;
+            }
+            nt += (uint32_t)tie;
+        }
+        veto[r] = nv;
+        ties[r] = nt;
+    }
+    free(cand); free(mark); free(ocand); free(omark);
+    return 0;
+}
+
+/* The corners box_intersect uses (box.go:21-26 NewBox on the rtreego rect): {MinCorner,
+ * MaxCorner} of face.Bounds (mesh.go:30-50) and Object.Bounds (object.go:31-59). */
+static void rect_out(const rect *bb, double out[6]) {
+    for (int k = 0; k < 3; k++) { out[k] = bb->p[k]; out[3 + k] = bb->p[k] + (bb->q[k] - bb->p[k]); }
+}
+int or_face_box(const or_ctx *c, uint32_t mesh, uint32_t f, double out[6]) {
+    if (mesh >= c->s.n_meshes || f >= c->s.meshes[mesh].n_faces) return -1;
+    rect r = face_bounds(&c->s.meshes[mesh], f);
+    rect_out(&r, out);
+    return 0;
+}
+int or_object_box(const or_ctx *c, uint32_t oi, double out[6]) {
+    if (oi >= c->s.n_objects) return -1;
+    rect r = object_bounds(c, oi);
+    rect_out(&r, out);
+    return 0;
+}
+/* box.go:29-68 on n rays against one box given as NewBox corners (known-answer tests). */
+int or_box_intersect(const double box[6], uint32_t n, const double *orig, const double *dir, uint8_t *out) {
+    vec3 mn = v_make(box[0], box[1], box[2]), mx = v_make(box[3], box[4], box[5]);
+    for (uint32_t i = 0; i < n; i++)
+        out[i] = (uint8_t)corners_intersect(mn, mx, v_make(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
+                                            v_make(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]));
     return 0;
 }

@@ -1,0 +1,273 @@
+"""The reference's box culling, restated exactly.
+
+The reference searches only faces whose padded box (shared/state/mesh.go:30-50) and objects
+whose box (shared/state/object.go:31-59) the ray meets by geom.Box.Intersect
+(shared/geom/box.go:29-68), through rtreego (object.go:76, tracer.go:32).  The kernels gate
+every candidate by that test on its own box (the oracle's culling="boxes"); rtreego's inner
+nodes are not replicated.
+
+CPU: the boxes libmirt builds equal the oracle's; the oracle's Box.Intersect equals a pure
+Python restatement on adversarial rays; the "boxes" culling equals the R-tree oracle on every
+vertex-light soup, and wherever the two can differ per ray the audit names the cause (an
+rtreego inner node pruning a candidate whose own box passes, or a tie at the minimum
+distance, whose order rtreego's DFS decides).
+GPU: the device's Box.Intersect equals the oracle's on the same rays; frames and rays whose
+results hinge on a face box that rounds a hit out equal the R-tree oracle; the ablation
+(MIRT_OPT_NO_BOX_GATE) equals brute force.
+"""
+import math
+
+import numpy as np
+import pytest
+
+_NORMALS = ((1.0, 0.0, 0.0), (-1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, -1.0, 0.0), (0.0, 0.0, 1.0), (0.0, 0.0, -1.0))
+
+
+def _dot(a, b):
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]  # vector.go Dot, left to right
+
+
+def py_box_intersect(mn, mx, o, d):
+    """box.go:29-68 on NewBox corners, literally (Python floats are IEEE doubles)."""
+    for sn in _NORMALS:
+        dd = _dot(d, sn)
+        if dd != 0.0:
+            sp = mn if _dot(sn, (1.0, 1.0, 1.0)) < 0 else mx
+            ds = _dot([sp[k] - o[k] for k in range(3)], sn) / dd
+            if ds >= 0.0:
+                ip = [o[k] + ds * d[k] for k in range(3)]
+                ax = [k for k in range(3) if sn[k] == 0.0]
+                if all(mn[k] <= ip[k] <= mx[k] for k in ax):
+                    return True
+    return False
+
+
+def _norm(v):
+    v = np.asarray(v, np.float64)
+    n = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    return np.array([v[0] / n, v[1] / n, v[2] / n])
+
+
+def adversarial_rays(boxes, rng, per_box=24):
+    """Rays aimed at box corners, edge points and face centres from outside, from inside
+    and from a face plane, axis-parallel rays, and non-finite origins: the cases where the
+    reference's rounding decides.  Returns (origins, dirs, box index)."""
+    O, D, I = [], [], []
+    for bi, b in enumerate(boxes):
+        mn, mx = b[:3], b[3:]
+        c = 0.5 * (mn + mx)
+        ext = np.maximum(mx - mn, 1e-3)
+        for k in range(per_box):
+            kind = k % 8
+            corner = np.where(rng.integers(0, 2, 3) == 1, mx, mn)
+            if kind == 0:  # at a corner from outside
+                tgt, org = corner, corner + rng.normal(size=3) * ext * 4
+            elif kind == 1:  # at an edge point
+                a = int(rng.integers(3))
+                tgt = corner.copy()
+                tgt[a] = mn[a] + rng.random() * (mx[a] - mn[a])
+                org = tgt + rng.normal(size=3) * ext * 4
+            elif kind == 2:  # from inside through a corner
+                org = mn + rng.random(3) * (mx - mn)
+                tgt = corner
+            elif kind == 3:  # from a face plane
+                a = int(rng.integers(3))
+                org = mn + rng.random(3) * (mx - mn)
+                org[a] = corner[a]
+                tgt = corner + rng.normal(size=3) * ext
+            elif kind == 4:  # axis-parallel along a box edge line
+                a = int(rng.integers(3))
+                org = corner.copy()
+                org[a] -= ext[a] * (1 + rng.random())
+                d = np.zeros(3)
+                d[a] = 1.0
+                O.append(org), D.append(d), I.append(bi)
+                continue
+            elif kind == 5:  # grazing a face
+                a = int(rng.integers(3))
+                org = c + rng.normal(size=3) * ext * 3
+                org[a] = corner[a]
+                tgt = c.copy()
+                tgt[a] = corner[a]
+            elif kind == 6:  # at the centre
+                tgt, org = c, c + rng.normal(size=3) * ext * 5
+            else:  # a non-finite origin coordinate
+                org = c + rng.normal(size=3) * ext * 3
+                org[int(rng.integers(3))] = [np.inf, -np.inf, np.nan][int(rng.integers(3))]
+                D.append(_norm(rng.normal(size=3))), O.append(org), I.append(bi)
+                continue
+            O.append(org), D.append(_norm(tgt - org)), I.append(bi)
+    return np.array(O), np.array(D), np.array(I)
+
+
+def _soup_boxes(seed, n=64):
+    from oracle.oracle import Oracle
+    from scenes import soup_scene
+    sc = soup_scene(seed, vertex_light=True)
+    o = Oracle(sc, culling="boxes")
+    m = sc.meshes[0]
+    return np.array([o.face_box(0, f) for f in range(min(n, len(m.face_v)))])
+
+
+def test_face_and_object_bounds_match_oracle():
+    """mirt_face_bounds / mirt_object_bounds (the corners the kernels test) equal the oracle's
+    face.Bounds / Object.Bounds through NewBox, over soups, suzanne and awkward positions
+    (signed zeros, huge and tiny offsets)."""
+    import ctypes as C
+
+    from distributed_raytracer_amd import _lib as L
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    from scenes import soup_scene
+    from conftest import SCENE
+    scenes = [soup_scene(s, vertex_light=True) for s in (11, 12, 17)] + [load_scene(SCENE)]
+    positions = [(0.0, 0.0, 0.0), (-0.0, -0.0, -0.0), (1e-300, -1e-300, 0.0), (3.0e5, -7.25, 0.1),
+                 (1e16, -1e16, 1.5), (0.1, 0.2, 0.3)]
+    out = np.zeros(6)
+    for sc in scenes:
+        import copy
+        for pos in positions:
+            s2 = copy.copy(sc)
+            s2.objects = [(0, pos)]
+            o = Oracle(s2, culling="boxes")
+            m = s2.meshes[0]
+            v = np.ascontiguousarray(m.vertices, np.float64)
+            p = np.ascontiguousarray(pos, np.float64)
+            L.lib().mirt_object_bounds(v.ctypes.data, len(v), p.ctypes.data, out.ctypes.data)
+            ref = o.object_box(0)
+            assert out.tobytes() == ref.tobytes(), (pos, out, ref)
+        o = Oracle(sc, culling="boxes")
+        m = sc.meshes[0]
+        for f in range(0, len(m.face_v), max(1, len(m.face_v) // 200)):
+            vs = [np.ascontiguousarray(m.vertices[int(i)], np.float64) for i in m.face_v[f]]
+            L.lib().mirt_face_bounds(vs[0].ctypes.data, vs[1].ctypes.data, vs[2].ctypes.data, out.ctypes.data)
+            assert out.tobytes() == o.face_box(0, f).tobytes(), f
+    del C
+
+
+def test_oracle_box_intersect_equals_python_restatement():
+    from oracle.oracle import box_intersect
+    rng = np.random.default_rng(5)
+    boxes = _soup_boxes(12)
+    O, D, I = adversarial_rays(boxes, rng)
+    got = np.concatenate([box_intersect(boxes[i], O[k:k + 1], D[k:k + 1]) for k, i in enumerate(I)])
+    ref = np.array([py_box_intersect(boxes[i][:3].tolist(), boxes[i][3:].tolist(), O[k].tolist(), D[k].tolist())
+                    for k, i in enumerate(I)])
+    assert np.array_equal(got, ref)
+    # the rounding cases are real: some corner-aimed rays miss, some hit
+    assert 0 < got.sum() < len(got)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 17, 25])
+def test_boxes_culling_equals_rtree_on_vertex_light_soups(seed):
+    """Lights exactly on soup vertices, where brute force and the reference differ: the
+    oracle's per-box gating (what the GPU computes) equals the R-tree oracle pixel for pixel."""
+    from oracle.oracle import Oracle
+    from scenes import soup_scene
+    sc = soup_scene(seed, vertex_light=True)
+    W, H = 64, 48
+    fr = {m: Oracle(sc, culling=m).frame(W, H, nthreads=8) for m in ("brute", "rtree", "boxes")}
+    for k in ("valid", "obj", "face", "rgb", "rgb8"):
+        assert np.array_equal(fr["boxes"][k], fr["rtree"][k]), k
+    assert not np.array_equal(fr["brute"]["rgb"], fr["rtree"]["rgb"])  # the gate matters here
+
+
+def _vertex_rays(sc, rng, n):
+    V = sc.meshes[0].vertices + np.array(sc.objects[0][1])
+    tgt = V[rng.integers(len(V), size=n)]
+    org = tgt + rng.normal(size=(n, 3)) * 3
+    d = tgt - org
+    return org, d / np.linalg.norm(d, axis=1)[:, None]
+
+
+def test_rtree_residue_is_inner_nodes_or_ties():
+    """Per ray, the R-tree oracle and the boxes culling can only differ where the audit finds
+    an rtreego inner node pruning a candidate whose own box passes, or a tie at the minimum
+    distance (the DFS order picks the winner): checked on 60,000 rays aimed exactly at soup
+    vertices, the worst case for box rounding.  The vetoes exist (the audit is not vacuous)."""
+    from oracle.oracle import Oracle
+    from scenes import soup_scene
+    rng = np.random.default_rng(0)
+    vetoes = differ = 0
+    for seed in (14, 17, 18):
+        sc = soup_scene(seed, vertex_light=True)
+        R, B = Oracle(sc, culling="rtree"), Oracle(sc, culling="boxes")
+        org, d = _vertex_rays(sc, rng, 20000)
+        a, b = R.trace_rays(org, d), B.trace_rays(org, d)
+        veto, ties = R.rtree_audit(org, d)
+        diff = (a["ok"] != b["ok"]) | (a["face"] != b["face"]) | (a["hit"] != b["hit"]).any(axis=1)
+        assert not (diff & (veto == 0) & (ties == 0)).any()
+        vetoes += int((veto > 0).sum())
+        differ += int(diff.sum())
+    assert vetoes > 0
+
+
+@pytest.mark.gpu
+def test_device_box_intersect_equals_oracle(ctx):
+    """The kernels' Box.Intersect (far plane of the leaning axis first, then the six planes)
+    against the oracle's restatement of box.go, on adversarial rays over soup face boxes."""
+    from oracle.oracle import box_intersect
+    rng = np.random.default_rng(7)
+    boxes = np.concatenate([_soup_boxes(s, 200) for s in (11, 12, 17)])
+    O, D, I = adversarial_rays(boxes, rng, per_box=40)
+    got = ctx.debug_box_intersect(O, D, boxes[I])
+    ref = np.concatenate([box_intersect(boxes[i], O[k:k + 1], D[k:k + 1]) for k, i in enumerate(I)])
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} of {len(ref)} differ"
+    assert 0 < ref.sum() < len(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(11, 27))
+def test_vertex_light_soups_match_rtree_oracle(ctx, seed):
+    """All 16 vertex-light soups: every pixel equals the R-tree oracle (the reference's culling),
+    default and split kernels; the ablation without the boxes equals brute force."""
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from scenes import gpu_env, soup_scene
+    sc = soup_scene(seed, vertex_light=True)
+    env = gpu_env(ctx, sc)
+    W, H = 64, 48
+    ref = Oracle(sc, culling="rtree").frame(W, H, nthreads=8)
+    for opts in (0, rt._lib.MIRT_OPT_SPLIT_KERNELS, rt._lib.MIRT_OPT_BRUTE_FORCE):
+        ctx.set_options(opts)
+        try:
+            fb = rt.draw(env, W, H)
+        finally:
+            ctx.set_options(0)
+        for k in ("valid", "obj", "face", "rgb", "rgb8"):
+            a, b = getattr(fb, k), ref[k]
+            assert np.array_equal(a, b), f"options {opts}: {k} differs in {(a != b).sum()} elements"
+    ctx.set_options(rt._lib.MIRT_OPT_NO_BOX_GATE)
+    try:
+        fb = rt.draw(env, W, H)
+    finally:
+        ctx.set_options(0)
+    brute = Oracle(sc).frame(W, H, nthreads=8)
+    assert np.array_equal(fb.rgb, brute["rgb"]) and np.array_equal(fb.valid, brute["valid"])
+
+
+@pytest.mark.gpu
+def test_vertex_aimed_rays_match_boxes_oracle(ctx):
+    """mirt_trace_rays on rays aimed exactly at soup vertices: hit, face, point and normal equal
+    the boxes oracle's, including the rays whose brute-force winner's face box rounds the hit
+    out (the wave's second pass gates every candidate)."""
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from scenes import gpu_env, soup_scene
+    rng = np.random.default_rng(3)
+    gated = 0
+    for seed in (12, 17, 30):
+        sc = soup_scene(seed, vertex_light=True)
+        env = gpu_env(ctx, sc)
+        org, d = _vertex_rays(sc, rng, 20000)
+        ref = Oracle(sc, culling="boxes").trace_rays(org, d)
+        brute = Oracle(sc).trace_rays(org, d)
+        gated += int(((ref["ok"] != brute["ok"]) | (ref["face"] != brute["face"])).sum())
+        got = rt.trace_rays(org, d, env)
+        assert np.array_equal(got["ok"], ref["ok"])
+        ok = ref["ok"].astype(bool)
+        for k in ("face", "obj"):
+            assert np.array_equal(got[k][ok], ref[k][ok]), k
+        for k in ("hit", "normal"):
+            assert np.array_equal(got[k][ok], ref[k][ok]), k
+    assert gated > 0

@@ -3,11 +3,11 @@ collinear and zero-area faces, several materials, vertex normals on one mesh and
 normals on the other, 1-3 overlapping objects, lights on a vertex, inside the soups and
 far away, random cameras.  CPU: the oracle's R-tree culling equals its brute force on
 them, except where a light sits exactly on a mesh vertex: there the reference's face-box
-test (box.go:29-68 on mesh.go:30-50's padded box) can round a hit at the box's corner out,
-which brute force and the GPU's exact culling keep (pinned below).
+test (box.go:29-68 on mesh.go:30-50's padded box) can round a hit at the box's corner out
+(pinned below).  The kernels apply that test too (tests/test_box_gate.py
+checks the vertex-light soups against the R-tree oracle).
 GPU: every pixel (valid, object, face, fp64 colour, rgb8) equals the R-tree oracle's, and
-the kernel variants (brute force, no light table, split kernels) equal the default; with a
-light on a vertex, every pixel equals the brute-force oracle's."""
+the kernel variants (brute force, no light table, split kernels) equal the default."""
 import dataclasses
 import math
 
@@ -135,19 +135,6 @@ def test_soup_frames_match_oracle(ctx, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [12, 17])
-def test_vertex_light_soups_match_brute_force_oracle(ctx, seed):
-    """The documented face-box exception: the GPU keeps the hit at the vertex (exact culling),
-    like the brute-force oracle."""
-    import distributed_raytracer_amd as rt
-    from oracle.oracle import Oracle
-    from scenes import gpu_env, soup_scene
-    sc = soup_scene(seed, vertex_light=True)
-    env = gpu_env(ctx, sc)
-    _check(rt.draw(env, 64, 48), Oracle(sc).frame(64, 48, nthreads=8))
-
-
-@pytest.mark.gpu
 def test_streamed_soup_matches_oracle(ctx):
     """A soup above kLdsTris (1024) triangles: the HBM-streamed mesh path."""
     import distributed_raytracer_amd as rt
@@ -156,7 +143,7 @@ def test_streamed_soup_matches_oracle(ctx):
     sc = soup_scene(21, ntri=(1500, 2500))
     env = gpu_env(ctx, sc)
     fb = rt.draw(env, 96, 72)
-    ref = Oracle(sc).frame(96, 72, nthreads=8)
+    ref = Oracle(sc, culling="rtree").frame(96, 72, nthreads=8)
     assert ref["valid"].sum() > 200
     _check(fb, ref)
 

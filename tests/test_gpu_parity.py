@@ -353,8 +353,15 @@ def test_device_tiles_packed_and_unpacked(ctx, env):
         assert np.array_equal(full.rgb8.cpu().numpy()[hit], g["rgb8"])
 
 
-def test_trace_rays_matches_oracle(env, oracle, py_scene):
+def test_trace_rays_matches_oracle(env, py_scene):
+    """Rays aimed exactly at vertices (box corners of their faces), edge midpoints and surface
+    points: every output equals the oracle with the reference's face and object boxes
+    (culling="boxes"; on these rays it differs from brute force on 6, and from the R-tree
+    oracle only on rays with two faces at the minimum distance, whose order rtreego's DFS
+    decides: tests/test_box_gate.py)."""
     import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    oracle = Oracle(py_scene, culling="boxes")
     rng = np.random.default_rng(3)
     n = 4000
     m = py_scene.meshes[0]
@@ -694,7 +701,7 @@ def test_near_coplanar_and_subnormal_direction_rays(ctx, env, py_scene):
     sd = (X - so) / np.linalg.norm(X - so, axis=1)[:, None]
     sub_o = np.concatenate([so, so])
     sub_d = np.concatenate([sd * 1e-310, sd * 4e-320])
-    orc = Oracle(py_scene, use_rtree=False)
+    orc = Oracle(py_scene, culling="boxes")  # the kernels' semantics: every candidate box-gated
     try:
         for origins, dirs, exact in ((go, gd, True), (sub_o, sub_d, False)):
             ref = orc.trace_rays(origins, dirs)
@@ -736,7 +743,8 @@ def test_rays_at_triangle_edges_and_vertices(ctx, env, py_scene):
     rays it must leave undecided: rays aimed exactly at vertices, edge midpoints and points
     1e-15 .. 1e-9 (relative) inside and outside edges, from random origins (primary-like)
     and from just above the surface (shadow-like).  Default kernel, MIRT_OPT_NO_PREFILTER
-    (the reference's divides for every lane) and brute force all equal the oracle."""
+    (the reference's divides for every lane) and brute force all equal the oracle with the
+    reference's face and object boxes (culling="boxes"; vertices are box corners)."""
     import distributed_raytracer_amd as rt
     import distributed_raytracer_amd._lib as L
     from oracle.oracle import Oracle
@@ -760,7 +768,7 @@ def test_rays_at_triangle_edges_and_vertices(ctx, env, py_scene):
     origins = np.concatenate([far, near])
     dirs = np.concatenate([T, T]) - origins
     dirs /= np.linalg.norm(dirs, axis=1)[:, None]
-    ref = Oracle(py_scene, use_rtree=False).trace_rays(origins, dirs)
+    ref = Oracle(py_scene, culling="boxes").trace_rays(origins, dirs)
     assert ref["ok"].sum() > len(origins) // 2
     try:
         for opts in (0, L.MIRT_OPT_NO_PREFILTER, L.MIRT_OPT_BRUTE_FORCE):

@@ -168,3 +168,74 @@ def test_light_table_record_layout():
     ntL = np.einsum("ij,ij->i", A, (L - pos)[None, :] - tri[:, 0:3])
     assert np.allclose(rec[:, 12], ntL, rtol=1e-5, atol=1e-9)
     assert (rec[:, 13:16] > 0).all()
+
+
+@pytest.mark.gpu
+def test_device_light_table_equals_host(ctx):
+    """k_light_table (the builder the cache uses) and the host builder share lighttab.hpp's
+    arithmetic: bit-identical records for suzanne with lights on a vertex, in a face plane,
+    inside the mesh, far away and at 1e30, and for a soup at an offset position."""
+    from scenes import soup_scene
+    tri, scale, pos, V, F = _mesh()
+    rng = np.random.default_rng(4)
+    lights = np.concatenate([_light_positions(V, F, rng), [[0.1, 0.2, 0.3], [1e30, -2.0, 3.0], [40.0, 50.0, -60.0]]])
+    cases = [(tri, scale, pos, lights[:16])]
+    sc = soup_scene(12, vertex_light=True)
+    m = sc.meshes[0]
+    Vs, Fs = np.asarray(m.vertices, np.float64), np.asarray(m.face_v, np.int64)
+    ts = np.concatenate([Vs[Fs[:, 0]], Vs[Fs[:, 1]] - Vs[Fs[:, 0]], Vs[Fs[:, 2]] - Vs[Fs[:, 0]]], axis=1)
+    cases.append((ts, float(np.abs(Vs).max()), np.array([0.5, -3.0, 2.25]), np.array([l[0] for l in sc.lights])))
+    for t, s, p, L in cases:
+        host = _records(t, s, p, L)
+        dev = np.zeros_like(host)
+        tt = np.ascontiguousarray(t, np.float64)
+        pp = np.ascontiguousarray(p, np.float64)
+        lp = np.ascontiguousarray(L, np.float64)
+        assert _lib().mirt_debug_light_table_gpu(ctx.handle, tt.ctypes.data, len(t), s, pp.ctypes.data, lp.ctypes.data,
+                                                 len(L), dev.ctypes.data) == 0
+        assert host.tobytes() == dev.tobytes()
+
+
+def _cache_stats(ctx):
+    out = np.zeros(8, np.uint64)
+    assert _lib().mirt_light_cache_stats(ctx.handle, out.ctypes.data) == 0
+    return dict(zip(("builds", "hits", "evictions", "fallbacks", "reused", "live", "bytes", "cap"), map(int, out)))
+
+
+@pytest.mark.gpu
+def test_light_cache_cycles_more_keys_than_fit(ctx):
+    """Lights moving every frame with a cache that holds three tables: 40 light sets, each
+    traced twice in a row, then the first ones again.  Every frame equals the oracle; tables
+    are built on the device, reused on a repeat, evicted (least recently used, once their
+    readers are done) and their buffers reused; frames that find no room are counted."""
+    import dataclasses
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.tracer import Light
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    sc = load_scene(SCENE)
+    env = rt.Environment.from_file(SCENE, ctx)
+    base = env.mutable()
+    n_tri = len(sc.meshes[0].face_v)
+    one = len(sc.lights) * n_tri * 64
+    W, H = 48, 36
+    s0 = _cache_stats(ctx)
+    _lib().mirt_set_light_cache(ctx.handle, 3 * one + 1024)
+    rng = np.random.default_rng(9)
+    keys = [[(tuple(np.array(p) + rng.normal(size=3) * 0.5), c) for p, c in sc.lights] for _ in range(40)]
+    try:
+        for k in list(range(40)) + list(range(4)):
+            lights = keys[k]
+            mut = dataclasses.replace(base, lights=[Light(pos=p, col=c) for p, c in lights])
+            sck = dataclasses.replace(sc, lights=lights)
+            ref = Oracle(sck, culling="rtree").frame(W, H, nthreads=8)
+            for _ in range(2):
+                fb = rt.draw(env, W, H, mut)
+                assert np.array_equal(fb.rgb, ref["rgb"]) and np.array_equal(fb.valid, ref["valid"]), k
+        st = _cache_stats(ctx)
+        d = {k: st[k] - s0[k] for k in ("builds", "hits", "evictions", "fallbacks", "reused")}
+        # (tables of the last 16 calls are never evicted, so some frames find no room here)
+        assert d["builds"] > 3 and d["hits"] > 3 and d["evictions"] > 0 and d["reused"] > 0, d
+        assert st["bytes"] <= 3 * one + 1024 and st["live"] <= 3
+    finally:
+        _lib().mirt_set_light_cache(ctx.handle, 4 << 30)
