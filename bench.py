@@ -169,6 +169,8 @@ def parse():
     ap.add_argument("--reflect-chains", action="store_true",
                     help="variant (--bounces): reflections as per-pixel chains in one kernel (k_reflect) instead of "
                          "level by level with rays packed in block order (k_bounce / k_pack / k_shadow)")
+    ap.add_argument("--no-box-gate", action="store_true",
+                    help="ablation: without the reference's face/object Box.Intersect (brute-force semantics)")
     ap.add_argument("--no-light-table", action="store_true",
                     help="ablation: shadow segments without the fp32 light-table pre-classification")
     ap.add_argument("--views", action="store_true",
@@ -378,7 +380,7 @@ def main():
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
         rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0) | (
-        rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0)
+        rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0) | (rt._lib.MIRT_OPT_NO_BOX_GATE if a.no_box_gate else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses

@@ -275,18 +275,44 @@ __device__ __forceinline__ bool box_plane(const double* bx, V3 o, V3 d, int a, b
     const double ib = v3c(o, b) + ds * v3c(d, b), ic = v3c(o, c) + ds * v3c(d, c);  // box.go:47
     return da != 0.0 && ds >= 0.0 && bx[b] <= ib && ib <= bx[3 + b] && bx[c] <= ic && ic <= bx[3 + c];
 }
+// The far plane of axis A (+e_A for d_A > 0, -e_A for d_A < 0), A known at compile time.
+template <int A>
+__device__ __forceinline__ bool box_far(const double* bx, V3 o, V3 d) {
+    return box_plane(bx, o, d, A, (A == 0 ? d.x : A == 1 ? d.y : d.z) > 0.0);
+}
+// A pointer the compiler cannot prove loop-invariant: loads through it stay at their use
+// instead of being hoisted to the kernel's start and held in SGPRs across the work loop.
+template <typename T>
+__device__ __forceinline__ const T* at_use(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
 // Box.Intersect for the lanes `on` (false on the others).  A ray that meets a box leaves it
 // through the far plane of some axis (+e_a for d_a > 0, -e_a for d_a < 0); the wave first
 // tries the far plane of the axis its first lane's direction leans on most (a wave-uniform
-// axis), and only the lanes that plane does not prove true go through the six planes, one
-// at a time (a short loop: this is the rare path).  Same boolean as the reference's.
+// axis: one branch to straight-line code), and only the lanes that plane does not prove true
+// go through the six planes, one at a time (a short loop: this is the rare path).  Same
+// boolean as the reference's.
 __device__ __forceinline__ bool box_gate(const double* bx, V3 o, V3 d, bool on) {
     if (__ballot(on) == 0) return false;
     const double ax = __builtin_fabs(d.x), ay = __builtin_fabs(d.y), az = __builtin_fabs(d.z);
     const int lean = (ax >= ay && ax >= az) ? 0 : ay >= az ? 1 : 2;
     const int a = __builtin_amdgcn_readfirstlane(lean);
     bool r = false;
-    if (on) r = box_plane(bx, o, d, a, v3c(d, a) > 0.0);
+    if (on) r = a == 0 ? box_far<0>(bx, o, d) : a == 1 ? box_far<1>(bx, o, d) : box_far<2>(bx, o, d);
+    if (__ballot(on && !r) == 0) return r;
+#pragma unroll 1
+    for (int q = 0; q < 6; ++q) {
+        const bool left = on && !r;
+        if (__ballot(left) == 0) break;
+        if (left) r = box_plane(bx, o, d, q >> 1, (q & 1) == 0);
+    }
+    return r;
+}
+// The same boolean with the least code: the six planes one at a time (the second pass's
+// per-candidate test, inside the sweep, where registers are scarce).
+__device__ __forceinline__ bool box_gate_small(const double* bx, V3 o, V3 d, bool on) {
+    bool r = false;
 #pragma unroll 1
     for (int q = 0; q < 6; ++q) {
         const bool left = on && !r;
@@ -344,9 +370,10 @@ __device__ __forceinline__ bool seg_reject(const SegPre& p, const float* w) {
 // record of position pos0 (in LDS or in HBM).
 //   lt (shadow segments; NULL: none): the light table at position pos0 (kLtD floats per
 //   triangle), sp the lane's SegPre, live the lanes whose result still matters.
-//   fbox (non-null: a trace's second pass, trace_nearest / shadow_lit_single): a candidate
-//   counts only if its face box passes the reference's Box.Intersect (object.go:76).
-template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, bool LT3 = true, typename SrcPtr>
+//   GATE (a trace's second pass, trace_nearest / shadow_lit_single): a candidate counts only
+//   if its face box (fbox, BVH order) passes the reference's Box.Intersect (object.go:76).
+template <bool REL, bool PREFILTER, int DG = 0, bool TPRE = false, bool LT3 = true, bool GATE = false,
+          typename SrcPtr>
 __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restrict__ fidx, uint32_t pos0,
                                            uint32_t n, V3 ro, V3 d, V3 neg, Best& b, uint32_t& wtests,
                                            const float* lt = nullptr, const SegPre* sp = nullptr, bool live = true,
@@ -364,7 +391,7 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
         const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
         bool acc = maybe && mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt);
-        if (fbox) acc = box_gate(fbox + (size_t)k * kBoxD, ro, d, acc);  // wave-uniform branch
+        if (GATE) acc = box_gate_small(fbox + (size_t)k * kBoxD, ro, d, acc);
         if (acc) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
@@ -400,12 +427,18 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
             if (__ballot(m0) != 0) test(i, m0);
             if (__ballot(m1) != 0) test(i + 1, m1);
         }
+    } else if (TPRE && GATE) {  // a second pass (rare): the least code
+#pragma unroll 1
+        for (uint32_t i = 0; i < n; ++i) test(i, true);
     } else if (TPRE) {
         // unrolled by two by hand, as the classified loop above
         for (uint32_t i = 0; i < n; i += 2) {
             test(i, true);
             if (i + 1 < n) test(i + 1, true);
         }
+    } else if (GATE) {  // a second pass (rare): the least code
+#pragma unroll 1
+        for (uint32_t i = 0; i < n; ++i) test(i, true);
     } else {
 #pragma unroll 2
         for (uint32_t i = 0; i < n; ++i) test(i, true);
@@ -670,8 +703,8 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 //   made); the walk ends when no live lane is left.
 // Packets with a lane whose object-space origin is beyond the cull limit (the inflation
 // argument needs a bounded origin) enter every child.
-//   fbox: candidates pass their face box first (test_range; a trace's second pass).
-template <bool REL, bool PREFILTER, bool SEG, bool LT3 = true, typename SrcPtr>
+//   GATE: candidates pass their face box (fbox) first (test_range; a trace's second pass).
+template <bool REL, bool PREFILTER, bool SEG, bool LT3 = true, bool GATE = false, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
                                           Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true,
                                           const float* lt = nullptr, const SegPre* sp = nullptr,
@@ -693,8 +726,9 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
             diag(SEG ? 14 : 6);
-            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
-                                                    vis.tests, lt ? lt + (size_t)first * kLtD : nullptr, sp, live, fbox);
+            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3, GATE>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d,
+                                                                 neg, b, vis.tests,
+                                                                 lt ? lt + (size_t)first * kLtD : nullptr, sp, live, fbox);
             if (SEG) {
                 live = live && !(b.has && b.d < resolve);
                 if (__ballot(live) == 0) break;
@@ -1022,94 +1056,116 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   direction and crect the block's range of directions (view_sweep).
 //   The reference searches only objects whose box the ray meets (tracer.go:32) and only faces
 //   whose box it meets (object.go:76), by Box.Intersect (box.go:29-68) on the padded boxes of
-//   shared/state (rtreego's inner nodes are not replicated).  Pass 1 sweeps
-//   every candidate (the culling is exact) and applies the boxes to its outcome: an object
+//   shared/state (rtreego's inner nodes are not replicated).  The sweep keeps
+//   every candidate (the culling is exact) and the boxes are applied to its outcome: an object
 //   box that fails removes the object; a winner whose face box passes, with no NaN distance
 //   around (whose first-hit rule could elect another face), is the nearest gated candidate
-//   itself.  Should some lane's winner fail its face box, the wave runs pass 2: every lane
-//   again, each candidate gated before it counts (test_range) — the same sweep code, so the
-//   rare path adds no register pressure to the common one.  MIRT_OPT_NO_BOX_GATE: no boxes
-//   (brute-force semantics).
+//   itself.  Should some lane's winner fail its face box, `redo` is set (wave-uniform; the
+//   result is then meaningless) and the caller runs its work item again with pass2, where every
+//   candidate is gated before it counts (an LDS-resident mesh swept whole, an HBM mesh through
+//   its BVH).  The retry lives in the callers' work loops: a loop around the sweep here cost
+//   ~5% of the frame (VALU and SALU of the restructured sweep, tools/ab_valu.sh).
+//   MIRT_OPT_NO_BOX_GATE: no boxes (brute-force semantics).
 template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
 __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
-                                 bool lane_on, bool want_normal, Visits& vis, uint32_t* __restrict__ stk = nullptr,
-                                 const ViewLeaf* vt = nullptr, uint32_t vn = 0, float ls = 0.0f, float lt = 0.0f,
-                                 float4 crect = float4{0.0f, 0.0f, 0.0f, 0.0f}) {
+                                 bool lane_on, bool want_normal, Visits& vis, bool pass2, bool& redo,
+                                 uint32_t* __restrict__ stk = nullptr, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                 float ls = 0.0f, float lt = 0.0f, float4 crect = float4{0.0f, 0.0f, 0.0f, 0.0f}) {
     Nearest best;
+    best.ok = false;
+    best.obj = best.face = best.mat = 0;
+    best.hit = best.normal = V3{0, 0, 0};
+    double bestcd = 0;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
-    bool pass2 = false;  // wave-uniform
-#pragma unroll 1
-    for (;;) {
-        best.ok = false;
-        best.obj = best.face = best.mat = 0;
-        best.hit = best.normal = V3{0, 0, 0};
-        double bestcd = 0;
-        bool redo = false;
-        for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
-            const DevObject& ob = fa.obj[oi];
-            V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
-            V3 neg = scale(d, -1);  // triangle.go:38 rDir.Scale(-1)
-            Best b;
-            best_init(b);
-            const uint32_t ntri = ob.m.ntri;
-            const double* fgate = pass2 ? mesh_fbox(ob.m) : nullptr;
-            if (BRUTE) {
-                if (resident)
-                    test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests, nullptr, nullptr, true,
-                                               fgate);
-                else  // every triangle straight from HBM (waves run independently: no LDS staging)
-                    test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests, nullptr,
-                                                 nullptr, true, fgate);
-            } else if (COMMON && !pass2) {
-                const Ray32 r = ray32(ro, d);
-                const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-                const bool force = !(far <= ob.m.cull_limit);
-                const Cone cone = make_cone(ro, r.ix, r.iy, r.iz, lane_on, force, 0.0f, __builtin_inff(), ob.m.cull_limit);
-                if (resident)
-                    bvh_wide<REL, PREFILTER, false>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow);
-                else
-                    bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
-                                                      vis.overflow);
-            } else if (resident && !REL && vt && !pass2) {
-                view_sweep<PREFILTER, false>(ob.m, lds, vt, vn, ls, lt, false, crect.x, crect.y, crect.z, crect.w,
-                                             __builtin_inff(), ro, d, neg, lane_on, b, vis);
-            } else if (resident) {
-                bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
-                                                 !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr, fgate);
-            } else {
-                bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
-                                                   !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr, fgate);
-            }
-            uint32_t face = 0, pos = 0;
-            bool got = lane_on && best_result(b, face, pos);
-            if (gating) {
-                got = box_gate(ob.box, o, d, got);  // tracer.go:32: the object's box
-                if (!pass2) {
-                    const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)pos * kBoxD, ro, d, got);  // object.go:76
-                    redo = redo || (got && (!fok || b.any_nan));
-                }
-            }
-            if (got) {
-                V3 world, normal{0, 0, 0};
-                uint32_t mat = 0;
-                winner(ob, pos, ro, d, neg, world, normal, mat, want_normal);
-                double cd = len(sub(world, cam));  // tracer.go:38
-                if (!best.ok || cd < bestcd) {
-                    best.ok = true;
-                    bestcd = cd;
-                    best.obj = oi;
-                    best.face = face;
-                    best.mat = mat;
-                    best.hit = world;
-                    best.normal = normal;
-                }
+    bool again = false;
+    for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
+        const DevObject& ob = fa.obj[oi];
+        V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
+        V3 neg = scale(d, -1);  // triangle.go:38 rDir.Scale(-1)
+        Best b;
+        best_init(b);
+        const uint32_t ntri = ob.m.ntri;
+        if (pass2) {
+            // every candidate gated: an LDS-resident mesh (<= kLdsTris faces) is swept whole,
+            // which keeps the gate's code out of the BVH walk; an HBM mesh walks its BVH
+            if (resident)
+                test_range<REL, PREFILTER, 0, false, true, true>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests,
+                                                               nullptr, nullptr, true, mesh_fbox(ob.m));
+            else if (BRUTE)
+                test_range<false, PREFILTER, 0, false, true, true>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b,
+                                                                 vis.tests, nullptr, nullptr, true, mesh_fbox(ob.m));
+            else
+                bvh_sweep<false, PREFILTER, false, true, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f,
+                                                               0.0, !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr,
+                                                               mesh_fbox(ob.m));
+        } else if (BRUTE) {
+            if (resident)
+                test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+            else  // every triangle straight from HBM (waves run independently: no LDS staging)
+                test_range<false, PREFILTER>((cdptr)ob.m.tri, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
+        } else if (COMMON) {
+            const Ray32 r = ray32(ro, d);
+            const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+            const bool force = !(far <= ob.m.cull_limit);
+            const Cone cone = make_cone(ro, r.ix, r.iy, r.iz, lane_on, force, 0.0f, __builtin_inff(), ob.m.cull_limit);
+            if (resident)
+                bvh_wide<REL, PREFILTER, false>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow);
+            else
+                bvh_wide<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                                  vis.overflow);
+        } else if (resident && !REL && vt) {
+            view_sweep<PREFILTER, false>(ob.m, lds, vt, vn, ls, lt, false, crect.x, crect.y, crect.z, crect.w,
+                                         __builtin_inff(), ro, d, neg, lane_on, b, vis);
+        } else if (resident) {
+            bvh_sweep<REL, PREFILTER, false>(ob.m, lds, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                             !(fa.flags & MIRT_OPT_NO_OCTANT));
+        } else {
+            bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
+                                               !(fa.flags & MIRT_OPT_NO_OCTANT));
+        }
+        uint32_t face = 0, pos = 0;
+        bool got = lane_on && best_result(b, face, pos);
+        if (gating) {
+            got = box_gate(ob.box, o, d, got);  // tracer.go:32: the object's box
+            if (!pass2) {
+                const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)pos * kBoxD, ro, d, got);  // object.go:76
+                again = again || (got && (!fok || b.any_nan));
             }
         }
-        if (pass2 || __ballot(redo) == 0) break;
-        pass2 = true;
+        if (got) {
+            V3 world, normal{0, 0, 0};
+            uint32_t mat = 0;
+            winner(ob, pos, ro, d, neg, world, normal, mat, want_normal);
+            double cd = len(sub(world, cam));  // tracer.go:38
+            if (!best.ok || cd < bestcd) {
+                best.ok = true;
+                bestcd = cd;
+                best.obj = oi;
+                best.face = face;
+                best.mat = mat;
+                best.hit = world;
+                best.normal = normal;
+            }
+        }
     }
+    redo = __ballot(again) != 0;
     return best;
+}
+// trace_nearest with its second pass in place, for callers without a work loop to retry in
+// (k_rays, the reflection chains, k_bounce's own shadows).
+template <bool REL, bool PREFILTER, bool BRUTE>
+__device__ __forceinline__ Nearest trace_nearest_settled(const FrameArgs& fa, const double* __restrict__ lds,
+                                                         bool resident, V3 o, V3 d, bool lane_on, bool want_normal,
+                                                         Visits& vis) {
+    bool redo = false;
+    Nearest r;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        r = trace_nearest<REL, PREFILTER, BRUTE>(fa, lds, resident, o, d, lane_on, want_normal, vis, pass == 1, redo);
+        if (!redo) break;
+    }
+    return r;
 }
 
 // Shadow ray of a one-object frame as a segment query (exact; DESIGN.md §4 "Shadow
@@ -1124,13 +1180,25 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
 //   vt / vh (LDS-resident): the light's view table and header (view_sweep from the light).
 //   LT3: a three-face leaf loads its three light-table records at once (k_trace; the split
 //   k_shadow loads two per step, which spills fewer VGPRs there)
+//   The reference's boxes (trace_nearest) are applied to what the decision rests on: a lane
+//   that retired rests on its candidate b.pos (a gated candidate nearer than `resolve` proves
+//   "not lit" whatever else the boxes remove); a lane whose candidates all lie beyond the light
+//   (no NaN distance) is lit under any gating; else it rests on the winner, which must pass
+//   with no NaN distance around.  An object box that fails leaves no candidate (lit).  A face
+//   box that fails sets `redo` (wave-uniform; the result is then meaningless): the caller runs
+//   the work item again with pass2, where every candidate is gated before it counts.  The
+//   retry lives in the callers' own work loops, so the sweep's code is not wrapped in a second
+//   loop (that cost 12 spilled VGPRs in k_trace).
 template <bool PREFILTER, bool LT3 = true>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
                                                   uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, uint32_t li,
-                                                  bool lane_on, Visits& vis, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                                  bool lane_on, Visits& vis, bool pass2, bool& redo,
+                                                  const ViewLeaf* vt = nullptr, uint32_t vn = 0,
                                                   const ViewHead* vh = nullptr) {
     const DevObject& ob = fa.obj[0];
     const V3 pos{ob.pos[0], ob.pos[1], ob.pos[2]};
+    const V3 ro = sub(o, pos);  // object.go:71
+    const V3 neg = scale(d, -1);
     const double lh = len(sub(lpos, hit));
     const double mag = fmax(fmax(fmax(__builtin_fabs(o.x), __builtin_fabs(o.y)), __builtin_fabs(o.z)),
                             fmax(fmax(__builtin_fabs(pos.x), __builtin_fabs(pos.y)), __builtin_fabs(pos.z)));
@@ -1138,91 +1206,90 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     const double resolve = lh - 1e-4 - M;
     const float tmax = (float)(lh + 1e-4 + M) * (1.0f + 0x1p-20f);
     const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
+    redo = false;
     Best b;
-    bool pass2 = false;  // wave-uniform: trace_nearest's two passes
-#pragma unroll 1
-    for (;;) {
-        best_init(b);
-        // (the sweep's inputs are made inside the loop: kept live across the box tests they
-        // would cost registers the sweep needs)
-        const V3 ro = sub(o, pos);  // object.go:71
-        const V3 neg = scale(d, -1);
-        // Culling cone: the packet's rays walked backwards from the light, L + s * (-d), over
-        // s in [-(2e-4 + M), lh]: it covers o + t * d for t in [0, tmax] (o, L and d are
-        // collinear up to fp64 rounding, far inside the box inflation).
-        const Ray32 r = ray32(ro, d);
-        const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
-        const bool force = !(far <= ob.m.cull_limit);
-        const float smin = -(float)(2e-4 + M) * (1.0f + 0x1p-20f);
-        const float smax = (float)lh * (1.0f + 0x1p-20f);
-        Cone cone;
-        if (MIRT_SHADOW_WIDE) cone = make_cone(sub(lpos, pos), -r.ix, -r.iy, -r.iz, lane_on, force, smin, smax, ob.m.cull_limit);
-        if (MIRT_SHADOW_WIDE && !pass2) {
-            if (resident)
-                bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
-                                                 tmax, resolve);
-            else
-                bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
-                                                 vis.overflow, tmax, resolve);
-        } else if (resident && vt && !pass2) {
-            // the lane's direction from the light: its hit point relative to the view point (every
-            // point of the segment short of the light lies in that direction)
-            const double* R0 = vh->R[0];
-            const double* R1 = vh->R[1];
-            const double* R2 = vh->R[2];
-            const V3 X = sub(sub(hit, pos), V3{vh->O[0], vh->O[1], vh->O[2]});
-            const double z = R0[0] * X.x + R0[1] * X.y + R0[2] * X.z;
-            const double mag = fmax(fmax(__builtin_fabs(X.x), __builtin_fabs(X.y)), __builtin_fabs(X.z));
-            const bool unb = !(z > 0x1p-20 * mag);
-            float ls = 0.0f, lt = 0.0f;
-            if (!unb) {
-                ls = (float)((R1[0] * X.x + R1[1] * X.y + R1[2] * X.z) / z);
-                lt = (float)((R2[0] * X.x + R2[1] * X.y + R2[2] * X.z) / z);
-            }
-            const bool any_unb = __ballot(lane_on && unb) != 0;
-            const float inf = __builtin_inff();
-            float cs0 = -inf, cs1 = inf, ct0 = -inf, ct1 = inf;
-            if (!any_unb) {
-                const bool on = lane_on;
-                cs0 = wave_reduce<true>(on ? ls : inf);
-                cs1 = wave_reduce<false>(on ? ls : -inf);
-                ct0 = wave_reduce<true>(on ? lt : inf);
-                ct1 = wave_reduce<false>(on ? lt : -inf);
-            }
-            // a candidate of the segment lies within |L - hit| of the light (or within near_r)
-            const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
-            view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b,
-                                        vis, resolve, tmax);
-        } else {
-            // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
-            const float* lt = fa.ltab && li < fa.n_lights ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
-            SegPre sp;
-            if (lt) sp = seg_pre(d, lh);
-            const double* fgate = pass2 ? mesh_fbox(ob.m) : nullptr;
-            if (resident)
-                bvh_sweep<false, PREFILTER, true, LT3>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                                      !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp, fgate);
-            else
-                bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                                      !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp, fgate);
+    best_init(b);
+    // Culling cone: the packet's rays walked backwards from the light, L + s * (-d), over
+    // s in [-(2e-4 + M), lh]: it covers o + t * d for t in [0, tmax] (o, L and d are
+    // collinear up to fp64 rounding, far inside the box inflation).
+    const Ray32 r = ray32(ro, d);
+    const double far = fmax(fmax(__builtin_fabs(ro.x), __builtin_fabs(ro.y)), __builtin_fabs(ro.z));
+    const bool force = !(far <= ob.m.cull_limit);
+    const float smin = -(float)(2e-4 + M) * (1.0f + 0x1p-20f);
+    const float smax = (float)lh * (1.0f + 0x1p-20f);
+    Cone cone;
+    if (MIRT_SHADOW_WIDE) cone = make_cone(sub(lpos, pos), -r.ix, -r.iy, -r.iz, lane_on, force, smin, smax, ob.m.cull_limit);
+    if (pass2) {
+        // every candidate gated (as trace_nearest's pass 2): an LDS-resident mesh swept whole,
+        // an HBM mesh through its BVH
+        if (resident)
+            test_range<false, PREFILTER, 8, true, false, true>(lds, ob.m.fidx, 0, ob.m.ntri, ro, d, neg, b, vis.tests,
+                                                             nullptr, nullptr, lane_on, mesh_fbox(ob.m));
+        else
+            bvh_sweep<false, PREFILTER, true, LT3, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax,
+                                                         resolve, !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr,
+                                                         mesh_fbox(ob.m));
+    } else if (MIRT_SHADOW_WIDE) {
+        if (resident)
+            bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
+                                             tmax, resolve);
+        else
+            bvh_wide<false, PREFILTER, true>(ob.m, (cdptr)ob.m.tri, stk, cone, r, force, ro, d, neg, lane_on, b, vis,
+                                             vis.overflow, tmax, resolve);
+    } else if (resident && vt) {
+        // the lane's direction from the light: its hit point relative to the view point (every
+        // point of the segment short of the light lies in that direction)
+        const double* R0 = vh->R[0];
+        const double* R1 = vh->R[1];
+        const double* R2 = vh->R[2];
+        const V3 X = sub(sub(hit, pos), V3{vh->O[0], vh->O[1], vh->O[2]});
+        const double z = R0[0] * X.x + R0[1] * X.y + R0[2] * X.z;
+        const double mag = fmax(fmax(__builtin_fabs(X.x), __builtin_fabs(X.y)), __builtin_fabs(X.z));
+        const bool unb = !(z > 0x1p-20 * mag);
+        float ls = 0.0f, lt = 0.0f;
+        if (!unb) {
+            ls = (float)((R1[0] * X.x + R1[1] * X.y + R1[2] * X.z) / z);
+            lt = (float)((R2[0] * X.x + R2[1] * X.y + R2[2] * X.z) / z);
         }
-        if (!gating) break;
-        // The reference's boxes (trace_nearest), applied to what the decision below rests on: a
-        // lane that retired rests on its candidate b.pos (a gated candidate nearer than
-        // `resolve` proves "not lit" whatever else the boxes remove); a lane whose candidates
-        // all lie beyond the light (no NaN distance) is lit under any gating; else it rests on
-        // the winner, which must pass with no NaN distance around.  An object box that fails
-        // leaves no candidate (lit).  A face box that fails: pass 2, every candidate gated.
+        const bool any_unb = __ballot(lane_on && unb) != 0;
+        const float inf = __builtin_inff();
+        float cs0 = -inf, cs1 = inf, ct0 = -inf, ct1 = inf;
+        if (!any_unb) {
+            const bool on = lane_on;
+            cs0 = wave_reduce<true>(on ? ls : inf);
+            cs1 = wave_reduce<false>(on ? ls : -inf);
+            ct0 = wave_reduce<true>(on ? lt : inf);
+            ct1 = wave_reduce<false>(on ? lt : -inf);
+        }
+        // a candidate of the segment lies within |L - hit| of the light (or within near_r)
+        const float zl = (float)(lh + (double)vh->near_r) * (1.0f + 0x1p-20f);
+        view_sweep<PREFILTER, true>(ob.m, lds, vt, vn, ls, lt, unb, cs0, cs1, ct0, ct1, zl, ro, d, neg, lane_on, b, vis,
+                                    resolve, tmax);
+    } else {
+        // the light's fp32 table (SegPre): per lane d, |d|_inf and the distance along d
+        const float* lt = fa.ltab && li < fa.n_lights ? fa.ltab + (size_t)li * fa.ltab_n * kLtD : nullptr;
+        SegPre sp;
+        if (lt) sp = seg_pre(d, lh);
+        if (resident)
+            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, lds, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                                  !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
+        else
+            bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
+                                                  !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
+    }
+    if (gating) {
         uint32_t face = 0, p = 0;
         const bool retired = b.has && b.d < resolve;
         const bool far_lit = !retired && b.has && !b.any_nan && b.d > lh + 1e-4 + M;
         const bool need = lane_on && best_result(b, face, p) && !far_lit;
         const bool ok = box_gate(ob.box, o, d, need);  // tracer.go:32
         if (need && !ok) best_init(b);
-        if (pass2) break;
-        const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)(retired ? b.pos : p) * kBoxD, ro, d, ok);  // object.go:76
-        if (__ballot(ok && (!fok || (!retired && b.any_nan))) == 0) break;
-        pass2 = true;
+        if (!pass2) {
+            V3 o2 = o;  // (object-space origin made again here, not kept live through the sweep)
+            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+            const bool fok = box_gate(at_use(mesh_fbox(ob.m)) + (size_t)(retired ? b.pos : p) * kBoxD, sub(o2, pos), d, ok);  // object.go:76
+            redo = __ballot(ok && (!fok || (!retired && b.any_nan))) != 0;
+        }
     }
     if (b.has && b.d < resolve) return false;
     // the nearest candidate (not a NaN-distance first hit, which wins regardless) lies beyond
@@ -1232,8 +1299,21 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     if (!best_result(b, face, p)) return true;
     V3 world, normal;
     uint32_t mat;
-    winner(ob, p, sub(o, pos), d, scale(d, -1), world, normal, mat, false);
+    V3 o3 = o;
+    asm volatile("" : "+v"(o3.x), "+v"(o3.y), "+v"(o3.z));
+    winner(ob, p, sub(o3, pos), d, scale(d, -1), world, normal, mat, false);
     return lh < len(sub(world, hit));
+}
+// shadow_lit_single with its retry in place, for callers that hold per-lane chain state
+// (k_reflect, k_bounce with MIRT_BOUNCE_SHADE) rather than a work queue.
+template <bool PREFILTER, bool LT3 = true>
+__device__ __forceinline__ bool shadow_lit_single_settled(const FrameArgs& fa, const double* __restrict__ lds,
+                                                          bool resident, uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d,
+                                                          V3 lpos, uint32_t li, bool lane_on, Visits& vis) {
+    bool redo = false;
+    bool lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, false, redo);
+    if (redo) lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, true, redo);
+    return lit;
 }
 
 // A hit pixel's packed word: uint8(255 c) per channel (colour.go:59-61), valid = 1.
@@ -1489,11 +1569,13 @@ __device__ __forceinline__ uint32_t ring_take(uint32_t* ring, uint32_t c) {
     }
     return p;
 }
+//   pass2 / returns: trace_nearest's retry.  true = the block must run again with pass2 (its
+//   result rested on a face box that fails: nothing was written); false = done.
 template <bool REL, bool PREFILTER, bool BRUTE>
-__device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
+__device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
-                                              bool frustum = false, const float4* __restrict__ frect = nullptr,
+                                              bool pass2, bool frustum = false, const float4* __restrict__ frect = nullptr,
                                               const LocalChunks* lc = nullptr, uint32_t classified = 0,
                                               const ViewLeaf* vt = nullptr, uint32_t vn = 0,
                                               const FrustumArgs* vfr = nullptr, uint32_t blk = ~0u) {
@@ -1522,7 +1604,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
             if (out.rgbv) out.rgbv[oidx] = 0u;
         }
         pc.lap(2);
-        return;
+        return false;
     }
     const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
 
@@ -1547,14 +1629,16 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         crect = float4{fminf(s0, s1), fmaxf(s0, s1), fminf(t0, t1), fmaxf(t0, t1)};
     }
     pc.lap(0);
+    bool redo = false;
     Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d,
-                                                                         active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis, stk,
-                                                                         vt, vn, ls, lt, crect);
+                                                                         active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis,
+                                                                         pass2, redo, stk, vt, vn, ls, lt, crect);
     pc.lap(1);
     ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
     ws.nodes += vis.nodes;
     ws.leaves += vis.leaves;
     ws.overflow += vis.overflow;
+    if (redo) return true;  // wave-uniform: nothing written yet
 
     const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
     const bool is_hit = active && nh.ok;
@@ -1629,6 +1713,7 @@ __device__ __forceinline__ void primary_block(const FrameArgs& fa, const WorkArg
         }
     }
     pc.lap(2);
+    return false;
 }
 
 // ---------------------------------------------------------------- view tables (ViewLeaf)
@@ -1868,11 +1953,13 @@ __device__ __forceinline__ const ViewHead* view_lookup(const WorkArgs& wa, uint3
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
 // the wave that finishes the chunk's last light.  n_lights == 0: one pass that shades.
 //   vf: the chunk's frame within the launch (its view tables, k_trace), ~0u: none.
+//   pass2 / returns: shadow_lit_single's retry.  true = the item must run again with pass2
+//   (nothing was published: no lit bit, no count, no shading); false = done.
 template <bool PREFILTER, bool BRUTE, bool LT3 = true>
-__device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
+__device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
-                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws, uint32_t vf = ~0u,
-                                            const ViewCache* vc = nullptr, uint32_t lim = 64,
+                                            bool segment, size_t chunk, uint32_t l, WaveStats& ws, bool pass2,
+                                            uint32_t vf = ~0u, const ViewCache* vc = nullptr, uint32_t lim = 64,
                                             uint32_t* ring = nullptr, uint32_t rpos = ~0u) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
@@ -1903,10 +1990,26 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
             vh = view_lookup(wa, q, *vc);
             if (vh) vt = wa.views + (size_t)q * wa.view_leaves;
         }
-        is_lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, vt, wa.view_leaves,
-                                              vh);
+        bool redo = false;
+        is_lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, pass2, redo, vt,
+                                                   wa.view_leaves, vh);
+        if (redo) {  // wave-uniform; the first pass's visits still count
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
+            return true;
+        }
     } else {
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis);
+        bool redo = false;
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis, pass2, redo);
+        if (redo) {  // wave-uniform: the item runs again with pass2 (nothing published)
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            ws.overflow += vis.overflow;
+            return true;
+        }
         // tracer.go:64: lit iff !shaded || |L - hit| < |occluder - hit|
         is_lit = !r.ok || len(sub(lpos, hit)) < len(sub(r.hit, hit));
     }
@@ -1925,7 +2028,7 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
     uint32_t done = 0;
     if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
     done = __builtin_amdgcn_readfirstlane(done);
-    if (done != nl - 1) return;
+    if (done != nl - 1) return false;
     // Phong of the lane's hit (tracer.go:53-76) once its lit word is complete, and its outputs
     auto shade = [&](uint64_t& oidx) {
         const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
@@ -1966,12 +2069,13 @@ __device__ __forceinline__ void shadow_item(const FrameArgs& fa, const WorkArgs&
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) atomicOr(ring, 1u << rpos);
         if (active) store(oidx, col);
-        return;
+        return false;
     }
-    if (!active) return;
+    if (!active) return false;
     uint64_t oidx = 0;
     const RGB col = shade(oidx);
     store(oidx, col);
+    return false;
 }
 
 // ---------------------------------------------------------------- primary kernel
@@ -2020,14 +2124,19 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
         if (c0 == 0) clock.mark_staged();
         __syncthreads();
         uint32_t t = wave;
+        bool pass2 = false;
         while (t < nc) {
             const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
             const uint32_t b = blockIdx.x + (c0 + t) * G;
             ++taken;
-            primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
-                                                      use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b);
+            if (primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
+                                                          pass2, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b)) {
+                pass2 = true;  // the same block again, every candidate box-gated
+                continue;
+            }
+            pass2 = false;
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -2083,14 +2192,21 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
         // item rank is this wave's (static); with the queue on, items peers + ticket follow,
         // each ticket taken while the previous item is traced
         const bool dyn = (wa.dynamic & kDynShadow) && items > peers;
-        uint32_t k = sc.rank();
+        uint32_t k = sc.rank(), nxt = 0;
+        bool pass2 = false;  // the same item again, every candidate box-gated (shadow_item)
         while (k < items) {
-            const uint32_t nxt = dyn ? ticket_issue(qc) : 0;
-            ++taken;
+            if (!pass2) {
+                nxt = dyn ? ticket_issue(qc) : 0;
+                ++taken;
+            }
             const uint32_t l = k / nch, c = k - l * nch;
-            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
-                                          (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, ~0u, nullptr,
-                                          min(64u, nrec - c * 64));
+            if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+                                                              (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, pass2, ~0u,
+                                                              nullptr, min(64u, nrec - c * 64))) {
+                pass2 = true;
+                continue;
+            }
+            pass2 = false;
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
@@ -2265,6 +2381,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
         const uint32_t nfront = s_front, back0 = s_back, nq = nfront + (nc - back0);
         LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0, &s_ring, chunk_pos};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
+        bool pass2 = false;     // pend runs again with every candidate box-gated (shadow_item)
+        uint32_t ppend = kNone;  // a primary ticket held
+        bool ppass2 = false;     // ppend runs again with every candidate box-gated (primary_block)
         for (;;) {
             // 1. a shadow item of an allocated chunk
             const uint32_t avail = lds_ld(&s_chunks) * nl;
@@ -2286,15 +2405,22 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
                 const FrameRec& fr = frame_rec(frames, cf);
                 const uint32_t cp = __builtin_amdgcn_readfirstlane(chunk_pos[c]);
-                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64, l,
-                                              wsh, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring, cp);
+                if (shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64,
+                                                  l, wsh, pass2, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring,
+                                                  cp)) {
+                    pass2 = true;  // the same item again (pend kept), every candidate box-gated
+                    continue;
+                }
+                pass2 = false;
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
             }
-            // 2. a primary block
-            if (lds_ld(&s_prim) < nq) {
-                const uint32_t q = lds_inc(&s_prim);
+            // 2. a primary block (ppend: a ticket held for a block that runs again with pass2)
+            if (ppend == kNone && lds_ld(&s_prim) < nq) ppend = lds_inc(&s_prim);
+            if (ppend != kNone) {
+                const uint32_t q = ppend;
+                if (q >= nq) ppend = kNone;
                 if (q < nq) {
                     const uint32_t t = q < nfront ? q : q - nfront + back0;
                     const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
@@ -2313,10 +2439,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                     if (VIEWS && RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     const uint64_t cost0 = wa.block_cost ? __builtin_amdgcn_s_memtime() : 0;
-                    primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
-                                                           use_frustum, frect[f], &lc,
-                                                           __builtin_amdgcn_readfirstlane(bq_cull[t]), vt, wa.view_leaves,
-                                                           &fr.fr);
+                    if (primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
+                                                               ppass2, use_frustum, frect[f], &lc,
+                                                               __builtin_amdgcn_readfirstlane(bq_cull[t]), vt,
+                                                               wa.view_leaves, &fr.fr)) {
+                        ppass2 = true;  // the same block again (ppend kept), every candidate box-gated
+                        continue;
+                    }
+                    ppass2 = false;
+                    ppend = kNone;
                     if (wa.block_cost && (threadIdx.x & 63) == 0) {  // this trace's time, for the slot's next frame
                         const uint64_t dc = (__builtin_amdgcn_s_memtime() - cost0) >> 6;
                         wa.block_cost[bq_bl[t]] = (uint16_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));
@@ -2404,7 +2535,7 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
                 const V3 R = sub(D, scale(N, 2 * dot(D, N)));
                 const V3 o = add(hit, scale(R, 0.0001));
                 Visits vis{0, 0, 0, 0};
-                const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, on, true, vis);
+                const Nearest r = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, on, true, vis);
                 refl_rays += __popcll(__ballot(on));
                 ws.tests += (cnt_t)vis.tests * __popcll(__ballot(on));
                 ws.nodes += vis.nodes;
@@ -2426,9 +2557,9 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
                     Visits sv{0, 0, 0, 0};
                     bool is_lit;
                     if (segment) {
-                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, on, sv);
+                        is_lit = shadow_lit_single_settled<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, on, sv);
                     } else {
-                        const Nearest sr = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, on, false, sv);
+                        const Nearest sr = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, on, false, sv);
                         is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
                     }
                     lit |= (uint32_t)is_lit << l;
@@ -2525,7 +2656,8 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     const uint32_t cp = (*lo32((cnt_t*)&ba.in_cnt[cnt_hits(0)]) + 63) / 64;
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
-        for (uint32_t k = sc.rank(); k < nch; k += sc.peers()) {
+        bool pass2 = false;  // the same chunk again, every candidate box-gated (trace_nearest)
+        for (uint32_t k = sc.rank(); k < nch;) {
             const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
             const bool inb = k * 64 + lane < n;
             const HitRec rec = ba.in[inb ? slot : (size_t)q * wa.hit_cap + (size_t)k * 64];
@@ -2540,7 +2672,16 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
             const V3 R = sub(D, scale(N, 2 * dot(D, N)));
             const V3 o = add(hit, scale(R, 0.0001));
             Visits vis{0, 0, 0, 0};
-            const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, active, true, vis);
+            bool redo = false;
+            const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, active, true, vis, pass2, redo);
+            if (redo) {  // wave-uniform: nothing written yet
+                ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+                ws.nodes += vis.nodes;
+                ws.leaves += vis.leaves;
+                pass2 = true;
+                continue;
+            }
+            pass2 = false;
             rays += __popcll(__ballot(active));
             ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
             ws.nodes += vis.nodes;
@@ -2565,9 +2706,9 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
                     Visits sv{0, 0, 0, 0};
                     bool is_lit;
                     if (segment) {
-                        is_lit = shadow_lit_single<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, got, sv);
+                        is_lit = shadow_lit_single_settled<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, got, sv);
                     } else {
-                        const Nearest sr = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, got, false, sv);
+                        const Nearest sr = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, got, false, sv);
                         is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
                     }
                     lit |= (uint32_t)is_lit << l;
@@ -2606,6 +2747,7 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
                 ba.src[j] = (uint32_t)(((size_t)q * wa.hit_cap + (size_t)k * 64) / 64 + 1) << 7 | (uint32_t)__popcll(m);
                 if (m) atomicAdd(&ba.gcnt[j / kPackGroup], (uint32_t)__popcll(m));
             }
+            k += sc.peers();
         }
     }
     WaveStats extra{rays, (uint32_t)shadow_rays, 0, 0, 0};  // per wave: well below 2^32
@@ -2790,7 +2932,7 @@ MIRT_TRACE_KERNEL void k_rays(const FrameArgs fa, RayIO io) {
             d = vload(io.dir + 3 * item);
         }
         Visits vis{0, 0, 0, 0};
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, true, vis);
+        Nearest r = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, d, active, true, vis);
         if (active) {
             io.ok[item] = r.ok ? 1 : 0;
             vstore(io.hit + 3 * item, r.ok ? r.hit : V3{0, 0, 0});

@@ -680,12 +680,12 @@ float* lt_reap(mirt_ctx* c, size_t want) {
         }
         for (hipEvent_t e : t.evs) c->lt_events.push_back(e);
         if (!got && want && t.bytes == want) {
-            got = t.d;
+            got = t.d;  // stays allocated (and counted in ltab_bytes) for the next table
             ++c->lt_stat[4];
         } else {
             (void)hipFree(t.d);
+            c->ltab_bytes -= t.bytes;
         }
-        c->ltab_bytes -= t.bytes;
         c->lt_dead[i] = c->lt_dead.back();
         c->lt_dead.pop_back();
     }
@@ -734,8 +734,13 @@ const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) 
     if (n == 0) return nullptr;
     const size_t bytes = (size_t)nl * n * kLtD * sizeof(float);
     float* buf = lt_reap(c, bytes);
-    // make room: least recently used first, never a table of the last kLtPinUses calls
+    // make room: least recently used first, never a table of the last kLtPinUses calls, and
+    // no more once retired tables still being read would make the room (their buffers come
+    // back to a later frame; this one traces without a table meanwhile)
     while (!buf && c->ltab_bytes + bytes > c->lt_cap) {
+        size_t retiring = 0;
+        for (const auto& t : c->lt_dead) retiring += t.bytes;
+        if (retiring >= bytes) break;
         size_t best = c->ltabs.size();
         for (size_t i = 0; i < c->ltabs.size(); ++i)
             if (now - c->ltabs[i]->last_use > kLtPinUses &&

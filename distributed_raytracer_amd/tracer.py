@@ -137,6 +137,8 @@ class Context:
 
     def light_cache_stats(self) -> dict:
         """mirt_light_cache_stats: the light-table cache's counters (mirt.h)."""
+        if not hasattr(L.lib(), "mirt_light_cache_stats"):
+            return {}  # an older build under A/B (MIRT_LIB)
         out = np.zeros(8, np.uint64)
         L.check(L.lib().mirt_light_cache_stats(self.handle, out.ctypes.data))
         return dict(zip(("builds", "hits", "evictions", "no_room", "reused_buffers", "tables", "bytes", "cap"),
