@@ -2651,9 +2651,9 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     WaveStats ws{0, 0, 0, 0, 0};
     cnt_t rays = 0, shadow_rays = 0;
     const uint32_t lv = ba.level;
-    // chunks per region of the input (k_pack fills regions in order, each but the last with
-    // the same number of chunks): input chunk (q, k) is source chunk q * cp + k of k_pack
-    const uint32_t cp = (*lo32((cnt_t*)&ba.in_cnt[cnt_hits(0)]) + 63) / 64;
+    // chunks per region of the input, as k_pack published it (high word of its region counts):
+    // input chunk (q, k) is source chunk q * cp + k of k_pack
+    const uint32_t cp = (uint32_t)(ba.in_cnt[cnt_hits(0)] >> 32);
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
         bool pass2 = false;  // the same chunk again, every candidate box-gated (trace_nearest)
@@ -2839,8 +2839,10 @@ __global__ __launch_bounds__(kPackWG) void k_pack(const WorkArgs wa, const PackA
     }
     const uint32_t per = ((tot + 63) / 64 + kQShards - 1) / kQShards * 64;  // records per region
     if (blockIdx.x == 0 && tid < (uint32_t)kQShards) {
+        // the region's records (low word) and every region's capacity in chunks (high word: the
+        // chunk stride k_bounce maps input chunks to source chunks with)
         const uint32_t a = tid * per;
-        *lo32(&pa.out_cnt[cnt_hits(tid)]) = tot > a ? min(per, tot - a) : 0u;
+        pa.out_cnt[cnt_hits(tid)] = (cnt_t)(tot > a ? min(per, tot - a) : 0u) | ((cnt_t)(per / 64) << 32);
     }
     for (uint32_t t = wave; t < j1 - j0; t += kPackWG / 64) pack_chunk(wa, pa, s_src[t], pre + s_off[t], per, lane);
 }

@@ -911,12 +911,15 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     // k_trace: workgroup w's hit region holds the kHitRing ring positions and one chunk per
     // block it owns (a chunk that finds the ring full)
     wa.wg_cap = (uint32_t)((kHitRing + (total + pgrid - 1) / pgrid) * 64);
-    // sized for any grid up to kWgPerCu per CU (G (R + ceil(total / G)) <= total + G (R + 1)): a
-    // launch whose grid differs from the slot's last one (MIRT_ADAPTIVE_GRID) never regrows the
-    // buffers (hipFree synchronises the device)
+    // k_trace (one launch): sized for any grid up to kWgPerCu per CU (G (R + ceil(total / G)) <=
+    // total + G (R + 1)): a launch whose grid differs from the slot's last one
+    // (MIRT_ADAPTIVE_GRID) never regrows the buffers (hipFree synchronises the device).  The split
+    // kernels and the reflection levels use the kQShards regions only (no ring), which also size
+    // every bounce-wave buffer below.
     const uint64_t hit_slots =
-        std::max<uint64_t>({(uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap,
-                            (total + (uint64_t)kWgPerCu * c->cus * (kHitRing + 1)) * 64});
+        one_launch ? std::max<uint64_t>({(uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap,
+                                         (total + (uint64_t)kWgPerCu * c->cus * (kHitRing + 1)) * 64})
+                   : (uint64_t)kQShards * wa.hit_cap;
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;

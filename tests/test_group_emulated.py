@@ -201,6 +201,33 @@ def test_host_output_frames(ctx, views, tile, emulate, wait, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [2, 4])
+def test_host_output_runahead_reserved_copy_cus(ctx, views, inflight, monkeypatch):
+    """Host run-ahead 4 (MIRT_RUNAHEAD) with the host copies on a stream of reserved CUs
+    (MIRT_D2H_CUS): an untiled group of one-frame batches, where batch nb - FB's copy on that
+    stream is the only guard on a framebuffer's reuse (mirt.cpp group_flush).  Three passes over
+    the moving, emptying and refilling hit rectangles: every host frame equals the oracle."""
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_RUNAHEAD", "4")
+    monkeypatch.setenv("MIRT_D2H_CUS", "8")
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=inflight, batch=1, host_output=True)
+    try:
+        prev = None
+        for k, name in enumerate(ORDER * 3):
+            idx = g.render(views[name][0])
+            if prev is not None:
+                rgb8, valid = g.host_frame(prev[0])
+                _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+            prev = (idx, name)
+        rgb8, valid = g.host_frame(prev[0])
+        _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+        g.wait()
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("emulate_after_host_output", [False, True])
 def test_library_owned_planes_host_output(ctx, views, emulate_after_host_output):
     """fbs == NULL on a tiled root (the group allocates its own rgb8 + valid planes, as the
