@@ -234,8 +234,8 @@ def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
     (i) the oracle's faithful variant (rtreego-style R-tree, 1 thread, fp64,
         worker/sequential's serial i/j loop) over one full frame — the reported value;
     (ii) the same code on all the host cores this process is allotted (the box's share for
-        one GPU, 16; column-interleaved threads) — os.cpu_count() (`nproc`) shows the whole,
-        shared machine and is reported, not used;
+        one GPU, 16; column-interleaved threads), and again at os.cpu_count() (`nproc`)
+        threads, the whole shared machine, as SURVEY.md §8(d) words it (`threads_<nproc>`);
     (iii) brute force (every triangle, no culling), 1 thread, on every 64th column of the
         frame (a bounded sample), scaled to the full frame."""
     from oracle.oracle import Oracle
@@ -246,7 +246,10 @@ def cpu_baseline(scene_path: str, W: int, H: int) -> dict:
     # the box allots HOST_CORES CPUs per GPU; os.cpu_count() shows the whole, shared machine,
     # so the all-cores variant runs on the allotted cores (sched_getaffinity if smaller)
     allc = max(1, min(host_threads(), HOST_CORES))
-    for threads in sorted({1, allc}):
+    # ... and at `nproc` threads as SURVEY.md §8(d) / BASELINE.md §2 word it (on the shared box
+    # these threads contend with other tenants for the machine's cores: an upper bound, not a share)
+    nproc = max(1, os.cpu_count() or 1)
+    for threads in sorted({1, allc, nproc}):
         t0 = time.perf_counter()
         r = orc.frame(W, H, nthreads=threads)
         dt = time.perf_counter() - t0

@@ -1077,7 +1077,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
     best.hit = best.normal = V3{0, 0, 0};
     double bestcd = 0;
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
-    const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
+    const bool gating = MIRT_BOX_GATE && !(fa.flags & MIRT_OPT_NO_BOX_GATE);
     bool again = false;
     for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
         const DevObject& ob = fa.obj[oi];
@@ -1149,6 +1149,10 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
             }
         }
     }
+    if (MIRT_BOX_GATE == 2) {  // measurement build: gates evaluated, no second pass
+        vis.overflow += __ballot(again) != 0;
+        again = false;
+    }
     redo = __ballot(again) != 0;
     return best;
 }
@@ -1205,7 +1209,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     const double M = 0x1p-36 * (1.0 + lh + mag);
     const double resolve = lh - 1e-4 - M;
     const float tmax = (float)(lh + 1e-4 + M) * (1.0f + 0x1p-20f);
-    const bool gating = !(fa.flags & MIRT_OPT_NO_BOX_GATE);
+    const bool gating = MIRT_BOX_GATE && !(fa.flags & MIRT_OPT_NO_BOX_GATE);
     redo = false;
     Best b;
     best_init(b);
@@ -1289,6 +1293,10 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
             asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
             const bool fok = box_gate(at_use(mesh_fbox(ob.m)) + (size_t)(retired ? b.pos : p) * kBoxD, sub(o2, pos), d, ok);  // object.go:76
             redo = __ballot(ok && (!fok || (!retired && b.any_nan))) != 0;
+            if (MIRT_BOX_GATE == 2) {  // measurement build: gates evaluated, no second pass
+                vis.overflow += redo;
+                redo = false;
+            }
         }
     }
     if (b.has && b.d < resolve) return false;

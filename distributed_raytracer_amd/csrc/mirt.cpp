@@ -679,7 +679,9 @@ float* lt_reap(mirt_ctx* c, size_t want) {
             continue;
         }
         for (hipEvent_t e : t.evs) c->lt_events.push_back(e);
-        if (!got && want && t.bytes == want) {
+        // a buffer is kept for reuse only while the cache is within its cap (a cap lowered by
+        // mirt_set_light_cache shrinks the cache as its tables die, instead of recycling them)
+        if (!got && want && t.bytes == want && c->ltab_bytes <= c->lt_cap) {
             got = t.d;  // stays allocated (and counted in ltab_bytes) for the next table
             ++c->lt_stat[4];
         } else {
@@ -1402,6 +1404,19 @@ int mirt_set_light_cache(mirt_ctx* c, uint64_t max_bytes) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
     std::lock_guard<std::mutex> g(c->lt_mu);
     c->lt_cap = (size_t)max_bytes;
+    // shrink to the new cap now: least recently used first, never a table of the last
+    // kLtPinUses calls; retired buffers are freed once their readers are done (lt_reap)
+    (void)lt_reap(c, 0);
+    while (c->ltab_bytes > c->lt_cap) {
+        size_t best = c->ltabs.size();
+        for (size_t i = 0; i < c->ltabs.size(); ++i)
+            if (c->lt_clock - c->ltabs[i]->last_use > kLtPinUses &&
+                (best == c->ltabs.size() || c->ltabs[i]->last_use < c->ltabs[best]->last_use))
+                best = i;
+        if (best == c->ltabs.size()) break;
+        lt_evict(c, best);
+        (void)lt_reap(c, 0);
+    }
     return MIRT_OK;
 }
 
