@@ -208,35 +208,38 @@ __device__ __forceinline__ void stage_tris(double* __restrict__ s, const double*
 // the minimum distance — except that a NaN distance on the lowest-indexed hit wins (no
 // later `<` beats NaN) and a NaN anywhere else never wins.  `consider` computes exactly
 // that in ANY visiting order, so culling/reordering cannot change the result.
+// (the flags are 0/1 words, not bools: a bool that lives across the test's divergent stages
+// is a lane mask the compiler merges with three scalar instructions at every join, a word in a
+// VGPR is merged by the exec mask for free)
 struct Best {
-    bool has;          // any non-NaN hit
+    uint32_t has;      // any non-NaN hit
     double d;          // its minimum distance
     uint32_t face;     // lowest original face index at that distance
     uint32_t pos;      // its position in the BVH-ordered arrays
     uint32_t first;    // lowest original face index of any hit (0xffffffff: none)
     uint32_t first_pos;
-    bool first_nan;    // that hit's distance is NaN
-    bool any_nan;      // some hit's distance is NaN (box_settle: the winner alone does not decide)
+    uint32_t first_nan;  // that hit's distance is NaN
+    uint32_t any_nan;    // some hit's distance is NaN (box_settle: the winner alone does not decide)
 };
 __device__ __forceinline__ void best_init(Best& b) {
-    b.has = false;
+    b.has = 0;
     b.d = 0;
     b.face = b.pos = 0;
     b.first = 0xffffffffu;
     b.first_pos = 0;
-    b.first_nan = false;
-    b.any_nan = false;
+    b.first_nan = 0;
+    b.any_nan = 0;
 }
 __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
     const bool isnan_d = dist != dist;
-    b.any_nan |= isnan_d;
+    b.any_nan |= isnan_d ? 1u : 0u;
     if (face < b.first) {
         b.first = face;
         b.first_pos = pos;
-        b.first_nan = isnan_d;
+        b.first_nan = isnan_d ? 1u : 0u;
     }
     if (!isnan_d && (!b.has || dist < b.d || (dist == b.d && face < b.face))) {
-        b.has = true;
+        b.has = 1;
         b.d = dist;
         b.face = face;
         b.pos = pos;
@@ -267,18 +270,32 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
 // d fails every plane both ways.)  The planes are pure tests, so any order gives the
 // reference's boolean.
 __device__ __forceinline__ double v3c(V3 v, int a) { return a == 0 ? v.x : a == 1 ? v.y : v.z; }
-// plane `hi` (MaxCorner, normal +e_a) or not (MinCorner, -e_a) of axis a (box.go:33-60)
-__device__ __forceinline__ bool box_plane(const double* bx, V3 o, V3 d, int a, bool hi) {
-    const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
-    const double da = v3c(d, a);
-    const double ds = ((hi ? bx[3 + a] : bx[a]) - v3c(o, a)) / da;  // box.go:42
-    const double ib = v3c(o, b) + ds * v3c(d, b), ic = v3c(o, c) + ds * v3c(d, c);  // box.go:47
-    return da != 0.0 && ds >= 0.0 && bx[b] <= ib && ib <= bx[3 + b] && bx[c] <= ic && ic <= bx[3 + c];
+// A box's corners in registers (loaded once per test: the object's from the kernel arguments,
+// a face's from the mesh; a pointer that could be either would take the kernel argument's
+// address, which copies the arguments to scratch).  Indexed with constants only (a run-time
+// index would move the array to LDS or scratch).
+struct Box6 {
+    double v[kBoxD];
+};
+__device__ __forceinline__ Box6 box_load(const double* p) {
+    Box6 b;
+#pragma unroll
+    for (int k = 0; k < kBoxD; ++k) b.v[k] = p[k];
+    return b;
 }
-// The far plane of axis A (+e_A for d_A > 0, -e_A for d_A < 0), A known at compile time.
+// plane `HI` (MaxCorner, normal +e_A) or not (MinCorner, -e_A) of axis A (box.go:33-60)
 template <int A>
-__device__ __forceinline__ bool box_far(const double* bx, V3 o, V3 d) {
-    return box_plane(bx, o, d, A, (A == 0 ? d.x : A == 1 ? d.y : d.z) > 0.0);
+__device__ __forceinline__ bool box_plane(const Box6& bx, V3 o, V3 d, bool hi) {
+    constexpr int B = A == 0 ? 1 : 0, C = A == 2 ? 1 : 2;
+    const double da = v3c(d, A);
+    const double ds = ((hi ? bx.v[3 + A] : bx.v[A]) - v3c(o, A)) / da;  // box.go:42
+    const double ib = v3c(o, B) + ds * v3c(d, B), ic = v3c(o, C) + ds * v3c(d, C);  // box.go:47
+    return da != 0.0 && ds >= 0.0 && bx.v[B] <= ib && ib <= bx.v[3 + B] && bx.v[C] <= ic && ic <= bx.v[3 + C];
+}
+// The far (FAR) or near plane of axis A: +e_A for d_A > 0 is the far one, -e_A for d_A < 0.
+template <int A, bool FAR>
+__device__ __forceinline__ bool box_side(const Box6& bx, V3 o, V3 d) {
+    return box_plane<A>(bx, o, d, (v3c(d, A) > 0.0) == FAR);
 }
 // A pointer the compiler cannot prove loop-invariant: loads through it stay at their use
 // instead of being hoisted to the kernel's start and held in SGPRs across the work loop.
@@ -288,36 +305,48 @@ __device__ __forceinline__ const T* at_use(const T* p) {
     return p;
 }
 // Box.Intersect for the lanes `on` (false on the others).  A ray that meets a box leaves it
-// through the far plane of some axis (+e_a for d_a > 0, -e_a for d_a < 0); the wave first
+// through the far plane of some axis (+e_a for d_a > 0, -e_a for d_a < 0).  The wave first
 // tries the far plane of the axis its first lane's direction leans on most (a wave-uniform
-// axis: one branch to straight-line code), and only the lanes that plane does not prove true
-// go through the six planes, one at a time (a short loop: this is the rare path).  Same
-// boolean as the reference's.
-__device__ __forceinline__ bool box_gate(const double* bx, V3 o, V3 d, bool on) {
+// axis: one branch to straight-line code), then the other two far planes, each only while a
+// lane is unproven, and last the three near planes (a ray through an edge, or one that misses
+// the box: the rare path).  Same boolean as the reference's: every plane is tried for every
+// lane the earlier planes did not prove.  (Trying the near and far planes in a fixed order
+// after the lean axis cost 3-10 far-plane evaluations per wave on the driver's frame, this
+// order 1.3-3: tests/gate_order_model.py.)
+__device__ __forceinline__ bool box_gate(const Box6& bx, V3 o, V3 d, bool on) {
     if (__ballot(on) == 0) return false;
     const double ax = __builtin_fabs(d.x), ay = __builtin_fabs(d.y), az = __builtin_fabs(d.z);
     const int lean = (ax >= ay && ax >= az) ? 0 : ay >= az ? 1 : 2;
     const int a = __builtin_amdgcn_readfirstlane(lean);
     bool r = false;
-    if (on) r = a == 0 ? box_far<0>(bx, o, d) : a == 1 ? box_far<1>(bx, o, d) : box_far<2>(bx, o, d);
-    if (__ballot(on && !r) == 0) return r;
-#pragma unroll 1
-    for (int q = 0; q < 6; ++q) {
-        const bool left = on && !r;
-        if (__ballot(left) == 0) break;
-        if (left) r = box_plane(bx, o, d, q >> 1, (q & 1) == 0);
+    diag(24);  // gates evaluated (wave-level)
+    if (on) r = a == 0 ? box_side<0, true>(bx, o, d) : a == 1 ? box_side<1, true>(bx, o, d) : box_side<2, true>(bx, o, d);
+    // the other far planes (A is a constant once unrolled; A == a was tried)
+#pragma unroll
+    for (int A = 0; A < 3; ++A) {
+        if (A == a || __ballot(on && !r) == 0) continue;
+        diag(25);  // further far planes evaluated
+        if (on && !r) r = A == 0 ? box_side<0, true>(bx, o, d) : A == 1 ? box_side<1, true>(bx, o, d) : box_side<2, true>(bx, o, d);
     }
+#pragma unroll
+    for (int A = 0; A < 3; ++A) {
+        if (__ballot(on && !r) == 0) break;
+        diag(26);  // near planes evaluated
+        if (on && !r) r = A == 0 ? box_side<0, false>(bx, o, d) : A == 1 ? box_side<1, false>(bx, o, d) : box_side<2, false>(bx, o, d);
+    }
+    if (__ballot(on && !r) != 0) diag(27);  // waves with a lane whose box fails
     return r;
 }
-// The same boolean with the least code: the six planes one at a time (the second pass's
-// per-candidate test, inside the sweep, where registers are scarce).
-__device__ __forceinline__ bool box_gate_small(const double* bx, V3 o, V3 d, bool on) {
+// The same boolean in a fixed order (the second pass's per-candidate test, inside the sweep):
+// the three far planes, then the three near ones, each while a lane is unproven.
+__device__ __forceinline__ bool box_gate_small(const Box6& bx, V3 o, V3 d, bool on) {
     bool r = false;
-#pragma unroll 1
+#pragma unroll
     for (int q = 0; q < 6; ++q) {
-        const bool left = on && !r;
-        if (__ballot(left) == 0) break;
-        if (left) r = box_plane(bx, o, d, q >> 1, (q & 1) == 0);
+        if (__ballot(on && !r) == 0) break;
+        if (on && !r)
+            r = q == 0 ? box_side<0, true>(bx, o, d) : q == 1 ? box_side<1, true>(bx, o, d) : q == 2 ? box_side<2, true>(bx, o, d)
+              : q == 3 ? box_side<0, false>(bx, o, d) : q == 4 ? box_side<1, false>(bx, o, d) : box_side<2, false>(bx, o, d);
     }
     return r;
 }
@@ -391,7 +420,7 @@ __device__ __forceinline__ void test_range(SrcPtr src, const uint32_t* __restric
         // k is wave-uniform: a scalar load (lgkmcnt), issued ahead of the test
         const uint32_t fk = ((const __attribute__((address_space(4))) uint32_t*)fidx)[k];
         bool acc = maybe && mt_test<PREFILTER, DG, TPRE>(p1or, e1, e2, neg, tt);
-        if (GATE) acc = box_gate_small(fbox + (size_t)k * kBoxD, ro, d, acc);
+        if (GATE) acc = box_gate_small(box_load(fbox + (size_t)k * kBoxD), ro, d, acc);
         if (acc) {
             V3 ip = add(ro, scale(d, tt));  // triangle.go:69
             consider(b, len(sub(ro, ip)), fk, k);  // object.go:97
@@ -1127,11 +1156,23 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
         uint32_t face = 0, pos = 0;
         bool got = lane_on && best_result(b, face, pos);
         if (gating) {
-            got = box_gate(ob.box, o, d, got);  // tracer.go:32: the object's box
-            if (!pass2) {
-                const bool fok = box_gate(mesh_fbox(ob.m) + (size_t)pos * kBoxD, ro, d, got);  // object.go:76
-                again = again || (got && (!fok || b.any_nan));
+            // the object's box (tracer.go:32), then, in a first pass, the winner's face box
+            // (object.go:76): one box_gate serves both (a loop, so its code is not repeated)
+            bool fok = true;
+#pragma unroll 1
+            for (int k = 0; k < (pass2 ? 1 : 2); ++k) {
+                Box6 bx;
+                if (k == 0)
+                    bx = Box6{{ob.box[0], ob.box[1], ob.box[2], ob.box[3], ob.box[4], ob.box[5]}};
+                else
+                    bx = box_load(mesh_fbox(ob.m) + (size_t)pos * kBoxD);
+                const bool r = box_gate(bx, k == 0 ? o : ro, d, got);
+                if (k == 0)
+                    got = r;
+                else
+                    fok = r;
             }
+            if (!pass2) again = again || (got && (!fok || b.any_nan));
         }
         if (got) {
             V3 world, normal{0, 0, 0};
@@ -1154,6 +1195,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
         again = false;
     }
     redo = __ballot(again) != 0;
+    if (redo) diag(28);  // nearest queries run again (pass 2)
     return best;
 }
 // trace_nearest with its second pass in place, for callers without a work loop to retry in
@@ -1286,13 +1328,20 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         const bool retired = b.has && b.d < resolve;
         const bool far_lit = !retired && b.has && !b.any_nan && b.d > lh + 1e-4 + M;
         const bool need = lane_on && best_result(b, face, p) && !far_lit;
-        const bool ok = box_gate(ob.box, o, d, need);  // tracer.go:32
-        if (need && !ok) best_init(b);
+        // the object's box (tracer.go:32), then, in a first pass, the face box the decision
+        // rests on (object.go:76)
+        const uint32_t fpos = retired ? b.pos : p;
+        const bool ok = box_gate(Box6{{ob.box[0], ob.box[1], ob.box[2], ob.box[3], ob.box[4], ob.box[5]}}, o, d, need);
+        bool fok = true;
         if (!pass2) {
             V3 o2 = o;  // (object-space origin made again here, not kept live through the sweep)
             asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-            const bool fok = box_gate(at_use(mesh_fbox(ob.m)) + (size_t)(retired ? b.pos : p) * kBoxD, sub(o2, pos), d, ok);  // object.go:76
+            fok = box_gate(box_load(at_use(mesh_fbox(ob.m)) + (size_t)fpos * kBoxD), sub(o2, pos), d, ok);
+        }
+        if (need && !ok) best_init(b);
+        if (!pass2) {
             redo = __ballot(ok && (!fok || (!retired && b.any_nan))) != 0;
+            if (redo) diag(29);  // segment queries run again (pass 2)
             if (MIRT_BOX_GATE == 2) {  // measurement build: gates evaluated, no second pass
                 vis.overflow += redo;
                 redo = false;
@@ -3032,7 +3081,7 @@ __global__ __launch_bounds__(256) void k_debug_fp64(int op, uint32_t n, const do
     double r;
     if (op == 4) {  // box.go:29-68 as the kernels evaluate it: ray i = a[6i..], box i = b[6i..]
         const double* ray = a + 6 * (size_t)i;
-        out[i] = box_gate(b + 6 * (size_t)i, V3{ray[0], ray[1], ray[2]}, V3{ray[3], ray[4], ray[5]}, true) ? 1.0 : 0.0;
+        out[i] = box_gate(box_load(b + 6 * (size_t)i), V3{ray[0], ray[1], ray[2]}, V3{ray[3], ray[4], ray[5]}, true) ? 1.0 : 0.0;
         return;
     }
     switch (op) {

@@ -34,6 +34,8 @@ def main():
     print("k_trace: ready-wait spins", c[17], " idle spins", c[18], " shadow items", c[19], " primary blocks", c[20],
           " culled blocks", c[21])
     print("shadow light-table classifications", c[22], " skipped by the wave", c[22] - c[8])
+    print("box gates", c[24], " further far planes", c[25], " near planes", c[26], " waves with a failing box", c[27],
+          " nearest redo", c[28], " segment redo", c[29])
     g.close()
 
 
