@@ -82,7 +82,8 @@
 #endif
 // The reference's face/object Box.Intersect gate compiled in (1) or out (0:
 // brute-force semantics, as MIRT_OPT_NO_BOX_GATE at run time; measures the gate's cost; 2: the
-// gates evaluated but a failure only counted (overflow statistic), no second pass: measurement).
+// gates evaluated but a failure only counted (overflow statistic), no second pass; 3: every box
+// passes without a test, the rest kept; 4: no NaN tracking in Best: measurement builds).
 #ifndef MIRT_BOX_GATE
 #define MIRT_BOX_GATE 1
 #endif

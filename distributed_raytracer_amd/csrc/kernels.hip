@@ -232,7 +232,7 @@ __device__ __forceinline__ void best_init(Best& b) {
 }
 __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
     const bool isnan_d = dist != dist;
-    b.any_nan |= isnan_d ? 1u : 0u;
+    if (MIRT_BOX_GATE != 4) b.any_nan |= isnan_d ? 1u : 0u;  // (4: measurement build without it)
     if (face < b.first) {
         b.first = face;
         b.first_pos = pos;
@@ -314,6 +314,7 @@ __device__ __forceinline__ const T* at_use(const T* p) {
 // after the lean axis cost 3-10 far-plane evaluations per wave on the driver's frame, this
 // order 1.3-3: tests/gate_order_model.py.)
 __device__ __forceinline__ bool box_gate(const Box6& bx, V3 o, V3 d, bool on) {
+    if (MIRT_BOX_GATE == 3) return on;  // measurement build: every box passes (the structure kept)
     if (__ballot(on) == 0) return false;
     const double ax = __builtin_fabs(d.x), ay = __builtin_fabs(d.y), az = __builtin_fabs(d.z);
     const int lean = (ax >= ay && ax >= az) ? 0 : ay >= az ? 1 : 2;
@@ -537,6 +538,11 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], in
 // (DEEP: two words, 128 entries; else one word, 64 entries, for trees of depth <=
 // kBvhShallowDepth).  Push and pop are v_writelane / v_readlane with the SGPR stack pointer:
 // no memory traffic and no LDS latency on the node-to-node dependency chain.
+// A 64-bit value every lane holds the same of, in SGPRs (no instruction where it is there already)
+__device__ __forceinline__ uint64_t u64_uniform(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+}
 template <bool DEEP>
 struct WaveStack {
     int a = 0, b = 0;
@@ -556,6 +562,10 @@ struct WaveStack {
     // s_and_b64 sets SCC exactly then and s_addc_u32 adds it.
     __device__ __forceinline__ void push_if(uint32_t ref, uint64_t m, uint64_t live) {
         put(ref);
+        // (scalar already in the kernels; an out-of-line second pass needs them said so)
+        m = u64_uniform(m);
+        live = u64_uniform(live);
+        sp = __builtin_amdgcn_readfirstlane(sp);
         uint64_t t;
         asm volatile("s_and_b64 %1, %2, %3\n\ts_addc_u32 %0, %0, 0" : "+s"(sp), "=&s"(t) : "s"(m), "s"(live) : "scc");
     }
@@ -1094,11 +1104,13 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   candidate is gated before it counts (an LDS-resident mesh swept whole, an HBM mesh through
 //   its BVH).  The retry lives in the callers' work loops: a loop around the sweep here cost
 //   ~5% of the frame (VALU and SALU of the restructured sweep, tools/ab_valu.sh).
+//   obj_sure (wave-uniform): the object's box is known to pass for every lane (a primary block
+//   inside the object-box certificate, block_obj_cert), so its gate is skipped.
 //   MIRT_OPT_NO_BOX_GATE: no boxes (brute-force semantics).
 template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
 __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
                                  bool lane_on, bool want_normal, Visits& vis, bool pass2, bool& redo,
-                                 uint32_t* __restrict__ stk = nullptr, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
+                                 bool obj_sure = false, uint32_t* __restrict__ stk = nullptr, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
                                  float ls = 0.0f, float lt = 0.0f, float4 crect = float4{0.0f, 0.0f, 0.0f, 0.0f}) {
     Nearest best;
     best.ok = false;
@@ -1159,8 +1171,9 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
             // the object's box (tracer.go:32), then, in a first pass, the winner's face box
             // (object.go:76): one box_gate serves both (a loop, so its code is not repeated)
             bool fok = true;
+            if (obj_sure) diag(30);  // object gates the block certificate skips
 #pragma unroll 1
-            for (int k = 0; k < (pass2 ? 1 : 2); ++k) {
+            for (int k = obj_sure ? 1 : 0; k < (pass2 ? 1 : 2); ++k) {  // obj_sure: the block's certificate
                 Box6 bx;
                 if (k == 0)
                     bx = Box6{{ob.box[0], ob.box[1], ob.box[2], ob.box[3], ob.box[4], ob.box[5]}};
@@ -1589,6 +1602,26 @@ __device__ __forceinline__ bool block_may_meet(const FrustumArgs& fr, const floa
     return meet;
 }
 
+// The object-box certificate (FrameRec::ocert, mirt.cpp object_cert): true iff the four
+// corner directions of the block's (s, t) range lie inside one certificate quad, so every ray
+// of the block passes the object's Box.Intersect (the quad is convex; its margin covers the
+// difference between the affine (s, t) of a pixel here and the kernel's pixelToPoint).  One
+// thread per block, at staging.
+__device__ __forceinline__ bool block_obj_cert(const FrameRec& rec, uint32_t px, uint32_t py, uint32_t vw, uint32_t vh) {
+    const FrustumArgs& fr = rec.fr;
+    const double s0 = fr.sB - fr.sA * (double)px, s1 = fr.sB - fr.sA * (double)(px + vw - 1);
+    const double t0 = fr.tB - fr.tA * (double)py, t1 = fr.tB - fr.tA * (double)(py + vh - 1);
+    for (uint32_t q = 0; q < fr.ocert_n && q < kOcertQuads; ++q) {
+        bool in = true;
+        for (int k = 0; k < 4; ++k) {
+            const double a = rec.ocert.h[q][k][0], b = rec.ocert.h[q][k][1], c = rec.ocert.h[q][k][2];
+            in = in && a * s0 + b * t0 >= c && a * s0 + b * t1 >= c && a * s1 + b * t0 >= c && a * s1 + b * t1 >= c;
+        }
+        if (in) return true;
+    }
+    return false;
+}
+
 // ---------------------------------------------------------------- primary block
 // One 8x8 pixel block: raygen (tracer.go:15-22, :86), nearest hit, outputs of misses,
 // and, if any lane hit, 64 hit slots of region q (slot = lane) with their lit word and
@@ -1643,8 +1676,9 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
     const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
     const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
     const bool active = lx < vw && ly < vh;
-    // classified (k_trace staging, block_may_meet): 1 culled, 2 may meet, 0 test here
-    if (frustum && (classified == 1 || (classified == 0 && block_frustum(wa.fr, frect, px, py, vw, vh) == 0))) {
+    // classified (k_trace staging, block_may_meet): 1 culled, 2 may meet, 0 test here; bit 4:
+    // the block lies in the object-box certificate (block_obj_cert)
+    if (frustum && ((classified & 3) == 1 || ((classified & 3) == 0 && block_frustum(wa.fr, frect, px, py, vw, vh) == 0))) {
         ++ws.nodes;
         diag(21);
         if (active && !MIRT_SKIP_MISS_STORES) {  // every ray misses (tracer.go:88-90: colour zero)
@@ -1689,7 +1723,7 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
     bool redo = false;
     Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d,
                                                                          active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis,
-                                                                         pass2, redo, stk, vt, vn, ls, lt, crect);
+                                                                         pass2, redo, (classified & 4) != 0, stk, vt, vn, ls, lt, crect);
     pc.lap(1);
     ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
     ws.nodes += vis.nodes;
@@ -2296,6 +2330,65 @@ __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uin
 // WorkArgs::frames (staged by k_stage_frames), a one-frame launch (frames == nullptr) from rec.
 // VIEWS: the instantiation that uses view tables (MIRT_OPT_VIEWS); the default one has no
 // view code at all (present, it cost 6 spilled VGPRs and 1.7% of the frame interval).
+// k_trace's second passes, out of line: a primary block or shadow item whose
+// first pass found a winner that its face box rounds out (or a NaN distance) runs again with
+// every candidate box-gated.  They are calls from the work loop, where little is live, so the
+// inlined first passes keep the registers and code of a kernel without them (an inlined second
+// pass cost ~5% of the frame although it never runs on the benchmark's scenes).  A callee's
+// arguments arrive in VGPRs: the wave-uniform ones are made scalar again, and the frame records
+// and work description are read through the constant address space as in the kernel.
+template <typename T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+    return (T*)u64_uniform((uint64_t)p);
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+typedef const __attribute__((address_space(4))) WorkArgs ConstWorkArgs;
+// k_trace's WorkArgs in the kernarg segment (after the first frame's record)
+constexpr size_t kTraceWaOffset = (sizeof(FrameRec) + alignof(WorkArgs) - 1) & ~(alignof(WorkArgs) - 1);
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) WaveStats trace_primary_pass2(const FrameRec* frames, const WorkArgs* wap, uint32_t f,
+                                                                    uint32_t b0, uint32_t b1, uint32_t b2, uint32_t cls,
+                                                                    uint32_t frustum, const float4* frect,
+                                                                    uint32_t* stk, LocalChunks lc) {
+    frames = uni_ptr(frames);
+    const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
+    const FrameRec& fr = frame_rec(frames, uni32(f));
+    lc.count = uni_ptr(lc.count);
+    lc.ready = uni_ptr(lc.ready);
+    lc.base = (size_t)u64_uniform((uint64_t)lc.base);
+    lc.frame_of = uni_ptr(lc.frame_of);
+    lc.frame = uni32(lc.frame);
+    lc.ring = uni_ptr(lc.ring);
+    lc.pos = uni_ptr(lc.pos);
+    WaveStats ws{0, 0, 0, 0, 0};
+    PhaseClock pc;
+    primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, g_lds_mesh, uni_ptr(stk), RESIDENT,
+                                           BlockDesc{uni32(b0), uni32(b1), uni32(b2), 0u}, 0, ws, pc, true,
+                                           uni32(frustum) != 0, uni_ptr(frect), &lc, uni32(cls));
+    return ws;
+}
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) WaveStats trace_shadow_pass2(const FrameRec* frames, const WorkArgs* wap, uint32_t f,
+                                                                   uint32_t segment, uint64_t chunk, uint32_t l,
+                                                                   uint32_t* stk, uint32_t* ring, uint32_t rpos) {
+    frames = uni_ptr(frames);
+    const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
+    const uint32_t cf = uni32(f);
+    const FrameRec& fr = frame_rec(frames, cf);
+    WaveStats ws{0, 0, 0, 0, 0};
+    shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, g_lds_mesh, uni_ptr(stk), RESIDENT, uni32(segment) != 0,
+                                  (size_t)u64_uniform(chunk), uni32(l), ws, true, RESIDENT ? cf : ~0u, nullptr, 64,
+                                  uni_ptr(ring), uni32(rpos));
+    return ws;
+}
+__device__ __forceinline__ void stats_add(WaveStats& a, const WaveStats& b) {
+    a.tests += b.tests;
+    a.nodes += b.nodes;
+    a.leaves += b.leaves;
+    a.hits += b.hits;
+    a.overflow += b.overflow;
+}
+
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
 MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     const FrameArgs& fa = rec.fa;
@@ -2382,7 +2475,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
         const uint32_t t = threadIdx.x;
         uint32_t cls = ~0u, qbl = 0, qf = 0;
         u32x4 qv{0u, 0u, 0u, 0u};
-        bool culled = false;
+        bool culled = false, ocert = false;
         if (t < nc) {
             const uint32_t b = blockIdx.x + (c0 + t) * G;  // over every frame's blocks
             qf = b / nbf;
@@ -2393,7 +2486,10 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
             const uint32_t px = qv[1] & 0xffffu, py = qv[1] >> 16, vw = (qv[2] >> 16) & 0xffu, vh = qv[2] >> 24;
             const uint32_t* lv = frame_rec(frames, qf).live;
             if (px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1]) {
-                if (classify) culled = !block_may_meet(frame_rec(frames, qf).fr, frect[qf], px, py, vw, vh);
+                if (classify) {
+                    culled = !block_may_meet(frame_rec(frames, qf).fr, frect[qf], px, py, vw, vh);
+                    ocert = !culled && block_obj_cert(frame_rec(frames, qf), px, py, vw, vh);
+                }
                 if (!partition) {
                     cls = 0;
                 } else if (culled) {
@@ -2425,7 +2521,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
             bq[slot][0] = qv[0];
             bq[slot][1] = qv[1];
             bq[slot][2] = qv[2];
-            bq_cull[slot] = classify ? (culled ? 1 : 2) : 0;  // 0: not classified
+            bq_cull[slot] = classify ? (culled ? 1 : 2 | (ocert ? 4 : 0)) : 0;  // 0: not classified
             bq_frame[slot] = (uint8_t)qf;
         }
         if (threadIdx.x == 0) {
@@ -2438,9 +2534,6 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
         const uint32_t nfront = s_front, back0 = s_back, nq = nfront + (nc - back0);
         LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0, &s_ring, chunk_pos};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
-        bool pass2 = false;     // pend runs again with every candidate box-gated (shadow_item)
-        uint32_t ppend = kNone;  // a primary ticket held
-        bool ppass2 = false;     // ppend runs again with every candidate box-gated (primary_block)
         for (;;) {
             // 1. a shadow item of an allocated chunk
             const uint32_t avail = lds_ld(&s_chunks) * nl;
@@ -2463,21 +2556,18 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                 const FrameRec& fr = frame_rec(frames, cf);
                 const uint32_t cp = __builtin_amdgcn_readfirstlane(chunk_pos[c]);
                 if (shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64,
-                                                  l, wsh, pass2, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring,
-                                                  cp)) {
-                    pass2 = true;  // the same item again (pend kept), every candidate box-gated
-                    continue;
-                }
-                pass2 = false;
+                                                  l, wsh, false, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring,
+                                                  cp))  // the same item again, every candidate box-gated
+                    stats_add(wsh, trace_shadow_pass2<PREFILTER, BRUTE, RESIDENT>(
+                                       frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset),
+                                       cf, segment ? 1u : 0u, chunk0 + (size_t)cp * 64, l, stk, &s_ring, cp));
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
             }
-            // 2. a primary block (ppend: a ticket held for a block that runs again with pass2)
-            if (ppend == kNone && lds_ld(&s_prim) < nq) ppend = lds_inc(&s_prim);
-            if (ppend != kNone) {
-                const uint32_t q = ppend;
-                if (q >= nq) ppend = kNone;
+            // 2. a primary block
+            if (lds_ld(&s_prim) < nq) {
+                const uint32_t q = lds_inc(&s_prim);
                 if (q < nq) {
                     const uint32_t t = q < nfront ? q : q - nfront + back0;
                     const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
@@ -2496,15 +2586,13 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                     if (VIEWS && RESIDENT && wa.views && fr.fr.on && view_lookup(wa, f * wa.nviews, vc))
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     const uint64_t cost0 = wa.block_cost ? __builtin_amdgcn_s_memtime() : 0;
-                    if (primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc,
-                                                               ppass2, use_frustum, frect[f], &lc,
-                                                               __builtin_amdgcn_readfirstlane(bq_cull[t]), vt,
-                                                               wa.view_leaves, &fr.fr)) {
-                        ppass2 = true;  // the same block again (ppend kept), every candidate box-gated
-                        continue;
-                    }
-                    ppass2 = false;
-                    ppend = kNone;
+                    const uint32_t cls = __builtin_amdgcn_readfirstlane(bq_cull[t]);
+                    if (primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc, false,
+                                                               use_frustum, frect[f], &lc, cls, vt, wa.view_leaves,
+                                                               &fr.fr))  // the same block again, every candidate box-gated
+                        stats_add(wp, trace_primary_pass2<PREFILTER, BRUTE, RESIDENT>(
+                                          frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset),
+                                          f, bd.out, bd.pxy, bd.geo, cls, use_frustum ? 1u : 0u, frect[f], stk, lc));
                     if (wa.block_cost && (threadIdx.x & 63) == 0) {  // this trace's time, for the slot's next frame
                         const uint64_t dc = (__builtin_amdgcn_s_memtime() - cost0) >> 6;
                         wa.block_cost[bq_bl[t]] = (uint16_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));

@@ -463,6 +463,97 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
         }
 }
 
+// The object-box certificate of the primary blocks (FrustumArgs::ocert).  A
+// face of the object's box (Object.Bounds as NewBox corners, world space, the box tracer.go:32
+// tests) whose four corners all lie in front of the camera projects onto a convex quad of the
+// (s, t) plane; a primary ray whose direction lies inside it meets the face's plane at a point
+// of the face, ahead of the camera, so the reference's Box.Intersect (box.go:29-68) accepts it
+// through that plane.  The quad is shrunk by a margin far above every rounding involved (the
+// kernel's pixelToPoint + Norm, the reference's dirScale and intersection point: ~2^-50 of
+// the magnitudes of the camera, the box and the ray, against 2^-24 here), and its float
+// half-planes by their own rounding, so a direction inside the shrunk quad passes exactly.
+// The two faces with the largest quads are kept (the kernarg block holds two).
+void object_cert(const FrameArgs& fa, const double R[3][3], FrustumArgs& fr, ObjCert& oc) {
+    const double* bx = fa.obj[0].box;  // {MinCorner, MaxCorner}
+    double big = 1.0;
+    for (int k = 0; k < 3; ++k) big = std::max({big, std::fabs(fa.cam[k]), std::fabs(bx[k]), std::fabs(bx[3 + k])});
+    // the screen's (s, t) extent
+    const double S = std::fabs(fr.sB) + std::fabs(fr.sA) * 2.0 * fa.halfW, T = std::fabs(fr.tB) + std::fabs(fr.tA) * 2.0 * fa.halfH;
+    struct Quad {
+        double area = 0.0;
+        float h[4][3];
+    };
+    Quad best[kOcertQuads];
+    for (int a = 0; a < 3; ++a)
+        for (int side = 0; side < 2; ++side) {
+            const int b = a == 0 ? 1 : 0, cc = a == 2 ? 1 : 2;
+            double st[4][2], zmin = INFINITY;
+            bool ok = true;
+            for (int k = 0; k < 4; ++k) {  // corners in cyclic order over the face's other two axes
+                const int ub = (k == 1 || k == 2) ? 1 : 0, uc = k >= 2 ? 1 : 0;
+                double X[3];
+                X[a] = bx[3 * side + a] - fa.cam[a];
+                X[b] = bx[3 * ub + b] - fa.cam[b];
+                X[cc] = bx[3 * uc + cc] - fa.cam[cc];
+                const double mag = std::max({std::fabs(X[0]), std::fabs(X[1]), std::fabs(X[2])});
+                const double z = R[0][0] * X[0] + R[0][1] * X[1] + R[0][2] * X[2];
+                if (!(z > 0x1p-20 * mag) || !(mag > 0.0)) {
+                    ok = false;
+                    break;
+                }
+                zmin = std::min(zmin, z);
+                st[k][0] = (R[1][0] * X[0] + R[1][1] * X[1] + R[1][2] * X[2]) / z;
+                st[k][1] = (R[2][0] * X[0] + R[2][1] * X[1] + R[2][2] * X[2]) / z;
+            }
+            if (!ok) continue;
+            double area = 0.0, cs = 0.0, ct = 0.0;
+            for (int k = 0; k < 4; ++k) {
+                const double* p = st[k];
+                const double* q = st[(k + 1) & 3];
+                area += p[0] * q[1] - q[0] * p[1];
+                cs += p[0] / 4;
+                ct += p[1] / 4;
+            }
+            area = std::fabs(area) / 2;
+            const double margin = 0x1p-24 * (1.0 + S + T) * (1.0 + big / zmin);
+            Quad qd;
+            qd.area = area;
+            for (int k = 0; k < 4; ++k) {
+                const double* p = st[k];
+                const double* q = st[(k + 1) & 3];
+                double na = q[1] - p[1], nb = -(q[0] - p[0]);
+                if (na * (cs - p[0]) + nb * (ct - p[1]) < 0) {
+                    na = -na;
+                    nb = -nb;
+                }
+                const double len = std::sqrt(na * na + nb * nb);
+                if (!(len > 0.0) || !std::isfinite(len)) {
+                    ok = false;
+                    break;
+                }
+                na /= len;
+                nb /= len;
+                const float fa_ = (float)na, fb_ = (float)nb;
+                // n . (s, t) >= n . p + margin, with the float coefficients' own rounding added
+                double c0 = na * p[0] + nb * p[1] + margin;
+                c0 += 0x1p-22 * (std::fabs(na) * S + std::fabs(nb) * T + std::fabs(c0)) + 0x1p-60;
+                qd.h[k][0] = fa_;
+                qd.h[k][1] = fb_;
+                qd.h[k][2] = detail::round_up(c0);
+            }
+            if (!ok || !(area > 0.0) || !std::isfinite(area)) continue;
+            for (uint32_t q = 0; q < kOcertQuads; ++q)
+                if (area > best[q].area) {
+                    for (uint32_t r = kOcertQuads - 1; r > q; --r) best[r] = best[r - 1];
+                    best[q] = qd;
+                    break;
+                }
+        }
+    fr.ocert_n = 0;
+    for (uint32_t q = 0; q < kOcertQuads; ++q)
+        if (best[q].area > 0.0) memcpy(oc.h[fr.ocert_n++], best[q].h, sizeof(best[q].h));
+}
+
 // Rectangles of the primary kernel's whole-block frustum pre-test (mirt_internal.hpp
 // FrustumArgs).  With R the inverse of the basis matrix [fwd left up], a point X (object
 // space, relative to the camera) lies on the ray of (s, t) at parameter z = R0.X > 0 iff
@@ -471,8 +562,9 @@ void fill_args(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, F
 // entirely behind it (z < 0 everywhere: rays start at z = 0) is never met; anything else
 // is always tested.  Hits lie inside the inflated boxes, and the margin
 // covers the fp64 rounding of this projection and of the kernels' rays.
-void frustum_args(const mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa, FrustumArgs& fr) {
+void frustum_args(const mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa, FrustumArgs& fr, ObjCert& oc) {
     memset(&fr, 0, sizeof(fr));
+    memset(&oc, 0, sizeof(oc));
     if (fa.n_objects != 1 || (c->flags & (MIRT_OPT_NO_FRUSTUM | MIRT_OPT_BRUTE_FORCE)) || fa.halfW < 1 ||
         fa.halfH < 1)
         return;
@@ -545,6 +637,7 @@ void frustum_args(const mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa, F
     fr.tA = fa.phh / (double)fa.halfH;
     fr.tB = fa.phh * ((double)fa.halfH - 0.5) / (double)fa.halfH;
     fr.on = std::isfinite(fr.sA) && std::isfinite(fr.sB) && std::isfinite(fr.tA) && std::isfinite(fr.tB) ? 1u : 0u;
+    if (fr.on && !(c->flags & MIRT_OPT_NO_BOX_GATE)) object_cert(fa, R, fr, oc);
 }
 
 int prof_get(mirt_ctx* c, ProfRec& r) {
@@ -832,7 +925,7 @@ void frame_record(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H
     fill_args(c, f, W, H, rec.fa, tris);
     rec.fa.ltab = light_table(const_cast<mirt_ctx*>(c), f, rec.fa);
     rec.fa.ltab_n = rec.fa.ltab ? c->meshes[f->objects[0].mesh_id].ntri : 0;
-    frustum_args(c, f, rec.fa, rec.fr);
+    frustum_args(c, f, rec.fa, rec.fr, rec.ocert);
     rec.out = out;
     rec.live[0] = rec.live[1] = 0;  // every block (a frame group narrows it to the hit rectangle)
     rec.live[2] = W;

@@ -258,7 +258,16 @@ struct FrustumArgs {
     float rect[8][4];      // per root child: s_lo, s_hi, t_lo, t_hi (empty child: an empty rectangle)
     double sA, sB, tA, tB; // tracer.go:19-20 offsets as affine maps: column i ~ sB - sA i, row j ~ tB - tA j
     uint32_t on;           // one object, culling on, bounded camera, W, H >= 2
-    uint32_t pad;
+    uint32_t ocert_n;      // FrameRec::ocert quads in use (0..kOcertQuads)
+};
+constexpr uint32_t kOcertQuads = 2;
+// Object-box certificate of the primary blocks: per quad, four half-planes
+// a s + b t >= c of the (s, t) plane, the projection of one face of the object's box shrunk by
+// a margin.  A primary ray whose direction lies in one passes the reference's Box.Intersect of
+// that box through that face's plane (tracer.go:32), so a block whose four corner directions
+// all lie in one quad skips the object's gate.  (In FrameRec only: the kernarg block is full.)
+struct ObjCert {
+    float h[kOcertQuads][4][3];
 };
 
 // One frame of a k_trace launch, in device memory (a launch traces up to kMaxFrames
@@ -269,6 +278,7 @@ struct alignas(16) FrameRec {
     FrameArgs fa;
     OutPlanes out;
     FrustumArgs fr;
+    ObjCert ocert;
     // Blocks with no pixel in [live[0], live[2]) x [live[1], live[3]) are not traced: every
     // ray of such a block misses, and the caller either cleared their outputs (a frame
     // group's whole-screen planes, launch_fill_planes) or never reads them (a share's packed

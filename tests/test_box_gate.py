@@ -271,3 +271,43 @@ def test_vertex_aimed_rays_match_boxes_oracle(ctx):
         for k in ("hit", "normal"):
             assert np.array_equal(got[k][ok], ref[k][ok]), k
     assert gated > 0
+
+
+@pytest.mark.gpu
+def test_object_box_certificate_cameras_match_rtree(ctx):
+    """Primary blocks inside the object-box certificate skip the object's gate (FrameRec::ocert,
+    mirt.cpp object_cert): a cube that fills its box (every face of the mesh lies on the object's
+    box, so rays along the box's edges and corners hit the mesh there) seen from cameras around
+    and near it, the box's edges crossing many blocks, equals the R-tree oracle pixel for pixel,
+    and equals the frame traced without the certificate (MIRT_OPT_NO_FRUSTUM)."""
+    import distributed_raytracer_amd as rt
+    from oracle.oracle import Oracle
+    from oracle.scene_py import PyScene
+    from scenes import box_mesh, gpu_env, with_camera
+    sc = PyScene()
+    sc.meshes = [box_mesh(1.0)]
+    sc.objects = [(0, (0.25, -0.5, 0.125))]
+    sc.lights = [((3.0, 4.0, 5.0), (1.0, 1.0, 1.0)), ((-4.0, 0.5, 2.0), (0.5, 0.2, 0.9))]
+    rng = np.random.default_rng(5)
+    W, H = 96, 64
+    n = 0
+    for k in range(10):
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        pos = np.asarray(sc.objects[0][1]) + (1.3 + 3.0 * rng.random()) * d
+        look = np.asarray(sc.objects[0][1]) + rng.normal(scale=0.3, size=3) - pos
+        s = with_camera(sc, pos, look, fov=float(rng.uniform(0.4, 1.2)))
+        env = gpu_env(ctx, s)
+        ref = Oracle(s, culling="rtree").frame(W, H, nthreads=8)
+        fb = rt.draw(env, W, H)
+        ctx.set_options(rt._lib.MIRT_OPT_NO_FRUSTUM)
+        try:
+            fb2 = rt.draw(env, W, H)
+        finally:
+            ctx.set_options(0)
+        for key in ("valid", "obj", "face", "rgb", "rgb8"):
+            a, b = getattr(fb, key), ref[key]
+            assert np.array_equal(a, b), f"camera {k}: {key} differs in {(a != b).sum()} elements"
+            assert np.array_equal(getattr(fb2, key), b), f"camera {k} (no certificate): {key}"
+        n += int(ref["valid"].sum())
+    assert n > 0

@@ -35,7 +35,8 @@ def main():
           " culled blocks", c[21])
     print("shadow light-table classifications", c[22], " skipped by the wave", c[22] - c[8])
     print("box gates", c[24], " further far planes", c[25], " near planes", c[26], " waves with a failing box", c[27],
-          " nearest redo", c[28], " segment redo", c[29])
+          " nearest redo", c[28], " segment redo", c[29],
+          " object gates skipped (block certificate)", c[30])
     g.close()
 
 
