@@ -217,9 +217,11 @@ struct Best {
     uint32_t face;     // lowest original face index at that distance
     uint32_t pos;      // its position in the BVH-ordered arrays
     uint32_t first;    // lowest original face index of any hit (0xffffffff: none)
-    uint32_t first_pos;
+    uint32_t first_pos;  // (bit 31: some hit's distance is NaN, see any_nan)
     uint32_t first_nan;  // that hit's distance is NaN
-    uint32_t any_nan;    // some hit's distance is NaN (box_settle: the winner alone does not decide)
+    // some hit's distance is NaN (the box gate: the winner alone does not decide).  Kept in
+    // first_pos's bit 31 (positions are < 2^24): one VGPR fewer live through the sweep.
+    __device__ __forceinline__ uint32_t any_nan() const { return MIRT_BOX_GATE == 4 ? 0u : first_pos >> 31; }
 };
 __device__ __forceinline__ void best_init(Best& b) {
     b.has = 0;
@@ -228,16 +230,16 @@ __device__ __forceinline__ void best_init(Best& b) {
     b.first = 0xffffffffu;
     b.first_pos = 0;
     b.first_nan = 0;
-    b.any_nan = 0;
 }
 __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
     const bool isnan_d = dist != dist;
-    if (MIRT_BOX_GATE != 4) b.any_nan |= isnan_d ? 1u : 0u;  // (4: measurement build without it)
+    const uint32_t nanbit = isnan_d ? 0x80000000u : 0u;
     if (face < b.first) {
         b.first = face;
-        b.first_pos = pos;
+        b.first_pos = pos | (b.first_pos & 0x80000000u);
         b.first_nan = isnan_d ? 1u : 0u;
     }
+    if (MIRT_BOX_GATE != 4) b.first_pos |= nanbit;  // (4: measurement build without it)
     if (!isnan_d && (!b.has || dist < b.d || (dist == b.d && face < b.face))) {
         b.has = 1;
         b.d = dist;
@@ -249,7 +251,7 @@ __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint3
     if (b.first == 0xffffffffu) return false;
     if (b.first_nan || !b.has) {
         face = b.first;
-        pos = b.first_pos;
+        pos = b.first_pos & 0x7fffffffu;
     } else {
         face = b.face;
         pos = b.pos;
@@ -548,6 +550,8 @@ struct WaveStack {
     int a = 0, b = 0;
     uint32_t sp = 0;
     __device__ __forceinline__ void put(uint32_t ref) {  // write the entry above the top
+        ref = __builtin_amdgcn_readfirstlane(ref);  // (scalar already, except in an out-of-line pass)
+        sp = __builtin_amdgcn_readfirstlane(sp);
         if (!DEEP || sp < 64)
             asm("v_writelane_b32 %0, %1, m0" : "+v"(a) : "s"(ref), "{m0}"(sp));
         else
@@ -1185,7 +1189,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
                 else
                     fok = r;
             }
-            if (!pass2) again = again || (got && (!fok || b.any_nan));
+            if (!pass2) again = again || (got && (!fok || b.any_nan()));
         }
         if (got) {
             V3 world, normal{0, 0, 0};
@@ -1339,7 +1343,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     if (gating) {
         uint32_t face = 0, p = 0;
         const bool retired = b.has && b.d < resolve;
-        const bool far_lit = !retired && b.has && !b.any_nan && b.d > lh + 1e-4 + M;
+        const bool far_lit = !retired && b.has && !b.any_nan() && b.d > lh + 1e-4 + M;
         const bool need = lane_on && best_result(b, face, p) && !far_lit;
         // the object's box (tracer.go:32), then, in a first pass, the face box the decision
         // rests on (object.go:76)
@@ -1353,7 +1357,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         }
         if (need && !ok) best_init(b);
         if (!pass2) {
-            redo = __ballot(ok && (!fok || (!retired && b.any_nan))) != 0;
+            redo = __ballot(ok && (!fok || (!retired && b.any_nan()))) != 0;
             if (redo) diag(29);  // segment queries run again (pass 2)
             if (MIRT_BOX_GATE == 2) {  // measurement build: gates evaluated, no second pass
                 vis.overflow += redo;
@@ -2172,6 +2176,59 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
 // ---------------------------------------------------------------- primary kernel
 // RESIDENT (host-decided): one object whose mesh fits in LDS; it is staged once per
 // persistent workgroup, relative to the camera (p1or), and every sweep reads LDS.
+// Out-of-line second passes (see k_trace's): helpers.
+template <typename T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+    return (T*)u64_uniform((uint64_t)p);
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ void stats_add(WaveStats& a, const WaveStats& b) {
+    a.tests += b.tests;
+    a.nodes += b.nodes;
+    a.leaves += b.leaves;
+    a.hits += b.hits;
+    a.overflow += b.overflow;
+}
+
+// The split kernels' parameters (fa, wa, then a third) in the kernarg segment, read through
+// the constant address space by their out-of-line second passes.
+template <typename T>
+__device__ __forceinline__ const T& kconst(const char* p) {
+    return *(const T*)(const __attribute__((address_space(4))) T*)p;
+}
+constexpr size_t kalign(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+constexpr size_t kSplitWaOff = kalign(sizeof(FrameArgs), alignof(WorkArgs));
+__device__ __forceinline__ const FrameArgs& split_fa(const char* ka) { return kconst<FrameArgs>(ka); }
+__device__ __forceinline__ const WorkArgs& split_wa(const char* ka) { return kconst<WorkArgs>(ka + kSplitWaOff); }
+template <typename T>
+__device__ __forceinline__ const T& split_third(const char* ka) {
+    return kconst<T>(ka + kalign(kSplitWaOff + sizeof(WorkArgs), alignof(T)));
+}
+
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) WaveStats split_primary_pass2(const char* ka, uint32_t b0, uint32_t b1, uint32_t b2,
+                                                                    uint32_t blk, uint32_t frustum, const float4* frect,
+                                                                    uint32_t* stk) {
+    ka = uni_ptr(ka);
+    const uint32_t b = uni32(blk);
+    WaveStats ws{0, 0, 0, 0, 0};
+    PhaseClock pc;
+    primary_block<RESIDENT, PREFILTER, BRUTE>(split_fa(ka), split_wa(ka), split_third<OutPlanes>(ka), g_lds_mesh,
+                                              uni_ptr(stk), RESIDENT, BlockDesc{uni32(b0), uni32(b1), uni32(b2), 0u},
+                                              b % kQShards, ws, pc, true, uni32(frustum) != 0, uni_ptr(frect), nullptr, 0,
+                                              nullptr, 0, nullptr, b);
+    return ws;
+}
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) WaveStats split_shadow_pass2(const char* ka, uint32_t segment, uint64_t chunk,
+                                                                   uint32_t l, uint32_t lim, uint32_t* stk) {
+    ka = uni_ptr(ka);
+    WaveStats ws{0, 0, 0, 0, 0};
+    shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(split_fa(ka), split_wa(ka), split_third<OutPlanes>(ka), g_lds_mesh,
+                                                   uni_ptr(stk), RESIDENT, uni32(segment) != 0,
+                                                   (size_t)u64_uniform(chunk), uni32(l), ws, true, ~0u, nullptr, uni32(lim));
+    return ws;
+}
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
@@ -2215,7 +2272,6 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
         if (c0 == 0) clock.mark_staged();
         __syncthreads();
         uint32_t t = wave;
-        bool pass2 = false;
         while (t < nc) {
             const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(bq[t][0]),
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
@@ -2223,11 +2279,11 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
             const uint32_t b = blockIdx.x + (c0 + t) * G;
             ++taken;
             if (primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
-                                                          pass2, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b)) {
-                pass2 = true;  // the same block again, every candidate box-gated
-                continue;
-            }
-            pass2 = false;
+                                                          false, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b))
+                // the same block again, every candidate box-gated, out of line (as k_trace's)
+                stats_add(ws, split_primary_pass2<PREFILTER, BRUTE, RESIDENT>((const char*)__builtin_amdgcn_kernarg_segment_ptr(),
+                                                                              bd.out, bd.pxy, bd.geo, b, use_frustum ? 1u : 0u,
+                                                                              frect, wstk[wave]));
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -2284,20 +2340,18 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
         // each ticket taken while the previous item is traced
         const bool dyn = (wa.dynamic & kDynShadow) && items > peers;
         uint32_t k = sc.rank(), nxt = 0;
-        bool pass2 = false;  // the same item again, every candidate box-gated (shadow_item)
         while (k < items) {
-            if (!pass2) {
-                nxt = dyn ? ticket_issue(qc) : 0;
-                ++taken;
-            }
+            nxt = dyn ? ticket_issue(qc) : 0;
+            ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
             if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
-                                                              (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, pass2, ~0u,
-                                                              nullptr, min(64u, nrec - c * 64))) {
-                pass2 = true;
-                continue;
-            }
-            pass2 = false;
+                                                              (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, false, ~0u,
+                                                              nullptr, min(64u, nrec - c * 64)))
+                // the same item again, every candidate box-gated, out of line (as k_trace's)
+                stats_add(ws, split_shadow_pass2<PREFILTER, BRUTE, RESIDENT>(
+                                  (const char*)__builtin_amdgcn_kernarg_segment_ptr(), segment ? 1u : 0u,
+                                  (size_t)q * wa.hit_cap + (size_t)c * 64, l, min(64u, nrec - c * 64),
+                                  wstk[threadIdx.x >> 6]));
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
@@ -2337,11 +2391,6 @@ __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uin
 // pass cost ~5% of the frame although it never runs on the benchmark's scenes).  A callee's
 // arguments arrive in VGPRs: the wave-uniform ones are made scalar again, and the frame records
 // and work description are read through the constant address space as in the kernel.
-template <typename T>
-__device__ __forceinline__ T* uni_ptr(T* p) {
-    return (T*)u64_uniform((uint64_t)p);
-}
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 typedef const __attribute__((address_space(4))) WorkArgs ConstWorkArgs;
 // k_trace's WorkArgs in the kernarg segment (after the first frame's record)
 constexpr size_t kTraceWaOffset = (sizeof(FrameRec) + alignof(WorkArgs) - 1) & ~(alignof(WorkArgs) - 1);
@@ -2380,13 +2429,6 @@ __device__ __attribute__((noinline)) WaveStats trace_shadow_pass2(const FrameRec
                                   (size_t)u64_uniform(chunk), uni32(l), ws, true, RESIDENT ? cf : ~0u, nullptr, 64,
                                   uni_ptr(ring), uni32(rpos));
     return ws;
-}
-__device__ __forceinline__ void stats_add(WaveStats& a, const WaveStats& b) {
-    a.tests += b.tests;
-    a.nodes += b.nodes;
-    a.leaves += b.leaves;
-    a.hits += b.hits;
-    a.overflow += b.overflow;
 }
 
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
@@ -2783,6 +2825,116 @@ MIRT_REFLECT_KERNEL void k_reflect(const FrameArgs fa, const WorkArgs wa, OutPla
 // through every level: 41% of its lanes had a ray at level 1, ~12% at level 4); k_shadow then
 // traces level lv's shadow rays and stores its
 // phong at the origin slot; k_refl_fold combines the levels per pixel, innermost first.
+// One input chunk of a bounce level (k_bounce): its reflection rays' nearest hits, the level's
+// records at the input's slots.  true: a second pass is needed (nothing written).
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __forceinline__ bool bounce_chunk(const FrameArgs& fa, const WorkArgs& wa, const BounceArgs& ba,
+                                             const double* __restrict__ lds, uint32_t q, uint32_t k, uint32_t n,
+                                             uint32_t cp, bool pass2, WaveStats& ws, cnt_t& rays, cnt_t& shadow_rays) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lv = ba.level;
+        const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
+        const bool inb = k * 64 + lane < n;
+        const HitRec rec = ba.in[inb ? slot : (size_t)q * wa.hit_cap + (size_t)k * 64];
+        const bool active = inb && rec.obj != kNoHit;
+        const size_t origin = (size_t)rec.out;  // k_pack: the primary hit slot of the chain
+        V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
+        if (active) {
+            D = vload(ba.in_dir + 3 * slot);
+            hit = vload(rec.h);
+            N = vload(rec.n);
+        }
+        const V3 R = sub(D, scale(N, 2 * dot(D, N)));
+        const V3 o = add(hit, scale(R, 0.0001));
+        Visits vis{0, 0, 0, 0};
+        bool redo = false;
+        const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, active, true, vis, pass2, redo);
+        if (redo) {  // wave-uniform: nothing written yet
+            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+            ws.nodes += vis.nodes;
+            ws.leaves += vis.leaves;
+            return true;
+        }
+        rays += __popcll(__ballot(active));
+        ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
+        ws.nodes += vis.nodes;
+        ws.leaves += vis.leaves;
+        ws.overflow += vis.overflow;
+        const bool got = active && r.ok;
+        if (active) ba.chain[origin] = got ? lv + 1 : (lv | 256u);  // levels with phong | missed
+        const uint64_t m = __ballot(got);
+        shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
+        if (MIRT_BOUNCE_SHADE && m) {
+            // the level's shadow rays and phong in this wave (tracer.go:53-77 at the hit;
+            // the packed lanes are mostly live): no k_shadow launch per level
+            const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
+            uint32_t lit = 0;
+            for (uint32_t l = 0; l < fa.n_lights; ++l) {
+                const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+                V3 so{0, 0, 0}, sd{1, 0, 0};
+                if (got) {
+                    sd = norm(sub(lpos, r.hit));
+                    so = add(r.hit, scale(sd, 0.0001));
+                }
+                Visits sv{0, 0, 0, 0};
+                bool is_lit;
+                if (segment) {
+                    is_lit = shadow_lit_single_settled<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, got, sv);
+                } else {
+                    const Nearest sr = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, got, false, sv);
+                    is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
+                }
+                lit |= (uint32_t)is_lit << l;
+                ws.tests += (cnt_t)sv.tests * __popcll(m);
+                ws.nodes += sv.nodes;
+                ws.leaves += sv.leaves;
+                ws.overflow += sv.overflow;
+            }
+            if (got) {
+                const RGB ph = phong(fa, fa.obj[r.obj].m.mats + (size_t)r.mat * 10, r.hit, r.normal, lit);
+                double* const e = wa.refl + ((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD;
+                e[0] = ph.r;
+                e[1] = ph.g;
+                e[2] = ph.b;
+            }
+        }
+        // the level's hits stay at the input's slots; k_pack compacts them in order
+        uint64_t* w = (uint64_t*)&ba.out[slot];
+        if (got) {
+            st64(w + 0, dbits(r.hit.x));
+            st64(w + 1, dbits(r.hit.y));
+            st64(w + 2, dbits(r.hit.z));
+            st64(w + 3, dbits(r.normal.x));
+            st64(w + 4, dbits(r.normal.y));
+            st64(w + 5, dbits(r.normal.z));
+            st64(w + 6, (uint64_t)origin);
+            st64(w + 7, (uint64_t)r.obj | ((uint64_t)r.mat << 32));
+            vstore(ba.out_dir + 3 * slot, R);
+            wa.refl[((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD + 3] =
+                bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
+        } else {
+            st64(w + 7, (uint64_t)kNoHit);
+        }
+        if (lane == 0) {
+            const uint32_t j = q * cp + k;
+            ba.src[j] = (uint32_t)(((size_t)q * wa.hit_cap + (size_t)k * 64) / 64 + 1) << 7 | (uint32_t)__popcll(m);
+            if (m) atomicAdd(&ba.gcnt[j / kPackGroup], (uint32_t)__popcll(m));
+        }
+    return false;
+}
+struct BounceOut {
+    WaveStats ws;
+    cnt_t rays, shadow_rays;
+};
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) BounceOut bounce_pass2(const char* ka, uint32_t q, uint32_t k, uint32_t n,
+                                                             uint32_t cp) {
+    ka = uni_ptr(ka);
+    BounceOut r{{0, 0, 0, 0, 0}, 0, 0};
+    bounce_chunk<PREFILTER, BRUTE, RESIDENT>(split_fa(ka), split_wa(ka), split_third<BounceArgs>(ka), g_lds_mesh, uni32(q),
+                                             uni32(k), uni32(n), uni32(cp), true, r.ws, r.rays, r.shadow_rays);
+    return r;
+}
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const BounceArgs ba) {
     double* const lds = g_lds_mesh;
@@ -2801,96 +2953,14 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     const uint32_t cp = (uint32_t)(ba.in_cnt[cnt_hits(0)] >> 32);
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
-        bool pass2 = false;  // the same chunk again, every candidate box-gated (trace_nearest)
         for (uint32_t k = sc.rank(); k < nch;) {
-            const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
-            const bool inb = k * 64 + lane < n;
-            const HitRec rec = ba.in[inb ? slot : (size_t)q * wa.hit_cap + (size_t)k * 64];
-            const bool active = inb && rec.obj != kNoHit;
-            const size_t origin = (size_t)rec.out;  // k_pack: the primary hit slot of the chain
-            V3 D{1, 0, 0}, hit{0, 0, 0}, N{0, 0, 1};
-            if (active) {
-                D = vload(ba.in_dir + 3 * slot);
-                hit = vload(rec.h);
-                N = vload(rec.n);
-            }
-            const V3 R = sub(D, scale(N, 2 * dot(D, N)));
-            const V3 o = add(hit, scale(R, 0.0001));
-            Visits vis{0, 0, 0, 0};
-            bool redo = false;
-            const Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, o, R, active, true, vis, pass2, redo);
-            if (redo) {  // wave-uniform: nothing written yet
-                ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-                ws.nodes += vis.nodes;
-                ws.leaves += vis.leaves;
-                pass2 = true;
-                continue;
-            }
-            pass2 = false;
-            rays += __popcll(__ballot(active));
-            ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
-            ws.nodes += vis.nodes;
-            ws.leaves += vis.leaves;
-            ws.overflow += vis.overflow;
-            const bool got = active && r.ok;
-            if (active) ba.chain[origin] = got ? lv + 1 : (lv | 256u);  // levels with phong | missed
-            const uint64_t m = __ballot(got);
-            shadow_rays += (cnt_t)__popcll(m) * fa.n_lights;
-            if (MIRT_BOUNCE_SHADE && m) {
-                // the level's shadow rays and phong in this wave (tracer.go:53-77 at the hit;
-                // the packed lanes are mostly live): no k_shadow launch per level
-                const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
-                uint32_t lit = 0;
-                for (uint32_t l = 0; l < fa.n_lights; ++l) {
-                    const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
-                    V3 so{0, 0, 0}, sd{1, 0, 0};
-                    if (got) {
-                        sd = norm(sub(lpos, r.hit));
-                        so = add(r.hit, scale(sd, 0.0001));
-                    }
-                    Visits sv{0, 0, 0, 0};
-                    bool is_lit;
-                    if (segment) {
-                        is_lit = shadow_lit_single_settled<PREFILTER>(fa, lds, RESIDENT, nullptr, r.hit, so, sd, lpos, l, got, sv);
-                    } else {
-                        const Nearest sr = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, lds, RESIDENT, so, sd, got, false, sv);
-                        is_lit = !sr.ok || len(sub(lpos, r.hit)) < len(sub(sr.hit, r.hit));
-                    }
-                    lit |= (uint32_t)is_lit << l;
-                    ws.tests += (cnt_t)sv.tests * __popcll(m);
-                    ws.nodes += sv.nodes;
-                    ws.leaves += sv.leaves;
-                    ws.overflow += sv.overflow;
-                }
-                if (got) {
-                    const RGB ph = phong(fa, fa.obj[r.obj].m.mats + (size_t)r.mat * 10, r.hit, r.normal, lit);
-                    double* const e = wa.refl + ((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD;
-                    e[0] = ph.r;
-                    e[1] = ph.g;
-                    e[2] = ph.b;
-                }
-            }
-            // the level's hits stay at the input's slots; k_pack compacts them in order
-            uint64_t* w = (uint64_t*)&ba.out[slot];
-            if (got) {
-                st64(w + 0, dbits(r.hit.x));
-                st64(w + 1, dbits(r.hit.y));
-                st64(w + 2, dbits(r.hit.z));
-                st64(w + 3, dbits(r.normal.x));
-                st64(w + 4, dbits(r.normal.y));
-                st64(w + 5, dbits(r.normal.z));
-                st64(w + 6, (uint64_t)origin);
-                st64(w + 7, (uint64_t)r.obj | ((uint64_t)r.mat << 32));
-                vstore(ba.out_dir + 3 * slot, R);
-                wa.refl[((size_t)(lv - 1) * wa.refl_stride + origin) * kReflD + 3] =
-                    bitsd((uint64_t)r.obj | ((uint64_t)r.mat << 32));
-            } else {
-                st64(w + 7, (uint64_t)kNoHit);
-            }
-            if (lane == 0) {
-                const uint32_t j = q * cp + k;
-                ba.src[j] = (uint32_t)(((size_t)q * wa.hit_cap + (size_t)k * 64) / 64 + 1) << 7 | (uint32_t)__popcll(m);
-                if (m) atomicAdd(&ba.gcnt[j / kPackGroup], (uint32_t)__popcll(m));
+            if (bounce_chunk<PREFILTER, BRUTE, RESIDENT>(fa, wa, ba, lds, q, k, n, cp, false, ws, rays, shadow_rays)) {
+                // the same chunk again, every candidate box-gated, out of line (as k_trace's)
+                const BounceOut r2 = bounce_pass2<PREFILTER, BRUTE, RESIDENT>(
+                    (const char*)__builtin_amdgcn_kernarg_segment_ptr(), q, k, n, cp);
+                stats_add(ws, r2.ws);
+                rays += r2.rays;
+                shadow_rays += r2.shadow_rays;
             }
             k += sc.peers();
         }
