@@ -208,40 +208,37 @@ __device__ __forceinline__ void stage_tris(double* __restrict__ s, const double*
 // the minimum distance — except that a NaN distance on the lowest-indexed hit wins (no
 // later `<` beats NaN) and a NaN anywhere else never wins.  `consider` computes exactly
 // that in ANY visiting order, so culling/reordering cannot change the result.
-// (the flags are 0/1 words, not bools: a bool that lives across the test's divergent stages
-// is a lane mask the compiler merges with three scalar instructions at every join, a word in a
-// VGPR is merged by the exec mask for free)
+// (no bools: a bool that lives across the test's divergent stages is a lane mask the compiler
+// merges with three scalar instructions at every join, a word in a VGPR is merged by the exec
+// mask for free; the flags are a sentinel and bits of words the state holds anyway)
 struct Best {
-    uint32_t has;      // any non-NaN hit
-    double d;          // its minimum distance
-    uint32_t face;     // lowest original face index at that distance
-    uint32_t pos;      // its position in the BVH-ordered arrays
-    uint32_t first;    // lowest original face index of any hit (0xffffffff: none)
-    uint32_t first_pos;  // (bit 31: some hit's distance is NaN, see any_nan)
-    uint32_t first_nan;  // that hit's distance is NaN
-    // some hit's distance is NaN (the box gate: the winner alone does not decide).  Kept in
-    // first_pos's bit 31 (positions are < 2^24): one VGPR fewer live through the sweep.
+    double d;           // the minimum non-NaN distance (if has())
+    uint32_t face;      // lowest original face index at that distance; ~0u: no non-NaN hit yet
+    uint32_t pos;       // its position in the BVH-ordered arrays
+    uint32_t first;     // lowest original face index of any hit (0xffffffff: none)
+    // that hit's position; bit 30: its distance is NaN; bit 31: some hit's distance is NaN (the
+    // box gate: the winner alone does not decide).  Positions are < 2^24, and the flags packed
+    // here keep two VGPRs fewer live through the sweep.
+    uint32_t first_pos;
+    __device__ __forceinline__ bool has() const { return face != 0xffffffffu; }
+    __device__ __forceinline__ uint32_t first_nan() const { return (first_pos >> 30) & 1u; }
     __device__ __forceinline__ uint32_t any_nan() const { return MIRT_BOX_GATE == 4 ? 0u : first_pos >> 31; }
 };
 __device__ __forceinline__ void best_init(Best& b) {
-    b.has = 0;
     b.d = 0;
-    b.face = b.pos = 0;
+    b.face = 0xffffffffu;
+    b.pos = 0;
     b.first = 0xffffffffu;
     b.first_pos = 0;
-    b.first_nan = 0;
 }
 __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, uint32_t pos) {
     const bool isnan_d = dist != dist;
-    const uint32_t nanbit = isnan_d ? 0x80000000u : 0u;
     if (face < b.first) {
         b.first = face;
-        b.first_pos = pos | (b.first_pos & 0x80000000u);
-        b.first_nan = isnan_d ? 1u : 0u;
+        b.first_pos = pos | (isnan_d ? 0x40000000u : 0u) | (b.first_pos & 0x80000000u);
     }
-    if (MIRT_BOX_GATE != 4) b.first_pos |= nanbit;  // (4: measurement build without it)
-    if (!isnan_d && (!b.has || dist < b.d || (dist == b.d && face < b.face))) {
-        b.has = 1;
+    if (MIRT_BOX_GATE != 4) b.first_pos |= isnan_d ? 0x80000000u : 0u;  // (4: measurement build without it)
+    if (!isnan_d && (!b.has() || dist < b.d || (dist == b.d && face < b.face))) {
         b.d = dist;
         b.face = face;
         b.pos = pos;
@@ -249,9 +246,9 @@ __device__ __forceinline__ void consider(Best& b, double dist, uint32_t face, ui
 }
 __device__ __forceinline__ bool best_result(const Best& b, uint32_t& face, uint32_t& pos) {
     if (b.first == 0xffffffffu) return false;
-    if (b.first_nan || !b.has) {
+    if (b.first_nan() || !b.has()) {
         face = b.first;
-        pos = b.first_pos & 0x7fffffffu;
+        pos = b.first_pos & 0x3fffffffu;
     } else {
         face = b.face;
         pos = b.pos;
@@ -773,9 +770,9 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
                                                                  neg, b, vis.tests,
                                                                  lt ? lt + (size_t)first * kLtD : nullptr, sp, live, fbox);
             if (SEG) {
-                live = live && !(b.has && b.d < resolve);
+                live = live && !(b.has() && b.d < resolve);
                 if (__ballot(live) == 0) break;
-            } else if (b.has) {
+            } else if (b.has()) {
                 tm = (float)(b.d + (Mbase + 0x1p-36 * b.d)) * (1.0f + 0x1p-20f);
             }
             continue;
@@ -983,7 +980,7 @@ __device__ __forceinline__ void bvh_wide(const DevMesh& m, SrcPtr src, uint32_t*
             const uint32_t first = lref & kBvhFirstMask, cnt = (lref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
             test_range<REL, PREFILTER>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b, vis.tests);
-            if (SEG) live = live && !(b.has && b.d < resolve);
+            if (SEG) live = live && !(b.has() && b.d < resolve);
         }
         if (SEG && __ballot(live) == 0) break;
     }
@@ -1049,12 +1046,12 @@ __device__ __forceinline__ void view_sweep(const DevMesh& m, SrcPtr src, const V
             test_range<false, PREFILTER, SEG ? 8 : 0, SEG>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d, neg, b,
                                                         vis.tests);
             if (SEG) {
-                live = live && !(b.has && b.d < resolve);
+                live = live && !(b.has() && b.d < resolve);
                 if (__ballot(live) == 0) {
                     done = true;
                     break;
                 }
-            } else if (b.has) {
+            } else if (b.has()) {
                 zl = fminf(zl, (float)(b.d + (Mbase + 0x1p-36 * b.d)) * (1.0f + 0x1p-20f));
             }
         }
@@ -1342,8 +1339,8 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
     }
     if (gating) {
         uint32_t face = 0, p = 0;
-        const bool retired = b.has && b.d < resolve;
-        const bool far_lit = !retired && b.has && !b.any_nan() && b.d > lh + 1e-4 + M;
+        const bool retired = b.has() && b.d < resolve;
+        const bool far_lit = !retired && b.has() && !b.any_nan() && b.d > lh + 1e-4 + M;
         const bool need = lane_on && best_result(b, face, p) && !far_lit;
         // the object's box (tracer.go:32), then, in a first pass, the face box the decision
         // rests on (object.go:76)
@@ -1365,10 +1362,10 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
             }
         }
     }
-    if (b.has && b.d < resolve) return false;
+    if (b.has() && b.d < resolve) return false;
     // the nearest candidate (not a NaN-distance first hit, which wins regardless) lies beyond
     // lh + 1e-4 + M from o: the occluder is farther from hit than the light
-    if (b.has && !b.first_nan && b.d > lh + 1e-4 + M) return true;
+    if (b.has() && !b.first_nan() && b.d > lh + 1e-4 + M) return true;
     uint32_t face, p;
     if (!best_result(b, face, p)) return true;
     V3 world, normal;
@@ -1421,7 +1418,9 @@ __device__ __forceinline__ RGB phong(const FrameArgs& fa, const double* __restri
 // the last workgroup (two-level done count, <= 64 same-address atomics per level) folds
 // the statistic shards into WorkArgs::summary and the profiling accumulator.  Shards are
 // read with atomics (device-coherent across the XCDs' L2s).
-__device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& wa) {
+// The launch's last workgroup (the done counters, one atomic per workgroup and shard): true in
+// every thread of that workgroup only.
+__device__ __forceinline__ bool launch_last(const WorkArgs& wa) {
     __shared__ bool last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics performed
     __syncthreads();
@@ -1436,6 +1435,10 @@ __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& 
         last = l;
     }
     __syncthreads();
+    return last;
+}
+// The frame's statistics totals, by the launch's last workgroup.
+__device__ __forceinline__ void frame_summary(const FrameArgs& fa, const WorkArgs& wa, bool last) {
     if (!last || threadIdx.x >= kStatN) return;
     const int st = threadIdx.x;
     cnt_t sum = 0;
@@ -1448,6 +1451,9 @@ __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& 
     }
     wa.summary[st] = sum;
     if (wa.prof_acc && sum) atomicAdd(&wa.prof_acc[st], sum);
+}
+__device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& wa) {
+    frame_summary(fa, wa, launch_last(wa));
 }
 
 // ---------------------------------------------------------------- work distribution
@@ -1640,6 +1646,7 @@ struct LocalChunks {
     uint32_t frame;
     uint32_t* ring;     // free positions of the hit-chunk ring (bit p: position p free)
     uint16_t* pos;      // per chunk: its position in the region (< kHitRing: a ring position)
+    uint32_t* key;      // per chunk: its block's redo key (frame << 28 | block), redo_mark
 };
 
 // Hit-chunk ring (k_trace): a chunk takes the lowest free one of kHitRing positions of the
@@ -1748,6 +1755,7 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
                 base = atomicAdd(lc->count, 1u);
                 rp = ring_take(lc->ring, base);
                 lc->pos[base] = (uint16_t)rp;  // LDS, in order before the ready flag
+                lc->key[base] = blk;
             } else {
                 base = atomicAdd(lo32(&wa.counters[cnt_hits(q)]), 64u);
             }
@@ -2043,6 +2051,26 @@ __device__ __forceinline__ const ViewHead* view_lookup(const WorkArgs& wa, uint3
 
 
 
+// ---------------------------------------------------------------- deferred second passes
+// k_trace's second passes never run inside its work loop, whose registers and
+// code they would take (an inlined second pass cost ~5% of the frame, one out of line ~11 MB
+// of scratch traffic per frame, although neither runs on the benchmark's scenes).  A block
+// whose primary first pass asks for one is recorded and skipped; a shadow item that asks for
+// one records its chunk's block and publishes its first-pass bit (the block's pixels are all
+// recomputed).  The launch's last workgroup then traces every recorded block again from its
+// pixels, every query with its second pass in place (redo_block), and overwrites its outputs.
+// Keys: frame << 28 | block index in the frame's table.  Flags (WorkArgs::bmap) dedupe the
+// list (WorkArgs::bgcnt); device-scope atomics throughout (the list crosses XCDs).
+__device__ __forceinline__ void redo_mark(const WorkArgs& wa, uint32_t key) {
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t fi = (key >> 28) * wa.nblocks_frame + (key & 0x0fffffffu);
+        if (__hip_atomic_fetch_or(&wa.bmap[fi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            const uint32_t i = __hip_atomic_fetch_add(&wa.bgcnt[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wa.bgcnt[1 + i], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- shadow item
 // 64 hit slots (chunk c of region q) x light l: shadow rays from hit + 1e-4 L
 // (tracer.go:61-64), the lit bit published by atomicOr, and Phong (tracer.go:53-76) by
@@ -2055,7 +2083,7 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, bool pass2,
                                             uint32_t vf = ~0u, const ViewCache* vc = nullptr, uint32_t lim = 64,
-                                            uint32_t* ring = nullptr, uint32_t rpos = ~0u) {
+                                            uint32_t* ring = nullptr, uint32_t rpos = ~0u, uint32_t defer = ~0u) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
@@ -2088,6 +2116,10 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
         bool redo = false;
         is_lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, pass2, redo, vt,
                                                    wa.view_leaves, vh);
+        if (redo && defer != ~0u) {  // k_trace: the block is traced again at the launch's end
+            redo_mark(wa, defer);
+            redo = false;
+        }
         if (redo) {  // wave-uniform; the first pass's visits still count
             ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
             ws.nodes += vis.nodes;
@@ -2098,6 +2130,10 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
     } else {
         bool redo = false;
         Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis, pass2, redo);
+        if (redo && defer != ~0u) {  // k_trace: the block is traced again at the launch's end
+            redo_mark(wa, defer);
+            redo = false;
+        }
         if (redo) {  // wave-uniform: the item runs again with pass2 (nothing published)
             ws.tests += (cnt_t)vis.tests * __popcll(__ballot(active));
             ws.nodes += vis.nodes;
@@ -2384,51 +2420,63 @@ __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uin
 // WorkArgs::frames (staged by k_stage_frames), a one-frame launch (frames == nullptr) from rec.
 // VIEWS: the instantiation that uses view tables (MIRT_OPT_VIEWS); the default one has no
 // view code at all (present, it cost 6 spilled VGPRs and 1.7% of the frame interval).
-// k_trace's second passes, out of line: a primary block or shadow item whose
-// first pass found a winner that its face box rounds out (or a NaN distance) runs again with
-// every candidate box-gated.  They are calls from the work loop, where little is live, so the
-// inlined first passes keep the registers and code of a kernel without them (an inlined second
-// pass cost ~5% of the frame although it never runs on the benchmark's scenes).  A callee's
-// arguments arrive in VGPRs: the wave-uniform ones are made scalar again, and the frame records
-// and work description are read through the constant address space as in the kernel.
-typedef const __attribute__((address_space(4))) WorkArgs ConstWorkArgs;
-// k_trace's WorkArgs in the kernarg segment (after the first frame's record)
-constexpr size_t kTraceWaOffset = (sizeof(FrameRec) + alignof(WorkArgs) - 1) & ~(alignof(WorkArgs) - 1);
+// One recorded block traced again from its pixels (redo_mark), every query with its second pass
+// in place: primary_block's raygen, the nearest hit, one shadow query per light and phong
+// (shadow_item's arithmetic, lane by lane), and all of the block's outputs.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__device__ __attribute__((noinline)) WaveStats trace_primary_pass2(const FrameRec* frames, const WorkArgs* wap, uint32_t f,
-                                                                    uint32_t b0, uint32_t b1, uint32_t b2, uint32_t cls,
-                                                                    uint32_t frustum, const float4* frect,
-                                                                    uint32_t* stk, LocalChunks lc) {
-    frames = uni_ptr(frames);
-    const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
-    const FrameRec& fr = frame_rec(frames, uni32(f));
-    lc.count = uni_ptr(lc.count);
-    lc.ready = uni_ptr(lc.ready);
-    lc.base = (size_t)u64_uniform((uint64_t)lc.base);
-    lc.frame_of = uni_ptr(lc.frame_of);
-    lc.frame = uni32(lc.frame);
-    lc.ring = uni_ptr(lc.ring);
-    lc.pos = uni_ptr(lc.pos);
-    WaveStats ws{0, 0, 0, 0, 0};
-    PhaseClock pc;
-    primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, g_lds_mesh, uni_ptr(stk), RESIDENT,
-                                           BlockDesc{uni32(b0), uni32(b1), uni32(b2), 0u}, 0, ws, pc, true,
-                                           uni32(frustum) != 0, uni_ptr(frect), &lc, uni32(cls));
-    return ws;
-}
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__device__ __attribute__((noinline)) WaveStats trace_shadow_pass2(const FrameRec* frames, const WorkArgs* wap, uint32_t f,
-                                                                   uint32_t segment, uint64_t chunk, uint32_t l,
-                                                                   uint32_t* stk, uint32_t* ring, uint32_t rpos) {
-    frames = uni_ptr(frames);
-    const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
-    const uint32_t cf = uni32(f);
-    const FrameRec& fr = frame_rec(frames, cf);
-    WaveStats ws{0, 0, 0, 0, 0};
-    shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, g_lds_mesh, uni_ptr(stk), RESIDENT, uni32(segment) != 0,
-                                  (size_t)u64_uniform(chunk), uni32(l), ws, true, RESIDENT ? cf : ~0u, nullptr, 64,
-                                  uni_ptr(ring), uni32(rpos));
-    return ws;
+__device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes& out, const BlockDesc& bd) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lx = lane >> 3, ly = lane & 7;
+    const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, th = bd.geo & 0xffffu;
+    const uint32_t vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
+    const bool active = lx < vw && ly < vh;
+    const uint32_t i = px + (active ? lx : 0), j = py + (active ? ly : 0);
+    const V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
+    // tracer.go:15-22, :86 (primary_block's operations)
+    const double si = fa.phw * ((double)(fa.halfW - (int32_t)i) - 0.5) / (double)fa.halfW;
+    const double sj = fa.phh * ((double)(fa.halfH - (int32_t)j) - 0.5) / (double)fa.halfH;
+    V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}), scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
+               scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
+    const V3 d = norm(sub(p, cam));
+    Visits vis{0, 0, 0, 0};
+    const Nearest nh = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, g_lds_mesh, RESIDENT, cam, d, active, true, vis);
+    const bool hit = active && nh.ok;
+    const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
+    uint32_t lit = 0;
+    for (uint32_t l = 0; l < fa.n_lights; ++l) {
+        const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
+        V3 o{0, 0, 0}, sd{1, 0, 0};
+        if (hit) {
+            sd = norm(sub(lpos, nh.hit));      // tracer.go:61
+            o = add(nh.hit, scale(sd, 0.0001));  // tracer.go:64
+        }
+        bool is_lit;
+        if (segment) {
+            is_lit = shadow_lit_single_settled<PREFILTER>(fa, g_lds_mesh, RESIDENT, nullptr, nh.hit, o, sd, lpos, l, hit, vis);
+        } else {
+            const Nearest r = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, g_lds_mesh, RESIDENT, o, sd, hit, false, vis);
+            is_lit = !r.ok || len(sub(lpos, nh.hit)) < len(sub(r.hit, nh.hit));
+        }
+        if (hit && is_lit) lit |= 1u << l;
+    }
+    if (!active) return;
+    const uint64_t oidx = (uint64_t)bd.out + (uint64_t)lx * th + ly;
+    if (out.valid) out.valid[oidx] = hit ? 1 : 0;
+    if (out.face) out.face[oidx] = hit ? (int32_t)nh.face : -1;
+    if (out.object) out.object[oidx] = hit ? (int32_t)nh.obj : -1;
+    RGB col{0, 0, 0};
+    if (hit) col = phong(fa, fa.obj[nh.obj].m.mats + (size_t)nh.mat * 10, nh.hit, nh.normal, lit);
+    if (out.rgb) {
+        out.rgb[3 * oidx] = col.r;
+        out.rgb[3 * oidx + 1] = col.g;
+        out.rgb[3 * oidx + 2] = col.b;
+    }
+    if (out.rgb8) {
+        out.rgb8[3 * oidx] = c_u8(col.r);
+        out.rgb8[3 * oidx + 1] = c_u8(col.g);
+        out.rgb8[3 * oidx + 2] = c_u8(col.b);
+    }
+    if (out.rgbv) out.rgbv[oidx] = hit ? pack_rgbv(col) : 0u;
 }
 
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
@@ -2450,6 +2498,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __shared__ uint8_t chunk_frame[kBlkQ];
     __shared__ uint32_t ready[kBlkQ];
     __shared__ uint16_t chunk_pos[kBlkQ];  // each chunk's position in the region (ring_take)
+    __shared__ uint32_t chunk_key[kBlkQ];  // each chunk's block (redo_mark)
     __shared__ uint32_t s_prim, s_pdone, s_chunks, s_item, s_front, s_back, s_ring;
     __shared__ ViewHead s_vhead[VIEWS ? kMaxViewTables : 1];
     __shared__ uint32_t s_vstate[VIEWS ? kMaxViewTables : 1];
@@ -2574,7 +2623,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
         __syncthreads();
         // queued blocks: [0, s_front) and [s_back, nc); ticket q is entry q or q - nfront + s_back
         const uint32_t nfront = s_front, back0 = s_back, nq = nfront + (nc - back0);
-        LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0, &s_ring, chunk_pos};
+        LocalChunks lc{&s_chunks, ready, chunk0, chunk_frame, 0, &s_ring, chunk_pos, chunk_key};
         uint32_t pend = kNone;  // a shadow ticket held (possibly for a chunk not yet allocated)
         for (;;) {
             // 1. a shadow item of an allocated chunk
@@ -2597,12 +2646,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                 const uint32_t cf = __builtin_amdgcn_readfirstlane(chunk_frame[c]);
                 const FrameRec& fr = frame_rec(frames, cf);
                 const uint32_t cp = __builtin_amdgcn_readfirstlane(chunk_pos[c]);
-                if (shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64,
-                                                  l, wsh, false, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring,
-                                                  cp))  // the same item again, every candidate box-gated
-                    stats_add(wsh, trace_shadow_pass2<PREFILTER, BRUTE, RESIDENT>(
-                                       frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset),
-                                       cf, segment ? 1u : 0u, chunk0 + (size_t)cp * 64, l, stk, &s_ring, cp));
+                const uint32_t ck = __builtin_amdgcn_readfirstlane(chunk_key[c]);
+                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64, l, wsh,
+                                              false, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring, cp, ck);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
                 continue;
@@ -2629,12 +2675,11 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
                         vt = wa.views + (size_t)f * wa.nviews * wa.view_leaves;
                     const uint64_t cost0 = wa.block_cost ? __builtin_amdgcn_s_memtime() : 0;
                     const uint32_t cls = __builtin_amdgcn_readfirstlane(bq_cull[t]);
+                    const uint32_t key = f << 28 | __builtin_amdgcn_readfirstlane(bq_bl[t]);
                     if (primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc, false,
-                                                               use_frustum, frect[f], &lc, cls, vt, wa.view_leaves,
-                                                               &fr.fr))  // the same block again, every candidate box-gated
-                        stats_add(wp, trace_primary_pass2<PREFILTER, BRUTE, RESIDENT>(
-                                          frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset),
-                                          f, bd.out, bd.pxy, bd.geo, cls, use_frustum ? 1u : 0u, frect[f], stk, lc));
+                                                               use_frustum, frect[f], &lc, cls, vt, wa.view_leaves, &fr.fr,
+                                                               key))
+                        redo_mark(wa, key);  // traced again, from its pixels, at the launch's end
                     if (wa.block_cost && (threadIdx.x & 63) == 0) {  // this trace's time, for the slot's next frame
                         const uint64_t dc = (__builtin_amdgcn_s_memtime() - cost0) >> 6;
                         wa.block_cost[bq_bl[t]] = (uint16_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));
@@ -2670,7 +2715,26 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     __syncthreads();
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
     if (wa.timeline && !MIRT_ITEM_TRACE) clock.record(wa, 0, taken);
-    frame_fold(fa, wa);
+    const bool last = launch_last(wa);
+    if (last && wa.bgcnt) {
+        // the deferred second passes (redo_mark): every other workgroup is done
+        const uint32_t n = __hip_atomic_load(&wa.bgcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t e = threadIdx.x >> 6; e < n; e += kWG / 64) {
+            const uint32_t key = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&wa.bgcnt[1 + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const uint32_t f = key >> 28, qbl = key & 0x0fffffffu;
+            const u32x4 qv = ((const u32x4*)wa.blocks)[(size_t)(qbl % kQShards) * wa.per_shard + qbl / kQShards];
+            const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(qv[0]), (uint32_t)__builtin_amdgcn_readfirstlane(qv[1]),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(qv[2]), 0u};
+            const FrameRec& fr = frame_rec(frames, f);
+            redo_block<PREFILTER, BRUTE, RESIDENT>(fr.fa, fr.out, bd);
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store(&wa.bmap[f * wa.nblocks_frame + qbl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && n) __hip_atomic_store(&wa.bgcnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    frame_summary(fa, wa, last);
 }
 
 // ---------------------------------------------------------------- reflections (configs[4])

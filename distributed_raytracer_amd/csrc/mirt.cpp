@@ -126,6 +126,11 @@ struct Slot {
     size_t ssrc_cap = 0;
     uint32_t* bmap = nullptr;
     size_t bmap_cap = 0;
+    // k_trace's deferred second passes (WorkArgs::bmap / bgcnt in one-launch frames): [0] the
+    // count, then kMaxFrames x nblocks list entries, then as many per-block flags; zero between
+    // launches (the launch's last workgroup clears what it used)
+    uint32_t* redo = nullptr;
+    size_t redo_cap = 0;
     uint32_t* gcnt = nullptr;  // [bounces + 1][groups]: records per group of kPackGroup source chunks
     size_t gcnt_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
@@ -265,7 +270,7 @@ void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->lhits[0], (void*)s->lhits[1], (void*)s->ldir[0], (void*)s->ldir[1], (void*)s->llitw[0],
                     (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain,
-                    (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt})
+                    (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt, (void*)s->redo})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
@@ -1049,6 +1054,16 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             HIP_TRY(hipMemsetAsync(sl->bmap, 0, (size_t)sl->nblocks * sizeof(uint32_t), s));
             HIP_TRY(hipMemsetAsync(sl->gcnt, 0, (size_t)(bounces + 1) * ng * sizeof(uint32_t), s));
         }
+    }
+    if (one_launch) {
+        // the deferred second passes (k_trace's redo list): flags and list reuse
+        // the bounce-wave fields, which one-launch frames never use
+        const size_t L = (size_t)kMaxFrames * std::max<uint32_t>(sl->nblocks, 1);
+        const size_t cap0 = sl->redo_cap;
+        if ((r = dev_grow(sl->redo, sl->redo_cap, 1 + 2 * L)) != MIRT_OK) return r;
+        if (sl->redo_cap != cap0) HIP_TRY(hipMemsetAsync(sl->redo, 0, sl->redo_cap * sizeof(uint32_t), s));
+        wa.bgcnt = sl->redo;
+        wa.bmap = sl->redo + 1 + L;
     }
     if (one_launch && !getenv("MIRT_NO_COST_ORDER")) {
         const size_t cap0 = sl->cost_cap;

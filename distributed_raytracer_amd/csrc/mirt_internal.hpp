@@ -334,6 +334,8 @@ struct WorkArgs {
     uint16_t* block_cost;
     uint32_t view_tag;       // this launch's tag (nonzero, differs from the slot's previous launch)
     uint32_t view_pad;
+    // k_trace (one-launch frames): bgcnt = the deferred second passes' list ([0] count, then
+    // f << 28 | block entries) and bmap = a flag per block of the launch (zero between launches).
     // bounce waves (reflection frames without MIRT_OPT_REFLECT_CHAINS): per linear block of the table, its hit chunk
     // ((slot / 64 + 1) << 7 | hits; 0: none), written by k_primary (zeroed per frame), and the
     // hits per group of kPackGroup blocks (k_pack's prefix sums)
