@@ -2241,29 +2241,42 @@ __device__ __forceinline__ const T& split_third(const char* ka) {
     return kconst<T>(ka + kalign(kSplitWaOff + sizeof(WorkArgs), alignof(T)));
 }
 
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__device__ __attribute__((noinline)) WaveStats split_primary_pass2(const char* ka, uint32_t b0, uint32_t b1, uint32_t b2,
-                                                                    uint32_t blk, uint32_t frustum, const float4* frect,
-                                                                    uint32_t* stk) {
-    ka = uni_ptr(ka);
-    const uint32_t b = uni32(blk);
-    WaveStats ws{0, 0, 0, 0, 0};
-    PhaseClock pc;
-    primary_block<RESIDENT, PREFILTER, BRUTE>(split_fa(ka), split_wa(ka), split_third<OutPlanes>(ka), g_lds_mesh,
-                                              uni_ptr(stk), RESIDENT, BlockDesc{uni32(b0), uni32(b1), uni32(b2), 0u},
-                                              b % kQShards, ws, pc, true, uni32(frustum) != 0, uni_ptr(frect), nullptr, 0,
-                                              nullptr, 0, nullptr, b);
-    return ws;
+// The split kernels' deferred second passes (as k_trace's): a work item whose
+// first pass asks for one records itself (two words) and publishes nothing; the launch's last
+// workgroup runs every recorded item again with the second pass in place, after its own work.
+// WorkArgs::split_redo: [0] workgroups done, [1] entries, then the entries; the last
+// workgroup zeroes both counts, so the buffer is clean for the next launch.
+__device__ __forceinline__ void split_redo_push(const WorkArgs& wa, uint32_t a, uint32_t b) {
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t i = __hip_atomic_fetch_add(&wa.split_redo[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&wa.split_redo[2 + 2 * i], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&wa.split_redo[3 + 2 * i], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__device__ __attribute__((noinline)) WaveStats split_shadow_pass2(const char* ka, uint32_t segment, uint64_t chunk,
-                                                                   uint32_t l, uint32_t lim, uint32_t* stk) {
-    ka = uni_ptr(ka);
-    WaveStats ws{0, 0, 0, 0, 0};
-    shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(split_fa(ka), split_wa(ka), split_third<OutPlanes>(ka), g_lds_mesh,
-                                                   uni_ptr(stk), RESIDENT, uni32(segment) != 0,
-                                                   (size_t)u64_uniform(chunk), uni32(l), ws, true, ~0u, nullptr, uni32(lim));
-    return ws;
+// Called once by every workgroup after its work: true in the launch's last one, which then
+// reads the entries (n = the count, or 0 elsewhere).
+__device__ __forceinline__ uint32_t split_redo_last(const WorkArgs& wa) {
+    __shared__ uint32_t s_n;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's entries are stored
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_n = 0;
+        if (__hip_atomic_fetch_add(&wa.split_redo[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+            s_n = 0x80000000u | __hip_atomic_load(&wa.split_redo[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return s_n;
+}
+__device__ __forceinline__ uint32_t split_redo_entry(const WorkArgs& wa, uint32_t e, int w) {
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&wa.split_redo[2 + 2 * e + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void split_redo_reset(const WorkArgs& wa, uint32_t last) {
+    __syncthreads();
+    if (threadIdx.x == 0 && last) {
+        __hip_atomic_store(&wa.split_redo[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&wa.split_redo[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
@@ -2316,10 +2329,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
             ++taken;
             if (primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
                                                           false, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b))
-                // the same block again, every candidate box-gated, out of line (as k_trace's)
-                stats_add(ws, split_primary_pass2<PREFILTER, BRUTE, RESIDENT>((const char*)__builtin_amdgcn_kernarg_segment_ptr(),
-                                                                              bd.out, bd.pxy, bd.geo, b, use_frustum ? 1u : 0u,
-                                                                              frect, wstk[wave]));
+                split_redo_push(wa, b, 0u);  // the same block again, every candidate box-gated, at the launch's end
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -2334,6 +2344,18 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     if (mine == 0) {
         __syncthreads();
         clock.mark_staged();
+    }
+    if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
+        const uint32_t last = split_redo_last(wa);
+        for (uint32_t e = wave; e < (last & 0x7fffffffu); e += kWG / 64) {
+            const uint32_t b = split_redo_entry(wa, e, 0);
+            const u32x4 v = ((const u32x4*)wa.blocks)[(size_t)(b % kQShards) * wa.per_shard + b / kQShards];
+            const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(v[0]), (uint32_t)__builtin_amdgcn_readfirstlane(v[1]),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(v[2]), 0u};
+            primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc, true,
+                                                      use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b);
+        }
+        split_redo_reset(wa, last);
     }
     stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, ws);
     if (MIRT_PHASE_TIMING) {  // record [4], [5], [6] = cycles in setup+raygen, trace, outputs
@@ -2383,13 +2405,20 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
                                                               (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, false, ~0u,
                                                               nullptr, min(64u, nrec - c * 64)))
-                // the same item again, every candidate box-gated, out of line (as k_trace's)
-                stats_add(ws, split_shadow_pass2<PREFILTER, BRUTE, RESIDENT>(
-                                  (const char*)__builtin_amdgcn_kernarg_segment_ptr(), segment ? 1u : 0u,
-                                  (size_t)q * wa.hit_cap + (size_t)c * 64, l, min(64u, nrec - c * 64),
-                                  wstk[threadIdx.x >> 6]));
+                // the same item again, every candidate box-gated, at the launch's end (not counted
+                // done, so its chunk is shaded then)
+                split_redo_push(wa, (uint32_t)((size_t)q * wa.hit_cap / 64 + c), l | min(64u, nrec - c * 64) << 8);
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
+    }
+    if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
+        const uint32_t last = split_redo_last(wa);
+        for (uint32_t e = threadIdx.x >> 6; e < (last & 0x7fffffffu); e += kWG / 64) {
+            const uint32_t ch = split_redo_entry(wa, e, 0), w1 = split_redo_entry(wa, e, 1);
+            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+                                                          (size_t)ch * 64, w1 & 0xffu, ws, true, ~0u, nullptr, w1 >> 8);
+        }
+        split_redo_reset(wa, last);
     }
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
@@ -2986,19 +3015,6 @@ __device__ __forceinline__ bool bounce_chunk(const FrameArgs& fa, const WorkArgs
         }
     return false;
 }
-struct BounceOut {
-    WaveStats ws;
-    cnt_t rays, shadow_rays;
-};
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-__device__ __attribute__((noinline)) BounceOut bounce_pass2(const char* ka, uint32_t q, uint32_t k, uint32_t n,
-                                                             uint32_t cp) {
-    ka = uni_ptr(ka);
-    BounceOut r{{0, 0, 0, 0, 0}, 0, 0};
-    bounce_chunk<PREFILTER, BRUTE, RESIDENT>(split_fa(ka), split_wa(ka), split_third<BounceArgs>(ka), g_lds_mesh, uni32(q),
-                                             uni32(k), uni32(n), uni32(cp), true, r.ws, r.rays, r.shadow_rays);
-    return r;
-}
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
 MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const BounceArgs ba) {
     double* const lds = g_lds_mesh;
@@ -3018,16 +3034,19 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
         const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]), nch = (n + 63) / 64;
         for (uint32_t k = sc.rank(); k < nch;) {
-            if (bounce_chunk<PREFILTER, BRUTE, RESIDENT>(fa, wa, ba, lds, q, k, n, cp, false, ws, rays, shadow_rays)) {
-                // the same chunk again, every candidate box-gated, out of line (as k_trace's)
-                const BounceOut r2 = bounce_pass2<PREFILTER, BRUTE, RESIDENT>(
-                    (const char*)__builtin_amdgcn_kernarg_segment_ptr(), q, k, n, cp);
-                stats_add(ws, r2.ws);
-                rays += r2.rays;
-                shadow_rays += r2.shadow_rays;
-            }
+            if (bounce_chunk<PREFILTER, BRUTE, RESIDENT>(fa, wa, ba, lds, q, k, n, cp, false, ws, rays, shadow_rays))
+                split_redo_push(wa, q, k);  // the same chunk again, every candidate box-gated, at the launch's end
             k += sc.peers();
         }
+    }
+    if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
+        const uint32_t last = split_redo_last(wa);
+        for (uint32_t e = threadIdx.x >> 6; e < (last & 0x7fffffffu); e += kWG / 64) {
+            const uint32_t q = split_redo_entry(wa, e, 0), k = split_redo_entry(wa, e, 1);
+            const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]);
+            bounce_chunk<PREFILTER, BRUTE, RESIDENT>(fa, wa, ba, lds, q, k, n, cp, true, ws, rays, shadow_rays);
+        }
+        split_redo_reset(wa, last);
     }
     WaveStats extra{rays, (uint32_t)shadow_rays, 0, 0, 0};  // per wave: well below 2^32
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);

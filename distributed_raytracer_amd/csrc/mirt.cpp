@@ -131,6 +131,9 @@ struct Slot {
     // launches (the launch's last workgroup clears what it used)
     uint32_t* redo = nullptr;
     size_t redo_cap = 0;
+    // the split kernels' deferred second passes (WorkArgs::split_redo), zero between launches
+    uint32_t* sredo = nullptr;
+    size_t sredo_cap = 0;
     uint32_t* gcnt = nullptr;  // [bounces + 1][groups]: records per group of kPackGroup source chunks
     size_t gcnt_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
@@ -270,7 +273,7 @@ void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : {(void*)s->lhits[0], (void*)s->lhits[1], (void*)s->ldir[0], (void*)s->ldir[1], (void*)s->llitw[0],
                     (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain,
-                    (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt, (void*)s->redo})
+                    (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt, (void*)s->redo, (void*)s->sredo})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
@@ -1151,6 +1154,17 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             HIP_TRY(hipEventRecord(pr.ev[2], s));
         }
     } else {
+        // the split kernels' deferred second passes: one entry per block (k_primary), per
+        // (chunk, light) item (k_shadow) or per chunk (k_bounce), the launch's last workgroup
+        // running them
+        {
+            const size_t items = std::max<size_t>({(size_t)sl->nblocks, (size_t)(wa.hit_cap / 64) * kQShards *
+                                                                        std::max<uint32_t>(nl, 1), 1});
+            const size_t cap0 = sl->sredo_cap;
+            if ((r = dev_grow(sl->sredo, sl->sredo_cap, 2 + 2 * items)) != MIRT_OK) return r;
+            if (sl->sredo_cap != cap0) HIP_TRY(hipMemsetAsync(sl->sredo, 0, sl->sredo_cap * sizeof(uint32_t), s));
+            wa.split_redo = sl->sredo;
+        }
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
         HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));

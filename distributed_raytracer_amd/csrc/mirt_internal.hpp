@@ -324,7 +324,12 @@ struct WorkArgs {
     uint32_t nblocks_frame;  // nblocks = nframes * nblocks_frame; the table describes one frame
     // view tables (k_trace, one-object frames, nullptr: none): frame f, view v at
     // views + (f * nviews + v) * nleaves, its header at view_heads[f * nviews + v]
-    ViewLeaf* views;
+    union {
+        ViewLeaf* views;
+        // split kernels (k_primary, k_shadow, k_bounce; never with view tables): their deferred
+        // second passes, [0] workgroups done, [1] entries, then two words per entry
+        uint32_t* split_redo;
+    };
     ViewHead* view_heads;
     uint32_t nviews;         // 1 + lights
     uint32_t view_leaves;    // leaves per table
