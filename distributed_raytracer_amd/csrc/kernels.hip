@@ -2508,6 +2508,29 @@ __device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes&
     if (out.rgbv) out.rgbv[oidx] = hit ? pack_rgbv(col) : 0u;
 }
 
+// One entry of k_trace's redo list (redo_mark), out of line: a call at the kernel's end, where
+// nothing of the work loop is live, keeps the second passes' code and registers out of the
+// kernel body (its SGPR allocation).  Arguments are made scalar again, the frame records and
+// the work description read through the constant address space.
+typedef const __attribute__((address_space(4))) WorkArgs ConstWorkArgs;
+constexpr size_t kTraceWaOffset = kalign(sizeof(FrameRec), alignof(WorkArgs));  // k_trace's second argument
+template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+__device__ __attribute__((noinline)) void trace_redo_entry(const FrameRec* frames, const WorkArgs* wap, uint32_t e) {
+    frames = uni_ptr(frames);
+    const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
+    e = uni32(e);
+    const uint32_t key = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&wa.bgcnt[1 + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t f = key >> 28, qbl = key & 0x0fffffffu;
+    const u32x4 qv = ((const u32x4*)wa.blocks)[(size_t)(qbl % kQShards) * wa.per_shard + qbl / kQShards];
+    const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(qv[0]), (uint32_t)__builtin_amdgcn_readfirstlane(qv[1]),
+                       (uint32_t)__builtin_amdgcn_readfirstlane(qv[2]), 0u};
+    const FrameRec& fr = frame_rec(frames, f);
+    redo_block<PREFILTER, BRUTE, RESIDENT>(fr.fa, fr.out, bd);
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(&wa.bmap[f * wa.nblocks_frame + qbl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
 MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     const FrameArgs& fa = rec.fa;
@@ -2748,18 +2771,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
     if (last && wa.bgcnt) {
         // the deferred second passes (redo_mark): every other workgroup is done
         const uint32_t n = __hip_atomic_load(&wa.bgcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t e = threadIdx.x >> 6; e < n; e += kWG / 64) {
-            const uint32_t key = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&wa.bgcnt[1 + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const uint32_t f = key >> 28, qbl = key & 0x0fffffffu;
-            const u32x4 qv = ((const u32x4*)wa.blocks)[(size_t)(qbl % kQShards) * wa.per_shard + qbl / kQShards];
-            const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(qv[0]), (uint32_t)__builtin_amdgcn_readfirstlane(qv[1]),
-                               (uint32_t)__builtin_amdgcn_readfirstlane(qv[2]), 0u};
-            const FrameRec& fr = frame_rec(frames, f);
-            redo_block<PREFILTER, BRUTE, RESIDENT>(fr.fa, fr.out, bd);
-            if ((threadIdx.x & 63) == 0)
-                __hip_atomic_store(&wa.bmap[f * wa.nblocks_frame + qbl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (uint32_t e = threadIdx.x >> 6; e < n; e += kWG / 64)
+            trace_redo_entry<PREFILTER, BRUTE, RESIDENT>(
+                frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset), e);
         __syncthreads();
         if (threadIdx.x == 0 && n) __hip_atomic_store(&wa.bgcnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
