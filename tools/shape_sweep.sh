@@ -12,5 +12,5 @@ import json, sys
 d = json.loads([l for l in open('$LOG').read().splitlines() if l.startswith('{')][-1])
 print(json.dumps({'F': $F, 'B': $B, 'steps': $STEPS, 'ms_per_step': d['ms_per_step'],
                   'device_ms': d['device_ms_per_frame'], 'latency_ms': d['frame_latency_ms'],
-                  'launch_ms': d['roofline']['launch_ms']}))"
+                  'launch_ms': d['roofline'].get('launch_ms', d['roofline'].get('algorithmic', {}).get('launch_ms'))}))"
 done
