@@ -3041,7 +3041,6 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     const ShardCursor sc;
     WaveStats ws{0, 0, 0, 0, 0};
     cnt_t rays = 0, shadow_rays = 0;
-    const uint32_t lv = ba.level;
     // chunks per region of the input, as k_pack published it (high word of its region counts):
     // input chunk (q, k) is source chunk q * cp + k of k_pack
     const uint32_t cp = (uint32_t)(ba.in_cnt[cnt_hits(0)] >> 32);
