@@ -3037,7 +3037,6 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
         stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
         __syncthreads();
     }
-    const uint32_t lane = threadIdx.x & 63;
     const ShardCursor sc;
     WaveStats ws{0, 0, 0, 0, 0};
     cnt_t rays = 0, shadow_rays = 0;
