@@ -7,9 +7,9 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DRIVER = "profiles/r03z_bench_driver_cmd.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
-LINES = [DRIVER, "profiles/r03z_bench_default.log", "profiles/r03z_bench_orbit.log", "profiles/r03z_bench_brute.log",
-         "profiles/r03z_bench_config3.log", "profiles/r03z_bench_config4.log"]
+DRIVER = "profiles/r04f_bench_bench.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
+LINES = [DRIVER, "profiles/r04f_bench_bench500.log", "profiles/r04d_bench_orbit.log", "profiles/r04d_bench_brute.log",
+         "profiles/r04f_bench_config3.log", "profiles/r04f_bench_config4.log", "profiles/r03z_bench_driver_cmd.log"]
 
 
 def _line(path):
