@@ -311,3 +311,44 @@ def test_object_box_certificate_cameras_match_rtree(ctx):
             assert np.array_equal(getattr(fb2, key), b), f"camera {k} (no certificate): {key}"
         n += int(ref["valid"].sum())
     assert n > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [None, 8])
+def test_deferred_second_passes_in_multi_frame_launches(ctx, tile):
+    """k_trace defers a block's second pass to the launch's last workgroup (redo_mark, keys
+    frame << 28 | block): vertex-light soups, whose rays through box corners need second passes,
+    traced by a frame group with four frames per launch (frames 1..3 of a launch carry nonzero
+    frame fields in their keys), whole-screen and in 8-px strips, equal the R-tree oracle for
+    every frame; the split kernels' deferral is checked on the same soups by
+    test_vertex_light_soups_match_rtree_oracle."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    from oracle.oracle import Oracle
+    from scenes import gpu_env, soup_scene, with_camera
+    W, H = 64, 48
+    for seed in (12, 17):
+        sc = soup_scene(seed, vertex_light=True)
+        env = gpu_env(ctx, sc)
+        base = env.mutable()
+        rng = np.random.default_rng(seed)
+        scenes, frames = [], []
+        for _ in range(4):
+            s = with_camera(sc, np.asarray(sc.cam_pos) + rng.normal(scale=0.3, size=3), sc.cam_dir)
+            scenes.append(s)
+            frames.append(rt.EnvMutables(base.objects, base.lights, rt.Camera.new(s.cam_pos, s.cam_dir, s.fov)).to_frame())
+        refs = [Oracle(s, culling="rtree").frame(W, H, nthreads=8) for s in scenes]
+        g = NativeFrameGroup(ctx, W, H, 0, 1, tile, inflight=8, batch=4)
+        try:
+            order = [0, 1, 2, 3, 3, 2, 1, 0]
+            for q in order:
+                g.render(frames[q])
+            g.flush()
+            torch.cuda.synchronize()
+            for k, q in enumerate(order):
+                got = g.frames[k % 8]
+                assert np.array_equal(got.valid.cpu().numpy(), refs[q]["valid"]), f"seed {seed} frame {k} valid"
+                assert np.array_equal(got.rgb8.cpu().numpy(), refs[q]["rgb8"]), f"seed {seed} frame {k} rgb8"
+        finally:
+            g.close()
