@@ -72,7 +72,7 @@ def find_profile(path: str, shape: dict):
 
 
 def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch, launch_ms,
-                   mesh_lds_resident, alg_kernel=None):
+                   mesh_lds_resident, alg_kernel=None, launch_ms_mean=None):
     """`roofline` of the bench line: the PHYSICAL binding roof of the frame kernel.  The
     kernels are fp64 VALU code whose mesh sits in LDS (suzanne) or streams from L2/HBM
     (configs[3]); the committed PMC passes of this exact command (profiles/) show the VALU as
@@ -87,11 +87,14 @@ def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per
     alg = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4),
            "kind": "algorithmic (north star): 72 B fp64 triangle record x ray-triangle tests performed "
-                   "(device counter) per launch / mean HIP-event duration of the launch" + (
+                   "(device counter) per launch / median HIP-event duration of the profiled region's "
+                   "launches (the mean, launch_ms_mean, counts a launch that waited behind an overlapped "
+                   "one)" + (
                        "; the mesh is LDS-resident, so these bytes are LDS reads, not HBM traffic"
                        if mesh_lds_resident else "; the mesh is HBM-resident (scalar loads through L2/MALL)"),
            "kernel": alg_kernel or kname, "bytes_per_unit": BYTES_PER_TRI_TEST, "units_per_launch": int(k_tests),
-           "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(launch_ms, 4)}
+           "frames_per_launch": round(frames_per_launch, 3), "launch_ms": round(launch_ms, 4),
+           "launch_ms_mean": None if launch_ms_mean is None else round(launch_ms_mean, 4)}
     if not pj or "sq_insts_valu_per_launch" not in pj:
         out = dict(alg)
         out["kernel"], out["kernels"] = kname, alg["kernel"]  # the dominant kernel names the shape
@@ -561,6 +564,9 @@ def main():
         rays_per_frame = primary + shadow + refl  # per frame, all ranks (device counters)
         nlaunch = max(prof["launches"], 1)
         prim_ms = prof["primary_ms_sum"] / nlaunch
+        # the algorithmic roofline's launch time: the median launch (a mean counts the odd launch
+        # that queued behind an overlapped frame: 665 us against a 191 us rocprof average, r03z)
+        prim_med = prof["primary_ms_median"] or prim_ms
         # the dominant kernel: k_trace (the whole frame, one launch); split frames: k_primary;
         # reflection frames: k_shadow (level 0 and each bounce level: the most time per frame,
         # profiles/r03config4_kernel_stats.csv), or k_reflect on the chain path (2.67 of 3.81 ms)
@@ -570,12 +576,13 @@ def main():
             # the algorithmic figure over all the frame's kernels: the reflection levels' tests are
             # counted with the shadow rays' (one statistic), so the whole frame's tests / its time
             k_tests = (prof["primary_tri_tests"] + prof["shadow_tri_tests"]) / nlaunch
-            alg_ms = prof["frame_ms_sum"] / nlaunch
+            alg_ms = prof["frame_ms_median"] or prof["frame_ms_sum"] / nlaunch
+            alg_mean = prof["frame_ms_sum"] / nlaunch
             alg_kernel = ("k_primary + k_shadow + k_reflect" if a.reflect_chains else
                           "k_primary + k_pack + k_bounce + k_shadow (levels 0..bounces) + k_refl_fold")
         else:
             k_tests = (prof["primary_tri_tests"] + (prof["shadow_tri_tests"] if one else 0)) / nlaunch
-            alg_ms, alg_kernel = prim_ms, kname
+            alg_ms, alg_kernel, alg_mean = prim_med, kname, prim_ms
         achieved = k_tests * BYTES_PER_TRI_TEST / (alg_ms / 1e3) / 1e9
         shape = {"width": W, "height": H, "gpus": world, "inflight": a.inflight, "batch": a.batch,
                  "steps": steps, "warmup": a.warmup, "d2h": d2h, "kernel": kname,
@@ -636,7 +643,8 @@ def main():
             "launches": launches,
             "light_cache": ctx.light_cache_stats(),
             "roofline": roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per_launch,
-                                       alg_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES, alg_kernel=alg_kernel),
+                                       alg_ms, mesh_lds_resident=tris <= LDS_RESIDENT_FACES, alg_kernel=alg_kernel,
+                                       launch_ms_mean=alg_mean),
         }
         # north_star's own target: the brute-force work, bytes/tri-test x tris
         # x rays, over the frame interval, against >= 40% of the per-GPU HBM roofline.  Culling

@@ -87,7 +87,7 @@ class Profile(C.Structure):
                 ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64),
                 ("stack_overflows", C.c_uint64), ("reflection_rays", C.c_uint64), ("reflect_ms_sum", C.c_double),
-                ("frames", C.c_uint64)]
+                ("frames", C.c_uint64), ("primary_ms_median", C.c_double), ("frame_ms_median", C.c_double)]
 
 
 class MeshView(C.Structure):

@@ -1778,6 +1778,9 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         recs.swap(c->prof_pending);
     }
     memset(out, 0, sizeof(*out));
+    std::vector<float> prim, whole;
+    prim.reserve(recs.size());
+    whole.reserve(recs.size());
     for (auto& r : recs) {
         HIP_TRY(hipEventSynchronize(r.ev[3]));
         float a = 0, b = 0, d = 0, t = 0;
@@ -1792,7 +1795,19 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->reflect_ms_sum += d;
         out->frame_ms_sum += t;
         out->primary_rays += r.pixels;
+        prim.push_back(a);
+        whole.push_back(t);
     }
+    auto median = [](std::vector<float>& v) -> double {
+        if (v.empty()) return 0.0;
+        size_t h = v.size() / 2;
+        std::nth_element(v.begin(), v.begin() + h, v.end());
+        double m = v[h];
+        if (v.size() % 2 == 0) m = 0.5 * (m + *std::max_element(v.begin(), v.begin() + h));
+        return m;
+    };
+    out->primary_ms_median = median(prim);
+    out->frame_ms_median = median(whole);
     if (c->prof_acc) {
         cnt_t acc[kStatN];
         HIP_TRY(hipMemcpy(acc, c->prof_acc, sizeof(acc), hipMemcpyDeviceToHost));

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 5
+#define MIRT_ABI_VERSION 6
 
 /* error codes */
 #define MIRT_OK 0
@@ -156,6 +156,9 @@ typedef struct {
     /* frames traced (a frame group launches up to 8 frames at once: per-frame figures
        divide by frames, per-launch kernel times by launches) */
     uint64_t frames;
+    /* ABI 6: medians over the read's launches of the first kernel's and the whole launch's
+       HIP-event durations (robust to a launch that waited behind an overlapped one) */
+    double primary_ms_median, frame_ms_median;
 } mirt_profile;
 
 int mirt_abi_version(void);

@@ -497,6 +497,10 @@ def test_profile_counters(ctx, env):
     assert b["primary_tri_tests"] == 76800 * 968 and b["shadow_tri_tests"] == 3 * 5820 * 968
     assert 0 < p["primary_tri_tests"] < 2 * 76800 * 968 / 5
     assert p["primary_ms_sum"] > 0 and p["frame_ms_sum"] >= p["primary_ms_sum"]
+    # two launches: the median is their mean; one launch: the launch itself
+    assert p["frame_ms_median"] == pytest.approx(p["frame_ms_sum"] / 2, rel=1e-5)
+    assert b["frame_ms_median"] == pytest.approx(b["frame_ms_sum"], rel=1e-5)
+    assert 0 < p["primary_ms_median"] <= p["frame_ms_median"] * (1 + 1e-6)
     assert p["stack_overflows"] == 0 and b["stack_overflows"] == 0
 
 
