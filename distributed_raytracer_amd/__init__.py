@@ -11,10 +11,10 @@ from ._lib import MirtError
 
 _lib.lib()  # fail loudly at import if the HIP library was not built
 
-from .tracer import (RGB, Camera, Context, EnvMutables, Environment, Framebuffer, Light,  # noqa: E402
+from .tracer import (RGB, Box, Camera, Context, EnvMutables, Environment, Framebuffer, Light,  # noqa: E402
                      SceneObject, TraceResults, Tracer, WorkOrder, draw, load_scene_arrays, trace,
                      trace_rays, trace_tile)
 
-__all__ = ["MirtError", "RGB", "Camera", "Context", "EnvMutables", "Environment", "Framebuffer", "Light",
+__all__ = ["MirtError", "RGB", "Box", "Camera", "Context", "EnvMutables", "Environment", "Framebuffer", "Light",
            "SceneObject", "TraceResults", "Tracer", "WorkOrder", "draw", "load_scene_arrays", "trace",
            "trace_rays", "trace_tile"]

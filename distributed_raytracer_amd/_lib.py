@@ -87,7 +87,8 @@ class Profile(C.Structure):
                 ("primary_node_visits", C.c_uint64), ("primary_leaf_visits", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_leaf_visits", C.c_uint64),
                 ("stack_overflows", C.c_uint64), ("reflection_rays", C.c_uint64), ("reflect_ms_sum", C.c_double),
-                ("frames", C.c_uint64), ("primary_ms_median", C.c_double), ("frame_ms_median", C.c_double)]
+                ("frames", C.c_uint64), ("primary_ms_median", C.c_double), ("frame_ms_median", C.c_double),
+                ("redo_items", C.c_uint64)]
 
 
 class MeshView(C.Structure):
@@ -108,6 +109,7 @@ class MirtError(RuntimeError):
 _P = C.c_void_p
 SIGNATURES = {
     "mirt_abi_version": (C.c_int, []),
+    "mirt_build_id": (C.c_char_p, []),
     "mirt_last_error": (C.c_char_p, []),
     "mirt_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "mirt_destroy": (None, [_P]),
@@ -173,7 +175,23 @@ SIGNATURES = {
     "mirt_scene_from_gob": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "mirt_scene_link_gob": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "mirt_gob_json": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    # one process driving the GPUs of a box (ABI 7)
+    "mirt_device_count": (C.c_int, []),
+    "mirt_box_create": (C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    "mirt_box_destroy": (None, [_P]),
+    "mirt_box_size": (C.c_int, [_P]),
+    "mirt_box_ctx": (_P, [_P, C.c_uint32]),
+    "mirt_box_set_transport": (C.c_int, [_P, C.c_int]),
+    "mirt_box_transport": (C.c_int, [_P]),
+    "mirt_box_set_strip": (C.c_int, [_P, C.c_uint32]),
+    "mirt_box_set_options": (C.c_int, [_P, C.c_uint32]),
+    "mirt_box_mesh_upload": (C.c_int, [_P, _P, C.c_uint32, _P, C.c_uint32, _P, _P, _P, C.c_uint32,
+                                       C.POINTER(Material), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "mirt_box_mesh_release": (C.c_int, [_P, C.c_uint32]),
+    "mirt_box_trace_tile": (C.c_int, [_P, C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_uint32, C.POINTER(Outputs), _P, C.POINTER(Stats)]),
 }
+MIRT_BOX_RCCL, MIRT_BOX_COPY, MIRT_BOX_HOST = 1, 2, 3
 
 _lib = None
 

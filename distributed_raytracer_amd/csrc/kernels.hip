@@ -2276,6 +2276,8 @@ __device__ __forceinline__ void split_redo_reset(const WorkArgs& wa, uint32_t la
     if (threadIdx.x == 0 && last) {
         __hip_atomic_store(&wa.split_redo[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&wa.split_redo[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wa.prof_acc && (last & 0x7fffffffu))  // mirt_profile.redo_items
+            atomicAdd(&wa.prof_acc[kProfRedo], (cnt_t)(last & 0x7fffffffu));
     }
 }
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
@@ -2775,7 +2777,10 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRec rec, const WorkArgs wa) {
             trace_redo_entry<PREFILTER, BRUTE, RESIDENT>(
                 frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset), e);
         __syncthreads();
-        if (threadIdx.x == 0 && n) __hip_atomic_store(&wa.bgcnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0 && n) {
+            __hip_atomic_store(&wa.bgcnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wa.prof_acc) atomicAdd(&wa.prof_acc[kProfRedo], (cnt_t)n);  // mirt_profile.redo_items
+        }
     }
     frame_summary(fa, wa, last);
 }

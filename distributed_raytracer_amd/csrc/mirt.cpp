@@ -25,6 +25,7 @@
 #include "mirt_internal.hpp"
 #include "lighttab.hpp"
 #include "bvh.hpp"
+#include "host_internal.hpp"
 
 using namespace mirt;
 
@@ -191,7 +192,7 @@ struct mirt_ctx {
     bool profiling = false;
     std::vector<ProfRec> prof_pending;
     std::vector<ProfRec> prof_free;
-    cnt_t* prof_acc = nullptr;     // kStatN device totals accumulated while profiling
+    cnt_t* prof_acc = nullptr;     // kProfN device totals accumulated while profiling
     uint64_t* timeline = nullptr;  // MIRT_OPT_TIMELINE buffer (2 kernels x timeline_cap waves)
     uint32_t timeline_cap = 0;
     // Light tables of one-object frames (light_table): an LRU cache of device tables keyed by
@@ -209,6 +210,10 @@ struct mirt_ctx {
         hipEvent_t ready = nullptr;     // recorded after the build
         bool ready_seen = false;        // `ready` has completed
         uint64_t last_use = 0;          // lt_clock at the last light_table() returning it
+        // frame records holding the table that have not been launched yet (light_table() takes
+        // a pin, lt_unpin gives it back after the launch or on the record's error path): a
+        // pinned table is never evicted
+        uint32_t pins = 0;
         // per stream whose frames read it: an event re-recorded after each such launch (the
         // library owns the events, so a reader stream may be destroyed meanwhile)
         std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
@@ -749,15 +754,13 @@ void light_records(const double* T, uint32_t n, double scale, const double pos[3
 // key reserves a buffer (a dead table's of the same size once its readers are done, else
 // hipMalloc) and is built by k_light_table on the stream of the first frame that reads it
 // (lt_launch) — no host work proportional to the mesh on the issue path.  Past the cap
-// (mirt_set_light_cache, default 4 GiB) the least recently used table whose last use is more
-// than kLtPinUses calls old is evicted: the events re-recorded after every launch that read it
-// (one per reader stream, lt_after) mark the point after which its buffer is free.  Only when
-// nothing is evictable (every table in use
-// by the frames being issued) does a frame trace without a table; the fallbacks are counted
-// (mirt_light_cache_stats), so a disabled prefilter is never silent.
-// tables returned by the last kLtPinUses calls may belong to frames not launched yet (a
-// group's open batch holds at most kMaxFrames; one-call paths launch at once)
-constexpr uint64_t kLtPinUses = 2 * kMaxFrames;
+// (mirt_set_light_cache, default 4 GiB) the least recently used table that no unlaunched frame
+// record holds (LightTab::pins: taken by light_table(), returned by lt_unpin once the record
+// has been launched or dropped) is evicted: the events re-recorded after every launch that read
+// it (one per reader stream, lt_after) mark the point after which its buffer is free.  Only when
+// nothing is evictable (every table pinned by frames being issued) does a frame trace without a
+// table; the fallbacks are counted (mirt_light_cache_stats), so a disabled prefilter is never
+// silent.
 hipEvent_t lt_event(mirt_ctx* c) {
     if (!c->lt_events.empty()) {
         hipEvent_t e = c->lt_events.back();
@@ -829,6 +832,7 @@ const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) 
         if (t->mesh == mid && t->nl == fa.n_lights && !memcmp(t->pos, fa.obj[0].pos, sizeof(t->pos)) &&
             !memcmp(t->lpos, fa.lpos, sizeof(double) * 3 * fa.n_lights)) {
             t->last_use = now;
+            ++t->pins;
             ++c->lt_stat[1];
             return t->d;
         }
@@ -837,16 +841,16 @@ const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) 
     if (n == 0) return nullptr;
     const size_t bytes = (size_t)nl * n * kLtD * sizeof(float);
     float* buf = lt_reap(c, bytes);
-    // make room: least recently used first, never a table of the last kLtPinUses calls, and
-    // no more once retired tables still being read would make the room (their buffers come
-    // back to a later frame; this one traces without a table meanwhile)
+    // make room: least recently used first, never a pinned table, and no more once retired
+    // tables still being read would make the room (their buffers come back to a later frame;
+    // this one traces without a table meanwhile)
     while (!buf && c->ltab_bytes + bytes > c->lt_cap) {
         size_t retiring = 0;
         for (const auto& t : c->lt_dead) retiring += t.bytes;
         if (retiring >= bytes) break;
         size_t best = c->ltabs.size();
         for (size_t i = 0; i < c->ltabs.size(); ++i)
-            if (now - c->ltabs[i]->last_use > kLtPinUses &&
+            if (c->ltabs[i]->pins == 0 &&
                 (best == c->ltabs.size() || c->ltabs[i]->last_use < c->ltabs[best]->last_use))
                 best = i;
         if (best == c->ltabs.size()) break;
@@ -869,9 +873,31 @@ const float* light_table(mirt_ctx* c, const mirt_frame* f, const FrameArgs& fa) 
     lt->d = buf;
     lt->bytes = bytes;
     lt->last_use = now;
+    lt->pins = 1;
     c->ltabs.push_back(std::move(lt));
     return buf;
 }
+// A frame record that held `tab` (light_table) was launched or dropped.
+void lt_unpin(mirt_ctx* c, const float* tab) {
+    if (!tab) return;
+    std::lock_guard<std::mutex> g(c->lt_mu);
+    for (auto& tp : c->ltabs)
+        if (tp->d == tab) {
+            if (tp->pins) --tp->pins;
+            return;
+        }
+}
+// The pins of up to kMaxFrames frame records, returned when the holder goes out of scope.
+struct LtPins {
+    mirt_ctx* c;
+    const float* tab[kMaxFrames] = {};
+    uint32_t n = 0;
+    explicit LtPins(mirt_ctx* c_) : c(c_) {}
+    void add(const float* t) { tab[n++] = t; }
+    ~LtPins() {
+        for (uint32_t i = 0; i < n; ++i) lt_unpin(c, tab[i]);
+    }
+};
 // Before frames reading `tab` launch on stream s: build it there if nobody has (stream order
 // then covers this stream; other streams wait for its `ready` event until it has completed),
 // and remember s as a reader for eviction.
@@ -906,7 +932,7 @@ int lt_launch(mirt_ctx* c, const float* tab, hipStream_t s) {
         }
         return MIRT_OK;
     }
-    return fail(MIRT_E_INVALID, "light table not in the cache");  // cannot happen (pinned by kLtPinUses)
+    return fail(MIRT_E_INVALID, "light table not in the cache");  // cannot happen (pinned until launched)
 }
 // After the frames reading `tab` were enqueued on s: the table's event for s marks their end.
 int lt_after(mirt_ctx* c, const float* tab, hipStream_t s) {
@@ -962,6 +988,8 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
     int r = check_tiles(W, H, tiles, n, pixels);
     if (r != MIRT_OK) return r;
     frame_record(c, f, W, H, out, sl->h_frames[0], tris);
+    LtPins pin(c);  // the record's light table, held until it has been launched
+    pin.add(sl->h_frames[0].fa.ltab);
     if ((r = launch_frames(c, sl, 1, W, H, tiles, n, f->max_bounces, s, cancel)) != MIRT_OK) return r;
     *pixels_out = pixels;
     *tris_out = tris;
@@ -1526,13 +1554,13 @@ int mirt_set_light_cache(mirt_ctx* c, uint64_t max_bytes) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
     std::lock_guard<std::mutex> g(c->lt_mu);
     c->lt_cap = (size_t)max_bytes;
-    // shrink to the new cap now: least recently used first, never a table of the last
-    // kLtPinUses calls; retired buffers are freed once their readers are done (lt_reap)
+    // shrink to the new cap now: least recently used first, never a pinned table; retired
+    // buffers are freed once their readers are done (lt_reap)
     (void)lt_reap(c, 0);
     while (c->ltab_bytes > c->lt_cap) {
         size_t best = c->ltabs.size();
         for (size_t i = 0; i < c->ltabs.size(); ++i)
-            if (c->lt_clock - c->ltabs[i]->last_use > kLtPinUses &&
+            if (c->ltabs[i]->pins == 0 &&
                 (best == c->ltabs.size() || c->ltabs[i]->last_use < c->ltabs[best]->last_use))
                 best = i;
         if (best == c->ltabs.size()) break;
@@ -1762,8 +1790,8 @@ int mirt_profile_enable(mirt_ctx* c, int enable) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
     HIP_TRY(hipSetDevice(c->device));
     if (enable && !c->prof_acc) {
-        HIP_TRY(hipMalloc((void**)&c->prof_acc, kStatN * sizeof(cnt_t)));
-        HIP_TRY(hipMemset(c->prof_acc, 0, kStatN * sizeof(cnt_t)));
+        HIP_TRY(hipMalloc((void**)&c->prof_acc, kProfN * sizeof(cnt_t)));
+        HIP_TRY(hipMemset(c->prof_acc, 0, kProfN * sizeof(cnt_t)));
     }
     c->profiling = enable != 0;
     return MIRT_OK;
@@ -1809,7 +1837,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
     out->primary_ms_median = median(prim);
     out->frame_ms_median = median(whole);
     if (c->prof_acc) {
-        cnt_t acc[kStatN];
+        cnt_t acc[kProfN];
         HIP_TRY(hipMemcpy(acc, c->prof_acc, sizeof(acc), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemset(c->prof_acc, 0, sizeof(acc)));
         out->hits = acc[kStatHits];
@@ -1822,6 +1850,7 @@ int mirt_profile_read(mirt_ctx* c, mirt_profile* out) {
         out->shadow_leaf_visits = acc[kStatShadowLeaves];
         out->stack_overflows = acc[kStatOverflow];
         out->reflection_rays = acc[kStatReflRays];
+        out->redo_items = acc[kProfRedo];
     }
     std::lock_guard<std::mutex> g(c->mu);
     for (auto& r : recs) c->prof_free.push_back(r);
@@ -1921,24 +1950,9 @@ int mirt_set_grid(mirt_ctx* c, uint32_t min_blocks_per_wg, uint32_t max_workgrou
 // ~60 us of host time per frame, tools/dist_host_probe.py).  RCCL is opened at run time
 // (dlopen of librccl.so.1: the copy torch already loaded, else /opt/rocm's), so the library
 // loads without it and single-GPU callers never touch it.
-namespace {
+namespace mirt {
 
-struct Rccl {
-    bool ok = false;
-    std::string err;
-    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
-    decltype(&ncclCommDestroy) comm_destroy = nullptr;
-    decltype(&ncclSend) send = nullptr;
-    decltype(&ncclRecv) recv = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclGetErrorString) error_string = nullptr;
-    decltype(&ncclCommAbort) comm_abort = nullptr;    // optional (peer exclusion)
-    decltype(&ncclCommShrink) comm_shrink = nullptr;  // optional (peer exclusion without a new id)
-};
-
-Rccl load_rccl() {
+static Rccl load_rccl() {
     Rccl R;
     void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -1964,6 +1978,7 @@ Rccl load_rccl() {
     MIRT_RCCL_SYM(error_string, "ncclGetErrorString")
 #undef MIRT_RCCL_SYM
     R.comm_abort = (decltype(R.comm_abort))dlsym(h, "ncclCommAbort");
+    R.comm_init_all = (decltype(R.comm_init_all))dlsym(h, "ncclCommInitAll");
     R.comm_shrink = (decltype(R.comm_shrink))dlsym(h, "ncclCommShrink");
     R.ok = true;
     return R;
@@ -1973,6 +1988,35 @@ const Rccl& rccl() {
     static const Rccl R = load_rccl();  // thread-safe one-time initialisation
     return R;
 }
+
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+int trace_tiles_enqueue(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
+                        uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel,
+                        cnt_t* h_summary, uint64_t* pixels) {
+    HIP_TRY(hipSetDevice(c->device));
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    Slot* sl = nullptr;
+    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    SlotGuard guard{c, sl};
+    uint64_t tris = 0;
+    if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, cancel, pixels, &tris)) != MIRT_OK) {
+        (void)hipStreamSynchronize(s);
+        sl->pending = false;
+        return r;
+    }
+    // the slot's next user waits for `done` (slot_acquire): recorded again after the copy's
+    // read of sl->summary
+    HIP_TRY(hipMemcpyAsync(h_summary, sl->summary, kStatN * sizeof(cnt_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(sl->done, s));
+    sl->pending = true;
+    return MIRT_OK;
+}
+
+}  // namespace mirt
+
+namespace {
 
 #define RCCL_TRY(expr)                                                                           \
     do {                                                                                         \
@@ -2616,6 +2660,8 @@ void mirt_group_destroy(mirt_group* g) {
             g_ht[7] / g->k, g_ht[8] / g->k, g_ht[9] / g->k, g_ht[10] / g->k, g_ht[11] / g->k);
 #endif
     (void)hipSetDevice(g->c->device);
+    for (uint32_t i = 0; i < g->bn; ++i) lt_unpin(g->c, g->stage[i].fa.ltab);  // never launched
+    g->bn = 0;
     if (g->comm) {
         // a broken group (a peer stopped answering) may have RCCL work that never ends
         if (g->broken && rccl().comm_abort) (void)rccl().comm_abort(g->comm);
@@ -2908,6 +2954,7 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
         if (keep[i] == (uint32_t)g->my_index) g->my_index = (int)i;
     g->members = members;
     g->emu_drop = 0;
+    for (uint32_t i = 0; i < g->bn; ++i) lt_unpin(g->c, g->stage[i].fa.ltab);  // the open batch is dropped
     g->bn = 0;
     g->nb = 0;
     for (BatchRec& br : g->binfo) br = BatchRec();
@@ -2932,6 +2979,8 @@ static int group_flush(mirt_group* g) {
     const bool is_root = g->rank == 0;
     const uint32_t n = g->bn;
     g->bn = 0;
+    LtPins pins(c);  // the staged records' light tables, held until every share has launched
+    for (uint32_t i = 0; i < n; ++i) pins.add(g->stage[i].fa.ltab);
     BatchRec& br = g->binfo[hs];
     br.n = n;
     br.first = g->k - n;
@@ -3144,14 +3193,19 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     // split kernels and reflection frames run one frame per launch
     if (g->bn > 0 && (g->bbounces || f->max_bounces || (c->flags & MIRT_OPT_SPLIT_KERNELS) ||
                       !frames_batchable(g->stage[0], rec)))
-        if ((r = group_flush(g)) != MIRT_OK) return r;
+        if ((r = group_flush(g)) != MIRT_OK) {
+            lt_unpin(c, rec.fa.ltab);
+            return r;
+        }
     const uint32_t hs = (uint32_t)(g->nb % g->HB);
     // back-pressure when a batch opens: batch nb - HB (the last user of this host ring slot)
     // must have finished; batch nb - FB, the last user of this batch's stream, device slot and
     // framebuffers, is ordered before it by the stream itself
     if (g->bn == 0 && g->nb >= g->HB) {
-        if ((r = group_wait_event(g, g->ev_done[hs], "mirt_trace_frame back-pressure")) != MIRT_OK)
+        if ((r = group_wait_event(g, g->ev_done[hs], "mirt_trace_frame back-pressure")) != MIRT_OK) {
+            lt_unpin(c, rec.fa.ltab);
             return group_timed_out(g, hs, r);
+        }
         batch_fold(g, hs);
     }
     HT(0);

@@ -230,6 +230,9 @@ struct HitRec {
 constexpr int kQShards = 64, kStatShards = 8, kLine = 16;
 enum { kStatPrimTests = 0, kStatShadowTests, kStatPrimNodes, kStatPrimLeaves, kStatShadowNodes,
        kStatShadowLeaves, kStatHits, kStatOverflow, kStatShadowRays, kStatReflRays, kStatReflShadowRays, kStatN };
+// WorkArgs::prof_acc holds the kStatN totals and then, at kProfRedo, the deferred second passes run
+// (k_trace's redone blocks, the split kernels' redone items: mirt_profile.redo_items)
+constexpr int kProfRedo = kStatN, kProfN = kStatN + 1;
 constexpr int kQueues = 3;
 __host__ __device__ constexpr int cnt_queue(int q, int s) { return (q * kQShards + s) * kLine; }
 __host__ __device__ constexpr int cnt_hits(int s) { return (kQueues * kQShards + s) * kLine; }

@@ -83,6 +83,9 @@ class Context:
         except Exception:
             pass
 
+    _upload_fn = "mirt_mesh_upload"
+    _trace_tile_fn = "mirt_trace_tile"
+
     def upload_mesh(self, vertices, normals, face_v, face_n, face_mat, materials) -> int:
         v = np.ascontiguousarray(vertices, np.float64).reshape(-1, 3)
         vn = np.ascontiguousarray(normals, np.float64).reshape(-1, 3)
@@ -94,7 +97,7 @@ class Context:
         for i, m in enumerate(mats):
             marr[i] = L.Material(_d3(m[0:3]), _d3(m[3:6]), _d3(m[6:9]), float(m[9]))
         mid = C.c_uint32()
-        L.check(L.lib().mirt_mesh_upload(
+        L.check(getattr(L.lib(), self._upload_fn)(
             self.handle, v.ctypes.data if len(v) else None, len(v),
             vn.ctypes.data if len(vn) else None, len(vn),
             fv.ctypes.data if len(fv) else None, fn.ctypes.data if len(fn) else None,
@@ -173,6 +176,63 @@ class Context:
 
 
 # --------------------------------------------------------------------- scene
+class Box(Context):
+    """One process driving several GPUs behind BulkTrace (mirt.h mirt_box_*): an order is cut
+    into `strip`-px column strips dealt round robin over the devices and assembled on the first
+    (RCCL over xGMI, device copies when devices repeat, or per-device D2H).  Usable wherever a
+    Context is (Environment.from_file / from_gob, trace_tile, draw, Tracer.bulk_trace); entries
+    may repeat a device, so one GPU can stand in for a box."""
+
+    _upload_fn = "mirt_box_mesh_upload"
+    _trace_tile_fn = "mirt_box_trace_tile"
+
+    def __init__(self, devices: Sequence[int]):  # noqa: super().__init__ makes a single-GPU context
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        self._h = C.c_void_p()
+        L.check(L.lib().mirt_box_create(devs, len(devices), C.byref(self._h)))
+        self.devices = [int(d) for d in devices]
+        self.device = self.devices[0]
+        self._lock = threading.Lock()
+        self._streams = []
+
+    def close(self) -> None:
+        if self._h:
+            L.lib().mirt_box_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def release_mesh(self, mesh_id: int) -> None:
+        L.check(L.lib().mirt_box_mesh_release(self.handle, mesh_id))
+
+    def set_options(self, flags: int) -> None:
+        L.check(L.lib().mirt_box_set_options(self.handle, flags))
+
+    @property
+    def transport(self) -> int:
+        return int(L.lib().mirt_box_transport(self.handle))
+
+    def set_transport(self, transport: int) -> None:
+        L.check(L.lib().mirt_box_set_transport(self.handle, int(transport)))
+
+    def set_strip(self, strip: int) -> None:
+        L.check(L.lib().mirt_box_set_strip(self.handle, int(strip)))
+
+    def entry(self, i: int) -> "Context":
+        """Entry i's context (profiling, light-cache statistics), owned by the box."""
+        h = L.lib().mirt_box_ctx(self.handle, int(i))
+        if not h:
+            raise L.MirtError(L.MIRT_E_INVALID, f"no box entry {i}")
+        c = Context.__new__(Context)
+        c._h, c.device, c._lock, c._streams = C.c_void_p(h), self.devices[i], threading.Lock(), []
+        c.close = lambda: None  # the box destroys its entries
+        return c
+
+    def _unsupported(self, *a, **k):
+        raise L.MirtError(L.MIRT_E_INVALID, "a Box traces orders (trace_tile / draw / bulk_trace); "
+                                            "use box.entry(i) for per-device calls")
+
+    stream_create = set_grid = profile_enable = profile_read = debug_fp64 = _unsupported
+
+
 @dataclass
 class Camera:
     """state.Camera (camera.go:20-24) as NewCamera builds it, plus tan(fov/2)."""
@@ -396,8 +456,9 @@ def trace_tile(env: Environment, x: int, y: int, w: int, h: int, W: int, H: int,
     obj = np.zeros(n, np.int32)
     out = L.Outputs(rgb.ctypes.data, rgb8.ctypes.data, valid.ctypes.data, face.ctypes.data, obj.ctypes.data)
     st = L.Stats()
-    L.check(L.lib().mirt_trace_tile(env.ctx.handle, C.byref(fr), x, y, w, h, W, H, C.byref(out),
-                                    C.byref(cancel) if cancel is not None else None, C.byref(st)))
+    # a Context traces the tile on its GPU; a Box deals it over the box's GPUs (mirt_box_trace_tile)
+    L.check(getattr(L.lib(), env.ctx._trace_tile_fn)(env.ctx.handle, C.byref(fr), x, y, w, h, W, H, C.byref(out),
+                                                     C.byref(cancel) if cancel is not None else None, C.byref(st)))
     del keep
     return TileResult(rgb, rgb8, valid, face, obj, {k: getattr(st, k) for k, _ in L.Stats._fields_})
 

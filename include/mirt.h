@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIRT_ABI_VERSION 6
+#define MIRT_ABI_VERSION 7
 
 /* error codes */
 #define MIRT_OK 0
@@ -159,10 +159,18 @@ typedef struct {
     /* ABI 6: medians over the read's launches of the first kernel's and the whole launch's
        HIP-event durations (robust to a launch that waited behind an overlapped one) */
     double primary_ms_median, frame_ms_median;
+    /* ABI 7: deferred second passes run by the launches' last workgroups: k_trace's
+       redone 8x8 blocks plus the split kernels' redone items.  They run serially in one workgroup
+       at the end of a launch, so a scene that needs many makes frames slow: this makes it visible. */
+    uint64_t redo_items;
 } mirt_profile;
 
 int mirt_abi_version(void);
 const char *mirt_last_error(void);
+/* ABI 7: a hash of the kernels, the host code that launches them and the compile flags this
+ * library was built from (16 hex digits).  Profiles record it; bench.py cites a profile only
+ * for the build it was taken on. */
+const char *mirt_build_id(void);
 
 /* Context bound to one HIP device (one process per GPU). */
 int mirt_create(int device, mirt_ctx **out);
@@ -427,6 +435,49 @@ int mirt_group_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h
                           mirt_tile *out, uint32_t cap);
 int mirt_plan_tiles(uint32_t W, uint32_t H, uint32_t tile, uint32_t tile_h, uint32_t world, uint32_t rank,
                     mirt_tile *out, uint32_t cap);
+
+/*
+ * One process driving the GPUs of a box behind the BulkTrace contract (SURVEY.md §8(b)
+ * mirt_create(n_devices)).  A reference master sees ONE drop-in worker
+ * (worker/distributed/main.go:46-91) whose orders — the rectangles of the master's partition
+ * (master/main.go:54-91) — are cut into `strip`-pixel-wide column strips (default 8) dealt
+ * round robin over the box's device entries; each entry traces its strips, and the order is
+ * assembled on entry 0 and copied into the caller's host buffers in exactly mirt_trace_tile's
+ * layout (pixel (x+i, y+j) at i*h + j, every plane of mirt_outputs).  Re-entrant like
+ * mirt_trace_tile: concurrent orders each take a workspace of their own.
+ *   devices   n device ordinals (NULL: 0..n-1).  Entries may repeat a device (one GPU
+ *             standing in for several: the same deal and assembly, device copies instead of
+ *             RCCL, which refuses two ranks on one GPU).  Each entry is a context of its own.
+ *   transport MIRT_BOX_RCCL (default for n > 1 distinct devices: ncclCommInitAll over them,
+ *             send/recv of each entry's planes to entry 0 over xGMI), MIRT_BOX_COPY (peer
+ *             copies to entry 0; the default when devices repeat or librccl lacks
+ *             ncclCommInitAll), MIRT_BOX_HOST (every entry copies its strips straight into a
+ *             pinned host buffer over its own link).  The bytes returned never depend on it.
+ *   Meshes go to every entry through mirt_box_mesh_upload (one id for all); options through
+ *   mirt_box_set_options; mirt_box_ctx(b, i) is entry i's context (read-only use: profiling,
+ *   light-cache statistics).
+ */
+#define MIRT_BOX_RCCL 1
+#define MIRT_BOX_COPY 2
+#define MIRT_BOX_HOST 3
+typedef struct mirt_box mirt_box;
+int mirt_device_count(void);
+int mirt_box_create(const int *devices, uint32_t n, mirt_box **out);
+void mirt_box_destroy(mirt_box *box);
+int mirt_box_size(const mirt_box *box);
+mirt_ctx *mirt_box_ctx(mirt_box *box, uint32_t i);
+int mirt_box_set_transport(mirt_box *box, int transport);
+int mirt_box_transport(const mirt_box *box);
+int mirt_box_set_strip(mirt_box *box, uint32_t strip);
+int mirt_box_set_options(mirt_box *box, uint32_t flags);
+int mirt_box_mesh_upload(mirt_box *box, const double *v, uint32_t nv, const double *vn, uint32_t nn,
+                         const uint32_t *fv, const uint32_t *fn, const uint32_t *fmat, uint32_t nf,
+                         const mirt_material *mats, uint32_t nm, uint32_t *mesh_id);
+int mirt_box_mesh_release(mirt_box *box, uint32_t mesh_id);
+/* BulkTrace of one order on every entry of the box; synchronous, host buffers, as mirt_trace_tile. */
+int mirt_box_trace_tile(mirt_box *box, const mirt_frame *frame, uint32_t x, uint32_t y, uint32_t w, uint32_t h,
+                        uint32_t W, uint32_t H, const mirt_outputs *host_out, const volatile int *cancel,
+                        mirt_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -16,8 +16,9 @@ from conftest import GOLDEN, ROOT, SCENE
 BIN = os.path.join(ROOT, "worker_c", "mirt_worker")
 
 
-def _run(W, H, out, workers=4):
-    return subprocess.run([BIN, SCENE, str(W), str(H), str(out), str(workers)], capture_output=True, text=True,
+def _run(W, H, out, workers=4, box=0):
+    pre = ["--box", str(box)] if box else []
+    return subprocess.run([BIN] + pre + [SCENE, str(W), str(H), str(out), str(workers)], capture_output=True, text=True,
                           timeout=120, env={k: v for k, v in os.environ.items() if not k.startswith("PYTHON")})
 
 
@@ -47,6 +48,23 @@ def test_c_worker_frames_match_golden(tmp_path, W, H, golden, workers):
         hit = np.nonzero(valid)[0]
         assert np.array_equal(hit, g["hit_index"].astype(np.int64))
         assert np.array_equal(rgb8[hit], g["rgb8"]) and not rgb8[valid == 0].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,workers,box", [(320, 240, 7, 8), (1920, 1080, 8, 8), (160, 120, 3, 3)])
+def test_c_worker_box_serves_the_master_partition(tmp_path, W, H, workers, box):
+    """--box N: ONE C worker driving N device entries (mirt_box_*; on a one-GPU box every entry
+    is device 0) serves the master's partition (master/main.go:54-91) concurrently; its frame
+    equals the one-context frame, and at 320x240 the golden frame."""
+    out = tmp_path / "fb.bin"
+    r = _run(W, H, out, workers, box)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"box of {box} entries" in r.stdout and "orders equal: yes" in r.stdout
+    if (W, H) == (320, 240):
+        raw = np.fromfile(out, np.uint8)
+        g = np.load(os.path.join(GOLDEN, "suzanne_320x240.npz"))
+        rgb8 = raw[:W * H * 3].reshape(W * H, 3)
+        assert np.array_equal(rgb8[g["hit_index"].astype(np.int64)], g["rgb8"])
 
 
 def _run_gob(name, W, H, out, workers=4):

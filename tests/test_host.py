@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in sorted(names):
         assert hasattr(lib, n), f"libmirt.so does not export {n}"
     assert names == set(L.SIGNATURES), "ctypes signatures out of sync with include/*.h"
-    assert lib.mirt_abi_version() == 6
+    assert lib.mirt_abi_version() == 7
 
 
 def test_no_gpu_is_a_loud_error():

@@ -239,3 +239,57 @@ def test_light_cache_cycles_more_keys_than_fit(ctx):
         assert st["bytes"] <= 3 * one + 1024 and st["live"] <= 3
     finally:
         _lib().mirt_set_light_cache(ctx.handle, 4 << 30)
+
+
+@pytest.mark.gpu
+def test_light_table_pinned_by_open_batch(ctx):
+    """A frame staged in a group's open batch holds its light table (LightTab::pins) until the
+    batch launches: 24 synchronous frames with other light sets on the same context, under a
+    cache that holds two tables, must neither evict it nor hand its buffer to another key.  The
+    staged frame, flushed afterwards, equals the oracle; so does every frame in between."""
+    import dataclasses
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    from distributed_raytracer_amd.tracer import Light
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    sc = load_scene(SCENE)
+    env = rt.Environment.from_file(SCENE, ctx)
+    base = env.mutable()
+    n_tri = len(sc.meshes[0].face_v)
+    one = len(sc.lights) * n_tri * 64
+    W, H = 48, 36
+    rng = np.random.default_rng(21)
+    keys = [[(tuple(np.array(p) + rng.normal(size=3) * 0.5), c) for p, c in sc.lights] for _ in range(25)]
+
+    def mut_of(k):
+        return dataclasses.replace(base, lights=[Light(pos=p, col=c) for p, c in keys[k]])
+
+    def ref_of(k):
+        return Oracle(dataclasses.replace(sc, lights=keys[k]), culling="rtree").frame(W, H, nthreads=8)
+
+    s0 = _cache_stats(ctx)
+    _lib().mirt_set_light_cache(ctx.handle, 2 * one + 1024)
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=4, batch=4, with_rgb=True)
+    try:
+        idx = g.render(mut_of(0).to_frame())  # staged: the batch holds 1 of 4 frames
+        for k in range(1, 25):
+            fb = rt.draw(env, W, H, mut_of(k))
+            ref = ref_of(k)
+            assert np.array_equal(fb.rgb, ref["rgb"]) and np.array_equal(fb.valid, ref["valid"]), k
+        st = _cache_stats(ctx)
+        assert st["evictions"] > s0["evictions"]  # the other keys did cycle through the cache
+        g.wait()
+        g.flush()
+        torch.cuda.synchronize()
+        dev = g.frames[idx % 4]
+        ref = ref_of(0)
+        assert np.array_equal(dev.rgb.cpu().numpy(), ref["rgb"])
+        assert np.array_equal(dev.valid.cpu().numpy().astype(bool), ref["valid"].astype(bool))
+        # the staged key was never rebuilt: its table survived the 24 other frames
+        d = _cache_stats(ctx)
+        assert d["fallbacks"] - s0["fallbacks"] < 24, d
+    finally:
+        g.close()
+        _lib().mirt_set_light_cache(ctx.handle, 4 << 30)

@@ -114,6 +114,9 @@ def main():
         w.writerows(summary_rows)
     out = {
         "tag": tag,
+        # mirt_build_id() of the library the passes ran on (bench.py cites this file only while the
+        # loaded library has the same id)
+        "build_id": line.get("build_id"),
         "command": "python3 bench.py " + open(os.path.join(src, "args.txt")).read().split("args:", 1)[1].strip(),
         "kernel": kname,
         "shape": {"width": line["config"]["width"], "height": line["config"]["height"], "gpus": line["n_gpus"],

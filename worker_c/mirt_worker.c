@@ -16,9 +16,13 @@
  *              them (master/main.go:164-176).
  *   Frame group (mirt_trace_frame, world 1, library-owned framebuffers, host output):
  *              three frames in flight; each host frame must equal the BulkTrace frame.
+ *   Box        (--box N, mirt_box_*): ONE worker driving N device entries (device i % the
+ *              devices present: one GPU may stand in for a box) serves the same orders
+ *              concurrently through mirt_box_trace_tile; the assembled frame must equal the
+ *              one-context frame.
  *
- *   mirt_worker <scene.json> <W> <H> <out.bin> [workers]
- *   mirt_worker --gob <state.gob> <diff.gob> <W> <H> <out.bin> [workers]
+ *   mirt_worker [--box N] <scene.json> <W> <H> <out.bin> [workers]
+ *   mirt_worker [--box N] --gob <state.gob> <diff.gob> <W> <H> <out.bin> [workers]
  * Writes rgb8 (W*H*3) then valid (W*H) of the assembled frame, column-major x*H + y.
  * Exit status 0 = every check passed.
  */
@@ -73,6 +77,7 @@ static uint32_t partition(rect area, uint32_t workers, uint32_t dim, rect *out, 
 
 typedef struct {
     mirt_ctx *ctx;
+    mirt_box *box;       /* non-NULL: the order is served by the box (mirt_box_trace_tile) */
     const mirt_frame *frame;
     rect order;          /* comms.WorkOrder x, y, width, height */
     uint32_t W, H;
@@ -101,8 +106,10 @@ static void *serve(void *p) {
     memset(&out, 0, sizeof(out));
     out.rgb8 = rgb8;
     out.valid = valid;
-    b->rc = mirt_trace_tile(b->ctx, b->frame, b->order.x, b->order.y, b->order.w, b->order.h, b->W, b->H, &out, NULL,
-                            NULL);
+    b->rc = b->box ? mirt_box_trace_tile(b->box, b->frame, b->order.x, b->order.y, b->order.w, b->order.h, b->W, b->H,
+                                         &out, NULL, NULL)
+                   : mirt_trace_tile(b->ctx, b->frame, b->order.x, b->order.y, b->order.w, b->order.h, b->W, b->H, &out,
+                                     NULL, NULL);
     b->results = malloc(3 * n * sizeof(uint32_t));
     for (size_t k = 0; k < n; ++k) /* misses are (0, 0, 0) already */
         for (int c = 0; c < 3; ++c) b->results[3 * k + c] = rgb8[3 * k + c];
@@ -111,7 +118,48 @@ static void *serve(void *p) {
     return NULL;
 }
 
+/* Serve the orders concurrently (one thread each) on ctx or box and draw them into fb_rgb8
+ * as the master does (master/main.go:164-176, pixel i*h + j).  Returns nonzero on a failure. */
+static int serve_orders(mirt_ctx *ctx, mirt_box *box, const mirt_frame *frame, const rect *orders, int n, uint32_t W,
+                        uint32_t H, uint8_t *fb_rgb8) {
+    bulk_trace bt[256];
+    pthread_t th[256];
+    int bad = 0;
+    for (int i = 0; i < n; ++i) {
+        bt[i] = (bulk_trace){ctx, box, frame, orders[i], W, H, NULL, 0};
+        pthread_create(&th[i], NULL, serve, &bt[i]);
+    }
+    for (int i = 0; i < n; ++i) {
+        pthread_join(th[i], NULL);
+        if (bt[i].rc != MIRT_OK) {
+            fprintf(stderr, "BulkTrace %d failed: %d (%s)\n", i, bt[i].rc, box ? "box" : "context");
+            bad = 1;
+            free(bt[i].results);
+            continue;
+        }
+        const rect o = bt[i].order;
+        for (uint32_t a = 0; a < o.w; ++a)
+            for (uint32_t b = 0; b < o.h; ++b) {
+                const size_t src = (size_t)a * o.h + b, dst = (size_t)(o.x + a) * H + (o.y + b);
+                for (int c = 0; c < 3; ++c) fb_rgb8[3 * dst + c] = (uint8_t)bt[i].results[3 * src + c];
+            }
+        free(bt[i].results);
+    }
+    return bad;
+}
+
 int main(int argc, char **argv) {
+    int box_n = 0;
+    if (argc > 2 && strcmp(argv[1], "--box") == 0) {
+        box_n = atoi(argv[2]);
+        if (box_n < 1 || box_n > 64) {
+            fprintf(stderr, "--box needs 1..64 entries\n");
+            return 2;
+        }
+        argv[2] = argv[0];  /* drop the two words: argv[0] moves up */
+        argv += 2;
+        argc -= 2;
+    }
     const int gob = argc > 1 && strcmp(argv[1], "--gob") == 0;
     char **a = argv + (gob ? 2 : 0);  /* a[1] = scene (or state.gob; a[0] = diff.gob), a[2] = W, ... */
     const int na = argc - (gob ? 2 : 0);
@@ -182,30 +230,8 @@ int main(int argc, char **argv) {
     int n = 0;
     if (workers < 1 || workers > 256) workers = 4;
     (void)partition((rect){0, 0, W, H}, workers, 0, orders, &n);
-    bulk_trace bt[256];
-    pthread_t th[256];
-    for (int i = 0; i < n; ++i) {
-        bt[i] = (bulk_trace){ctx, &frame, orders[i], W, H, NULL, 0};
-        pthread_create(&th[i], NULL, serve, &bt[i]);
-    }
     uint8_t *fb_rgb8 = calloc((size_t)W * H, 3), *fb_valid = calloc((size_t)W * H, 1);
-    int bad = 0;
-    for (int i = 0; i < n; ++i) {
-        pthread_join(th[i], NULL);
-        if (bt[i].rc != MIRT_OK) {
-            fprintf(stderr, "BulkTrace %d failed: %d\n", i, bt[i].rc);
-            bad = 1;
-            continue;
-        }
-        /* the master draws the results (master/main.go:164-176), pixel i*h + j */
-        const rect o = bt[i].order;
-        for (uint32_t a = 0; a < o.w; ++a)
-            for (uint32_t b = 0; b < o.h; ++b) {
-                const size_t src = (size_t)a * o.h + b, dst = (size_t)(o.x + a) * H + (o.y + b);
-                for (int c = 0; c < 3; ++c) fb_rgb8[3 * dst + c] = (uint8_t)bt[i].results[3 * src + c];
-            }
-        free(bt[i].results);
-    }
+    int bad = serve_orders(ctx, NULL, &frame, orders, n, W, H, fb_rgb8);
     /* the valid plane of the whole screen from one more call (the wire carries colours only) */
     {
         mirt_outputs out;
@@ -233,6 +259,39 @@ int main(int argc, char **argv) {
     }
     CHECK(mirt_group_wait(g, NULL));
     mirt_group_destroy(g);
+
+    /* the box: one worker, box_n device entries, the same orders (mesh ids agree: the box
+     * uploads every mesh in the same order as the context did) */
+    int box_equal = -1;
+    if (box_n > 0) {
+        const int ndev = mirt_device_count();
+        int devs[64];
+        for (int i = 0; i < box_n; ++i) devs[i] = ndev > 0 ? i % ndev : 0;
+        mirt_box *box = NULL;
+        CHECK(mirt_box_create(devs, (uint32_t)box_n, &box));
+        for (uint32_t i = 0; i < nm; ++i) {
+            mirt_mesh_view v;
+            uint32_t id = 0;
+            CHECK(mirt_scene_mesh(scene, i, &v));
+            CHECK(mirt_box_mesh_upload(box, v.vertices, v.n_vertices, v.normals, v.n_normals, v.face_v, v.face_n,
+                                       v.face_mat, v.n_faces, v.materials, v.n_materials, &id));
+            if (id != mesh_ids[i]) {
+                fprintf(stderr, "box mesh id %u != context mesh id %u\n", id, mesh_ids[i]);
+                bad = 1;
+            }
+        }
+        uint8_t *box_rgb8 = calloc((size_t)W * H, 3);
+        bad |= serve_orders(NULL, box, &frame, orders, n, W, H, box_rgb8);
+        box_equal = memcmp(box_rgb8, fb_rgb8, (size_t)W * H * 3) == 0;
+        if (!box_equal) {
+            fprintf(stderr, "the box's frame differs from the context's\n");
+            bad = 1;
+        }
+        free(box_rgb8);
+        printf("mirt_worker: box of %d entries (transport %d), orders equal: %s\n", box_n, mirt_box_transport(box),
+               box_equal ? "yes" : "NO");
+        mirt_box_destroy(box);
+    }
 
     FILE *f = fopen(out_path, "wb");
     if (!f || fwrite(fb_rgb8, 3, (size_t)W * H, f) != (size_t)W * H || fwrite(fb_valid, 1, (size_t)W * H, f) != (size_t)W * H) {
