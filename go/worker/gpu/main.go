@@ -3,7 +3,11 @@
 // loop of BulkTrace (main.go:67-89) replaced by one libmirt call (package gpu).  The master,
 // the pool and the registrar see an ordinary worker (shared/comms/comms.proto:20-47).
 //
-//   gpu <master address:port> <work order port> [GPU index]
+//   gpu <master address:port> <work order port> [GPU index | all | i,j,...]
+//
+// With "all" (or a list of indices) ONE worker serves every order on several GPUs of the box
+// (gpu.NewBox: the order is cut into 8-px column strips dealt over the GPUs and assembled
+// over RCCL), so the master's partition sees a single worker for the box.
 //
 // Uncompiled here: this image has no Go toolchain (go/README.md).  worker_c/mirt_worker.c
 // runs the same library call sequence in C and tests/test_c_worker.py checks its frames.
@@ -16,8 +20,10 @@ import (
 	"fmt"
 	"log"
 	"net"
+	"errors"
 	"os"
 	"strconv"
+	"strings"
 	"time"
 
 	"github.com/golang/protobuf/ptypes/empty"
@@ -129,29 +135,53 @@ func main() {
 		log.Fatalln("Improper parameters.  This program requires the parameters:" +
 			"\n\t(1) master address (including port)" +
 			"\n\t(2) work order listening port" +
-			"\n\t(3) optional: GPU index (default 0)")
+			"\n\t(3) optional: GPU index (default 0), \"all\", or a comma-separated list of GPU indices")
 	}
 	masterAddr := os.Args[1]
 	orderPort, err := strconv.ParseUint(os.Args[2], 10, 32)
 	if err != nil {
 		log.Fatalf("Could not parse port number \"%s\": %v.\n", os.Args[2], err)
 	}
-	device := 0
+	devices := []int{0}
 	if len(os.Args) == 4 {
-		if device, err = strconv.Atoi(os.Args[3]); err != nil {
-			log.Fatalf("Could not parse GPU index \"%s\": %v.\n", os.Args[3], err)
+		devices = nil
+		if os.Args[3] == "all" {
+			for d := 0; d < gpu.DeviceCount(); d++ {
+				devices = append(devices, d)
+			}
+			if len(devices) == 0 {
+				log.Fatalln("No GPU is visible.")
+			}
+		} else {
+			for _, f := range strings.Split(os.Args[3], ",") {
+				d, err := strconv.Atoi(f)
+				if err != nil {
+					log.Fatalf("Could not parse GPU index \"%s\": %v.\n", f, err)
+				}
+				devices = append(devices, d)
+			}
 		}
 	}
 
-	// One GPU context for the process's life (mirt_create sets up the device workspaces and
-	// streams once); while the device cannot be opened the worker keeps retrying, as the
-	// reference keeps retrying its registration (worker/distributed/main.go:131-185).
+	// One GPU context (or box) for the process's life (it sets up the device workspaces and
+	// streams once).  While a device is busy or out of memory the worker keeps retrying, as
+	// the reference keeps retrying its registration (worker/distributed/main.go:131-185); an
+	// error that cannot go away (no such GPU, a library built for another GPU) ends it.
 	var w *gpu.Worker
 	for {
-		if w, err = gpu.New(device); err == nil {
+		if len(devices) == 1 {
+			w, err = gpu.New(devices[0])
+		} else {
+			w, err = gpu.NewBox(devices)
+		}
+		if err == nil {
 			break
 		}
-		log.Printf("GPU %d: %v.\n", device, err)
+		var me *gpu.Error
+		if !errors.As(err, &me) || !me.Transient() {
+			log.Fatalf("GPU(s) %v: %v.\n", devices, err)
+		}
+		log.Printf("GPU(s) %v: %v (retrying).\n", devices, err)
 		time.Sleep(time.Millisecond * time.Duration(registerFrequency))
 	}
 	defer w.Close()

@@ -25,20 +25,45 @@ import (
 	"context"
 	"fmt"
 	"math"
+	"strings"
 	"unsafe"
 
 	"github.com/mwindels/distributed-raytracer/shared/state"
 )
 
-// Worker holds one libmirt context (one GPU) and the meshes uploaded to it.
+// Worker holds one libmirt context (one GPU), or one box (several GPUs behind one worker,
+// mirt_box_*), and the meshes uploaded to it.
 type Worker struct {
 	ctx    *C.mirt_ctx
+	box    *C.mirt_box
 	meshes map[string]C.uint32_t // model path -> GPU mesh id
 }
 
-func lastError(call string, rc C.int) error {
-	return fmt.Errorf("%s: %s (code %d)", call, C.GoString(C.mirt_last_error()), int(rc))
+// Error is a failed libmirt call: the entry, its MIRT_E_* code and mirt_last_error().
+type Error struct {
+	Call string
+	Code int
+	Msg  string
 }
+
+func (e *Error) Error() string { return fmt.Sprintf("%s: %s (code %d)", e.Call, e.Msg, e.Code) }
+
+// Transient reports whether retrying the call may succeed: the device or memory was
+// unavailable.  A bad argument (a GPU index that does not exist), a library built for another
+// GPU or a limit is permanent.
+func (e *Error) Transient() bool {
+	if e.Code == int(C.MIRT_E_NOMEM) {
+		return true
+	}
+	return e.Code == int(C.MIRT_E_DEVICE) && !strings.Contains(e.Msg, "built for gfx950 only")
+}
+
+func lastError(call string, rc C.int) error {
+	return &Error{Call: call, Code: int(rc), Msg: C.GoString(C.mirt_last_error())}
+}
+
+// DeviceCount is the number of HIP devices the process sees.
+func DeviceCount() int { return int(C.mirt_device_count()) }
 
 // New opens the GPU `device` (one worker process per GPU).
 func New(device int) (*Worker, error) {
@@ -49,11 +74,35 @@ func New(device int) (*Worker, error) {
 	return w, nil
 }
 
-// Close releases the context and every mesh on it.
+// NewBox opens one worker over several GPUs (mirt_box_create): every work order is cut into
+// 8-pixel column strips dealt over the devices and assembled on the first (RCCL over xGMI),
+// so a master sees ONE drop-in worker for the whole box.
+func NewBox(devices []int) (*Worker, error) {
+	if len(devices) == 0 {
+		return nil, &Error{Call: "mirt_box_create", Code: int(C.MIRT_E_INVALID), Msg: "no devices"}
+	}
+	devs := (*C.int)(C.calloc(C.size_t(len(devices)), C.size_t(unsafe.Sizeof(C.int(0)))))
+	defer C.free(unsafe.Pointer(devs))
+	arr := unsafe.Slice(devs, len(devices))
+	for i, d := range devices {
+		arr[i] = C.int(d)
+	}
+	w := &Worker{meshes: map[string]C.uint32_t{}}
+	if rc := C.mirt_box_create(devs, C.uint32_t(len(devices)), &w.box); rc != C.MIRT_OK {
+		return nil, lastError("mirt_box_create", rc)
+	}
+	return w, nil
+}
+
+// Close releases the context (or box) and every mesh on it.
 func (w *Worker) Close() {
 	if w.ctx != nil {
 		C.mirt_destroy(w.ctx)
 		w.ctx = nil
+	}
+	if w.box != nil {
+		C.mirt_box_destroy(w.box)
+		w.box = nil
 	}
 }
 
@@ -61,7 +110,11 @@ func (w *Worker) Close() {
 // scene.  The context (device workspaces, streams) stays open for the process's life.
 func (w *Worker) ReleaseMeshes() {
 	for path, id := range w.meshes {
-		C.mirt_mesh_release(w.ctx, id)
+		if w.box != nil {
+			C.mirt_box_mesh_release(w.box, id)
+		} else {
+			C.mirt_mesh_release(w.ctx, id)
+		}
 		delete(w.meshes, path)
 	}
 }
@@ -102,9 +155,16 @@ func (w *Worker) uploadMesh(path string, m *state.Mesh) error {
 		matp = &mats[0]
 	}
 	var id C.uint32_t
-	rc := C.mirt_mesh_upload(w.ctx, (*C.double)(unsafe.Pointer(&f.V[0])), C.uint32_t(len(f.V)/3), vn,
-		C.uint32_t(len(f.VN)/3), (*C.uint32_t)(unsafe.Pointer(&f.FV[0])), fn,
-		(*C.uint32_t)(unsafe.Pointer(&f.FMat[0])), C.uint32_t(len(f.FMat)), matp, C.uint32_t(len(mats)), &id)
+	var rc C.int
+	if w.box != nil {
+		rc = C.mirt_box_mesh_upload(w.box, (*C.double)(unsafe.Pointer(&f.V[0])), C.uint32_t(len(f.V)/3), vn,
+			C.uint32_t(len(f.VN)/3), (*C.uint32_t)(unsafe.Pointer(&f.FV[0])), fn,
+			(*C.uint32_t)(unsafe.Pointer(&f.FMat[0])), C.uint32_t(len(f.FMat)), matp, C.uint32_t(len(mats)), &id)
+	} else {
+		rc = C.mirt_mesh_upload(w.ctx, (*C.double)(unsafe.Pointer(&f.V[0])), C.uint32_t(len(f.V)/3), vn,
+			C.uint32_t(len(f.VN)/3), (*C.uint32_t)(unsafe.Pointer(&f.FV[0])), fn,
+			(*C.uint32_t)(unsafe.Pointer(&f.FMat[0])), C.uint32_t(len(f.FMat)), matp, C.uint32_t(len(mats)), &id)
+	}
 	if rc != C.MIRT_OK {
 		return lastError("mirt_mesh_upload", rc)
 	}
@@ -198,8 +258,14 @@ func (w *Worker) BulkTrace(ctx context.Context, scene state.Environment, env *st
 		}
 	}()
 	out := C.mirt_outputs{rgb8: rgb8}
-	rc := C.mirt_trace_tile(w.ctx, fr, C.uint32_t(x), C.uint32_t(y), C.uint32_t(width), C.uint32_t(height),
-		C.uint32_t(screenW), C.uint32_t(screenH), &out, cc, nil)
+	var rc C.int
+	if w.box != nil { // the order over every GPU of the box
+		rc = C.mirt_box_trace_tile(w.box, fr, C.uint32_t(x), C.uint32_t(y), C.uint32_t(width), C.uint32_t(height),
+			C.uint32_t(screenW), C.uint32_t(screenH), &out, cc, nil)
+	} else {
+		rc = C.mirt_trace_tile(w.ctx, fr, C.uint32_t(x), C.uint32_t(y), C.uint32_t(width), C.uint32_t(height),
+			C.uint32_t(screenW), C.uint32_t(screenH), &out, cc, nil)
+	}
 	if rc != C.MIRT_OK {
 		return nil, lastError("mirt_trace_tile", rc)
 	}

@@ -209,6 +209,9 @@ def test_cgo_binding_matches_header():
         n = call_arity(src, m.end() - 1)
         assert n == protos[name], f"{rel}: C.{name} called with {n} arguments, mirt.h takes {protos[name]}"
     assert protos["mirt_trace_tile"] >= 10 and "rgb8" in fields and "proj_half_width" in fields
+    # the box-level worker (one process, the box's GPUs): created, fed meshes and orders through the box
+    for n in ("mirt_box_create", "mirt_box_mesh_upload", "mirt_box_trace_tile", "mirt_box_destroy", "mirt_device_count"):
+        assert f"C.{n}(" in src, f"{rel} does not call {n}"
 
 
 def test_header_parser_sees_the_boundary():
