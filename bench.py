@@ -223,7 +223,7 @@ def resolve_shape(a) -> None:
     multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
     F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "4"))
     B = a.batch if a.batch is not None else int(os.environ.get("MIRT_BATCH", "4" if multi else "1"))
-    F = max(1, min(F, 16))
+    F = max(1, min(F, 32))
     if a.split_kernels or a.bounces:
         B = 1  # one frame per launch on those paths
     B = max(1, min(B, F, 8))
@@ -657,7 +657,7 @@ def main():
                        "culling": "none (brute force)" if a.brute_force else "exact BVH (packet traversal)",
                        "d2h": "rgb8 + valid to pinned host memory inside the timed region" if d2h else "none (HBM)",
                        "scene": scene_tag(a.scene), "bounces": a.bounces, "options": opts, "camera": a.camera,
-                       "lights": a.lights},
+                       "light_motion": a.lights},
             "frames_in_flight": getattr(sh, "F", a.inflight),
             "frames_per_launch": getattr(sh, "B", 1),
             "sharder": sharder,

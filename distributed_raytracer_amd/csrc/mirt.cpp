@@ -155,8 +155,7 @@ struct Slot {
     // pixelToPoint per column / per row (tracer.go:19-20), cached per (fov, W, H)
     cnt_t* summary = nullptr;     // kStatN totals of the last frame (device)
     cnt_t* h_summary = nullptr;   // pinned copy for mirt_stats
-    FrameRec* h_frames = nullptr; // kMaxFrames pinned records of the next k_trace launch
-    FrameRec* d_frames = nullptr; // their device copy
+    FrameRec* h_frames = nullptr; // kMaxFrames records of the next k_trace launch (its kernel argument)
     ViewLeaf* views = nullptr;    // view tables of the next k_trace launch (WorkArgs::views)
     size_t views_cap = 0;
     ViewHead* view_heads = nullptr;
@@ -269,7 +268,6 @@ int slot_init(Slot* s) {
     HIP_TRY(hipMalloc((void**)&s->summary, kStatN * sizeof(cnt_t)));
     HIP_TRY(hipHostMalloc((void**)&s->h_summary, kStatN * sizeof(cnt_t)));
     HIP_TRY(hipHostMalloc((void**)&s->h_frames, kMaxFrames * sizeof(FrameRec)));
-    HIP_TRY(hipMalloc((void**)&s->d_frames, kMaxFrames * sizeof(FrameRec)));
     HIP_TRY(hipMemset(s->counters, 0, 2 * kCntN * sizeof(cnt_t)));
     return MIRT_OK;
 }
@@ -282,7 +280,7 @@ void slot_free(Slot* s) {
         if (p) (void)hipFree(p);
     for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
-                    (void*)s->d_frames, (void*)s->views, (void*)s->view_heads})
+                    (void*)s->views, (void*)s->view_heads})
         if (p) (void)hipFree(p);
     if (s->h_blocks) (void)hipHostFree(s->h_blocks);
     if (s->h_tiles) (void)hipHostFree(s->h_tiles);
@@ -961,6 +959,7 @@ void frame_record(const mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H
     rec.fa.ltab_n = rec.fa.ltab ? c->meshes[f->objects[0].mesh_id].ntri : 0;
     frustum_args(c, f, rec.fa, rec.fr, rec.ocert);
     rec.out = out;
+    rec.xf = XferArgs{};  // the packed layout (a frame group's fused shares set their transfer form)
     rec.live[0] = rec.live[1] = 0;  // every block (a frame group narrows it to the hit rectangle)
     rec.live[2] = W;
     rec.live[3] = H;
@@ -1143,8 +1142,6 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
     if (one_launch) {
         // one launch for the frames (k_trace); its time lands in the primary slot of the profile
-        FrameRec* src = nullptr;
-        HIP_TRY(hipHostGetDevicePointer((void**)&src, sl->h_frames, 0));
         // per-view leaf tables (MIRT_OPT_VIEWS; one-object frames with an LDS-resident mesh):
         // built by k_trace's first workgroups, one per (frame, view)
         const DevMesh& m0 = fa.obj[0].m;
@@ -1170,12 +1167,12 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         }
         // one frame: its record travels as k_trace's argument (no staging kernel ahead of it)
         HT(10);
-        if (nf > 1) HIP_TRY(launch_stage_frames(src, sl->d_frames, nf, s));
+
         HT(11);
-        wa.frames = nf > 1 ? sl->d_frames : nullptr;
+        wa.frames = nullptr;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
-        HIP_TRY(launch_trace(sl->h_frames[0], wa, pgrid, c->flags, s));
+        HIP_TRY(launch_trace(*(const FrameRecs*)sl->h_frames, wa, pgrid, c->flags, s));
         HT(3);
         if (prof) {
             HIP_TRY(hipEventRecord(pr.ev[1], s));
@@ -2164,6 +2161,26 @@ uint64_t rect_pixels(const std::vector<mirt_tile>& tiles, const uint32_t R[4]) {
     return n;
 }
 
+// A share of full-height strips written by k_trace in its transfer form (FrameRec::xf):
+// k_pack_rect's layout of the share's columns inside R, trailer {tag, words} after the data.
+// The share's tiles are in screen order, so its packed columns ascend with x.
+void share_xfer(const std::vector<mirt_tile>& tiles, const uint32_t R[4], uint32_t tag, XferArgs& xf) {
+    uint32_t kA = 0, kB = 0;
+    for (const mirt_tile& t : tiles) {
+        kA += R[0] > t.x ? std::min(t.w, R[0] - t.x) : 0u;
+        kB += R[2] > t.x ? std::min(t.w, R[2] - t.x) : 0u;
+    }
+    const uint32_t ch = R[3] > R[1] && R[2] > R[0] ? R[3] - R[1] : 0u;
+    xf.on = 1;
+    xf.k0 = kA;
+    xf.x0 = R[0];
+    xf.x1 = R[2];
+    xf.y0 = R[1];
+    xf.ch = ch;
+    xf.words = (kB - kA) * ch;
+    xf.tag = tag;
+}
+
 // One rank's share of the deal, traced by this process: normally this rank's own; in the
 // emulated world (mirt_group_emulate) every rank's, so one GPU runs the whole N-rank
 // pack -> transfer -> check -> unpack chain.
@@ -2256,7 +2273,9 @@ struct mirt_group {
     std::vector<uint64_t> slot_frame;   // per frame slot: the frame it holds (~0: none)
     // per frame slot: only [dirty0, dirty1) x [dirty_y0, dirty_y1) may hold non-miss pixels
     // (whole-screen planes); a narrow frame refills those columns before it traces its hit
-    // rectangle, unless the rectangle covers them (the trace rewrites every pixel in it)
+    // rectangle, unless the rectangle covers them (the trace rewrites every pixel in it).
+    // Tiled groups (root): [dirty0, dirty1) are the columns the last unpack into the slot's
+    // framebuffer may have left non-miss; the next unpack rewrites them and its own rectangle.
     std::vector<uint32_t> dirty0, dirty1, dirty_y0, dirty_y1;
     std::vector<uint64_t> slot_bad;     // per frame slot: deal indices whose transfer failed
     // fault handling (master/pool/pool.go:224-260, master/main.go:111-161)
@@ -2266,6 +2285,7 @@ struct mirt_group {
     uint64_t pending_bad = 0;           // deal indices failed since the last mirt_group_wait
     uint64_t pending_bad_frame = ~0ull;
     bool broken = false;                // a wait timed out: only mirt_group_exclude / destroy
+    bool no_fused_pack = false;         // MIRT_NO_FUSED_PACK: k_pack_rect after the trace (A/B)
     hipStream_t probe_stream = nullptr;
 };
 
@@ -2708,7 +2728,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     *out = nullptr;
     if (world < 1 || world > 64 || rank < 0 || rank >= world) return fail(MIRT_E_INVALID, "bad rank / world (1..64)");
     if (!W || !H || W > 65535 || H > 65535) return fail(MIRT_E_INVALID, "bad screen size");
-    if (inflight < 1 || inflight > 16) return fail(MIRT_E_INVALID, "inflight must be 1..16");
+    if (inflight < 1 || inflight > 32) return fail(MIRT_E_INVALID, "inflight must be 1..32");
     if (world > 1 && !unique_id) return fail(MIRT_E_INVALID, "world > 1 needs the root's unique id");
     if (world > 1 && tile == 0) return fail(MIRT_E_INVALID, "world > 1 needs a tile size");
     const bool is_root = rank == 0;
@@ -2737,6 +2757,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     g->d2h_sdma = d2h && !strcmp(d2h, "sdma");
     const char* ag = getenv("MIRT_ADAPTIVE_GRID");
     if (ag) g->adaptive_grid = (uint32_t)std::min(std::max(atoi(ag), 0), 2);
+    g->no_fused_pack = getenv("MIRT_NO_FUSED_PACK") != nullptr;
     const char* wt = getenv("MIRT_WAIT");
     if (wt) g->spin_wait = !strcmp(wt, "spin");
     // MIRT_GROUP_REHEARSE=N (timing diagnostic, world == 1 only): trace one share of an
@@ -3063,12 +3084,20 @@ static int group_flush(mirt_group* g) {
         if (fill_max) HIP_TRY(launch_fill_planes(fj, n, fill_max, s));
     }
     HT(8);
+    // full-height strips traced by k_trace write each share straight into its transfer form
+    // (FrameRec::xf: no k_pack_rect launch, no packed plane read back)
+    const bool fuse = g->tiled && (g->tile_h == 0 || g->tile_h >= g->H) && !g->bbounces &&
+                      !(c->flags & MIRT_OPT_SPLIT_KERNELS) && !g->no_fused_pack;
     for (Share& sh : g->shares) {
         Slot* sl = sh.slots[bs].get();
         for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t j = g->bj[i];
             sl->h_frames[i] = g->stage[i];
-            sl->h_frames[i].out = g->tiled ? OutPlanes{nullptr, nullptr, nullptr, nullptr, nullptr, sh.packed[g->bj[i]]}
-                                           : g->fb[g->bj[i]];
+            uint32_t* xfer = (is_root && sh.q == 0) ? g->gathered[j] : sh.sendbuf[j];
+            sl->h_frames[i].out = g->tiled ? OutPlanes{nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                       fuse ? xfer : sh.packed[j]}
+                                           : g->fb[j];
+            if (fuse) share_xfer(sh.tiles, br.rect[i], jobs.tag[i], sl->h_frames[i].xf);
             if (narrow[i]) memcpy(sl->h_frames[i].live, br.rect[i], sizeof(br.rect[i]));
         }
         int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr,
@@ -3080,12 +3109,14 @@ static int group_flush(mirt_group* g) {
         if (!g->tiled) continue;
         // the share's tiles inside each frame's hit rectangle -> its transfer form (the root's
         // share straight into region 0 of the gathered plane)
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t j = g->bj[i];
-            jobs.src[i] = sh.packed[j];
-            jobs.dst[i] = (is_root && sh.q == 0) ? g->gathered[j] : sh.sendbuf[j];
+        if (!fuse) {
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t j = g->bj[i];
+                jobs.src[i] = sh.packed[j];
+                jobs.dst[i] = (is_root && sh.q == 0) ? g->gathered[j] : sh.sendbuf[j];
+            }
+            HIP_TRY(launch_pack_rect(sh.d_tiles, (uint32_t)sh.tiles.size(), jobs, n, s));
         }
-        HIP_TRY(launch_pack_rect(sh.d_tiles, (uint32_t)sh.tiles.size(), jobs, n, s));
         if (g->emulate > 1 && sh.q != 0 && !((g->emu_drop >> sh.q) & 1u))
             for (uint32_t i = 0; i < n; ++i) {  // exactly the bytes an RCCL send would carry
                 const uint32_t j = g->bj[i];
@@ -3122,9 +3153,23 @@ static int group_flush(mirt_group* g) {
             jobs.src[i] = g->gathered[j];
             jobs.out[i] = g->fb[j];
             jobs.bad[i] = g->h_bad + (size_t)j * P;
+            // the columns the unpack rewrites: this frame's hit rectangle and the one the slot's
+            // framebuffer held (every other column holds misses already)
+            const uint32_t* R = br.rect[i];
+            uint32_t u0 = R[0], u1 = R[2];
+            if (g->dirty1[j] > g->dirty0[j]) {
+                u0 = R[2] > R[0] ? std::min(u0, g->dirty0[j]) : g->dirty0[j];
+                u1 = R[2] > R[0] ? std::max(u1, g->dirty1[j]) : g->dirty1[j];
+            }
+            jobs.ucol[i][0] = u0;
+            jobs.ucol[i][1] = u1;
+            g->dirty0[j] = R[2] > R[0] ? R[0] : 0;
+            g->dirty1[j] = R[2] > R[0] ? R[2] : 0;
         }
-        if (!g->rehearse) HIP_TRY(launch_check_regions(g->d_unpack, g->d_regions, P, g->stride, jobs, n, s));
-        HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->stride, jobs, n, s));
+        // the regions' trailers are checked by the same launch (not in a rehearsal, whose
+        // peer regions were never sent)
+        HIP_TRY(launch_unpack_rect(g->d_unpack, g->n_unpack, g->max_tile_px, g->H, g->stride,
+                                   g->rehearse ? nullptr : g->d_regions, P, jobs, n, s));
     }
     if (g->host_out && is_root) {
         HostCopyJobs hj{};

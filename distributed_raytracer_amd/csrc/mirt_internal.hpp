@@ -170,6 +170,17 @@ struct FrameArgs {
     uint32_t ltab_n, ltab_pad;  // records per light (= obj[0]'s ntri)
 };
 
+// A tiled frame group's share in full-height strips (k_trace only, FrameRec::xf): the rgbv
+// plane is the share's TRANSFER form, written in place (k_pack_rect's layout, so no pack
+// launch): pixel (i, j) of packed column k goes to word (k - k0) * ch + (j - y0) when
+// x0 <= i < x1 and y0 <= j < y0 + ch, and nowhere otherwise; the launch's last workgroup
+// writes the trailer {tag, words} at word `words`.  on == 0: the packed layout (every pixel
+// at its packed index).
+struct XferArgs {
+    uint32_t on, k0, x0, x1, y0, ch, words, tag;
+};
+constexpr uint64_t kNoOut = ~0ull;  // out_index: a pixel the frame does not store
+
 struct TileDesc {
     uint32_t x, y, w, h;
     uint64_t out_off;      // first packed pixel of this tile
@@ -273,20 +284,24 @@ struct ObjCert {
     float h[kOcertQuads][4][3];
 };
 
-// One frame of a k_trace launch, in device memory (a launch traces up to kMaxFrames
-// frames that share the mesh, object count, light count and options; the kernel
-// argument FrameArgs is the first frame's).
+// One frame of a k_trace launch (a launch traces up to kMaxFrames frames that share the mesh,
+// object count, light count and options; the kernel takes FrameArgs from the first frame's).
 constexpr uint32_t kMaxFrames = 8;
 struct alignas(16) FrameRec {
     FrameArgs fa;
     OutPlanes out;
     FrustumArgs fr;
     ObjCert ocert;
+    XferArgs xf;
     // Blocks with no pixel in [live[0], live[2]) x [live[1], live[3]) are not traced: every
     // ray of such a block misses, and the caller either cleared their outputs (a frame
     // group's whole-screen planes, launch_fill_planes) or never reads them (a share's packed
     // plane, of which k_pack_rect sends only the hit rectangle).  {0, 0, W, H}: every block.
     uint32_t live[4];
+};
+// k_trace's first argument: the launch's records, read in place from the kernarg segment.
+struct FrameRecs {
+    FrameRec r[kMaxFrames];
 };
 
 // Per-frame work description shared by the primary, shadow and shade kernels.
@@ -322,7 +337,7 @@ struct WorkArgs {
     uint64_t* timeline;    // MIRT_OPT_TIMELINE: 8 x u64 per wave (mirt.h), else nullptr
     cnt_t* summary;        // kStatN totals of this frame (written by k_shade's last workgroup)
     cnt_t* prof_acc;       // kStatN running totals while profiling, else nullptr
-    const FrameRec* frames;  // k_trace: nframes records; blocks [f * nblocks_frame, ...) are frame f's
+    const FrameRec* frames;  // unused (k_trace reads its records from the kernarg segment)
     uint32_t nframes;
     uint32_t nblocks_frame;  // nblocks = nframes * nblocks_frame; the table describes one frame
     // view tables (k_trace, one-object frames, nullptr: none): frame f, view v at
@@ -419,12 +434,11 @@ struct LightTabArgs {
     float* out;         // nl * n * kLtD floats, light-major
 };
 hipError_t launch_light_table(const LightTabArgs& a, hipStream_t s);
-hipError_t launch_stage_frames(const FrameRec* host_src, FrameRec* dst, uint32_t n, hipStream_t s);
 hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                          hipStream_t s);
-hipError_t launch_trace(const FrameRec& rec, const WorkArgs& wa, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uint32_t opts,
                         hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
@@ -437,13 +451,16 @@ hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPl
                             int grid, hipStream_t s);
 hipError_t read_diag_counters(uint64_t* out, uint32_t n);  // MIRT_DIAG builds (zeros otherwise)
 hipError_t launch_debug_fp64(int op, uint32_t n, const double* a, const double* b, double* out, hipStream_t s);
-struct RectJobs {  // k_pack_rect / k_unpack_rect / k_check_regions: per frame of a batch
+struct RectJobs {  // k_pack_rect / k_unpack_rect (and its region check): per frame of a batch
     const uint32_t* src[kMaxFrames];  // pack: the rgbv plane; unpack/check: the gathered regions
     uint32_t* dst[kMaxFrames];        // pack: the transfer buffer
     OutPlanes out[kMaxFrames];        // unpack: the framebuffer
     uint32_t rect[kMaxFrames][4];     // hit rectangle x0, y0, x1, y1 (half-open)
     uint32_t tag[kMaxFrames];         // the frame's trailer tag (transfer_tag of its index)
     uint8_t* bad[kMaxFrames];         // check: one byte per region, 1 = trailer missing or wrong
+    // unpack: the framebuffer columns [ucol[f][0], ucol[f][1]) are written (the frame's hit
+    // rectangle and the one its slot held before: every other column already holds misses)
+    uint32_t ucol[kMaxFrames][2];
 };
 // Every transfer buffer ends with a two-word trailer written by k_pack_rect right after
 // the data: {tag of the frame, words of data}.  The root checks it in every gathered
@@ -486,10 +503,11 @@ hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uin
                                  hipStream_t s);
 hipError_t launch_pack_rect(const TileDesc* tiles, uint32_t ntiles, const RectJobs& jobs, uint32_t nframes,
                             hipStream_t s);
+// regions != nullptr: the launch also checks every region's trailer (check_region,
+// bad[f][r]) before its frames are used
 hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, uint64_t cap,
-                              const RectJobs& jobs, uint32_t nframes, hipStream_t s);
-hipError_t launch_check_regions(const TileDesc* tiles, const RegionDesc* regions, uint32_t nregions, uint64_t stride,
-                                const RectJobs& jobs, uint32_t nframes, hipStream_t s);
+                              const RegionDesc* regions, uint32_t nregions, const RectJobs& jobs, uint32_t nframes,
+                              hipStream_t s);
 hipError_t launch_unpack(const TileDesc* tiles, uint32_t ntiles, uint64_t max_tile_px, uint32_t H, const OutPlanes& src,
                          const OutPlanes& dst, hipStream_t s);
 

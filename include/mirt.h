@@ -159,8 +159,8 @@ typedef struct {
     /* ABI 6: medians over the read's launches of the first kernel's and the whole launch's
        HIP-event durations (robust to a launch that waited behind an overlapped one) */
     double primary_ms_median, frame_ms_median;
-    /* ABI 7: deferred second passes run by the launches' last workgroups: k_trace's
-       redone 8x8 blocks plus the split kernels' redone items.  They run serially in one workgroup
+    /* ABI 7: deferred second passes run by k_trace launches' last workgroups: its
+       redone 8x8 blocks (the split kernels' are not counted).  They run serially in one workgroup
        at the end of a launch, so a scene that needs many makes frames slow: this makes it visible. */
     uint64_t redo_items;
 } mirt_profile;
@@ -360,7 +360,7 @@ void mirt_object_bounds(const double *v, uint32_t nv, const double pos[3], doubl
  * planes a caller leaves NULL are not produced; with tile > 0 only rgb8, valid and rgbv can
  * be produced — rgb, face or object planes are rejected; fbs == NULL on the root: the group
  * allocates rgb8 + valid device planes itself, for callers that read frames through
- * mirt_group_frame_host and own no device memory).  world <= 64.  world == 1 with tile == 0 traces the
+ * mirt_group_frame_host and own no device memory).  world <= 64, inflight <= 32.  world == 1 with tile == 0 traces the
  * whole screen straight into the framebuffer (no tiles, no RCCL); world == 1 with tile > 0
  * rehearses the tiled path on one GPU.
  *   mirt_group_unique_id: rank 0 makes the RCCL id (128 bytes) every rank passes in.

@@ -92,7 +92,8 @@ def test_box_every_plane_equals_one_gpu(ctx, env, box8, box_env, transport, stri
             b = rt.trace_tile(box_env, x, y, w, h, W, H)
             for k in ("rgb", "rgb8", "valid", "face", "obj"):
                 assert np.array_equal(getattr(a, k), getattr(b, k)), (transport, strip, (x, y, w, h), k)
-            for k in ("primary_rays", "hits", "shadow_rays", "tri_tests"):
+            # (tri_tests depend on how the 8x8 packets fall: strips other than 8 px regroup the rays)
+            for k in ("primary_rays", "hits", "shadow_rays"):
                 assert a.stats[k] == b.stats[k], k
     finally:
         box8.set_transport(rt._lib.MIRT_BOX_COPY)
