@@ -38,7 +38,10 @@ extern "C" {
 #define MIRT_OK 0
 #define MIRT_E_INVALID (-1)   /* bad argument (null pointer, zero size, bad id) */
 #define MIRT_E_DEVICE (-2)    /* HIP runtime / kernel launch error */
-#define MIRT_E_LIMIT (-3)     /* more objects/lights than the kernel-argument block holds */
+#define MIRT_E_LIMIT (-3)     /* more objects/lights than the kernel-argument block holds, or an
+                                 object whose bounding box (object.go:31-59) overflows fp64: the
+                                 reference still traces such a frame (its Box.Intersect evaluates
+                                 inf/NaN planes, box.go:29-68); this library rejects it */
 #define MIRT_E_NOMEM (-4)     /* device or host allocation failed */
 #define MIRT_E_CAMERA (-5)    /* camera dir parallel to the global up vector (camera.go:37) */
 #define MIRT_E_CANCELLED (-6) /* *cancel became non-zero (worker/distributed/main.go:73) */

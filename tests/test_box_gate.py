@@ -352,3 +352,22 @@ def test_deferred_second_passes_in_multi_frame_launches(ctx, tile):
                 assert np.array_equal(got.rgb8.cpu().numpy(), refs[q]["rgb8"]), f"seed {seed} frame {k} rgb8"
         finally:
             g.close()
+
+
+@pytest.mark.gpu
+def test_object_box_overflow_is_rejected(ctx, env):
+    """An object whose bounding box overflows fp64 (object.go:31-59 at a position near the fp64
+    maximum) is refused with MIRT_E_LIMIT by every entry: the kernels' Box.Intersect needs finite
+    corners (the reference would trace it with inf/NaN planes; mirt.h MIRT_E_LIMIT).  An object
+    just inside the range still traces."""
+    import dataclasses
+    import distributed_raytracer_amd as rt
+    base = env.mutable()
+    o = base.objects[0]
+    far = dataclasses.replace(base, objects=[rt.SceneObject(o.mesh_id, (1.7e308, 0.0, 0.0))])
+    with pytest.raises(rt.MirtError) as e:
+        rt.draw(env, 32, 24, far)
+    assert e.value.code == rt._lib.MIRT_E_LIMIT and "overflows" in str(e.value)
+    ok = dataclasses.replace(base, objects=[rt.SceneObject(o.mesh_id, (1e300, 0.0, 0.0))])
+    fb = rt.draw(env, 32, 24, ok)  # far from the camera: every pixel misses
+    assert int(fb.valid.sum()) == 0

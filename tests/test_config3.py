@@ -1,8 +1,9 @@
 """BASELINE.json configs[3]: the synthetic 1,000,000-triangle UV sphere (SURVEY.md §8(d),
 tools/gen_sphere_obj.py) at 3840x2160.  The mesh is far beyond the LDS (BVH and
 triangles are read from HBM).  Parity: every 8th column of the full frame against the
-oracle (R-tree variant), bit-exact; the generator and both OBJ loaders are checked on CPU
-at a small size."""
+oracle (R-tree variant) — valid, rgb8 and the fp64 rgb bit-exact (and within 1e-5) — through
+mirt_trace_tile and through the bench's frame group; the generator and both OBJ loaders are
+checked on CPU at a small size."""
 import os
 import sys
 
@@ -34,12 +35,35 @@ def config3(tmp_path_factory):
     return g.write(str(tmp_path_factory.mktemp("config3")))
 
 
-@pytest.mark.gpu
-def test_config3_1m_triangles_4k_subsample_vs_oracle(ctx, config3):
-    import distributed_raytracer_amd as rt
+W4K, H4K = 3840, 2160
+RGB_TOL = 1e-5  # north_star's bound per channel (asserted beside bit-exactness)
+
+
+@pytest.fixture(scope="module")
+def config3_ref(config3):
+    """The oracle (R-tree restatement) on every 8th column of the 4K frame, and those pixels'
+    indices in the column-major framebuffer."""
     from oracle.oracle import Oracle
     from oracle.scene_py import load_scene
-    W, H = 3840, 2160
+    cols = list(range(7, W4K, 8))
+    ref = Oracle(load_scene(config3), use_rtree=True).trace_tiles(W4K, H4K, [(x, 0, 1, H4K) for x in cols],
+                                                                  nthreads=16)
+    sub = np.concatenate([np.arange(x * H4K, (x + 1) * H4K) for x in cols])
+    assert ref["valid"].sum() > 10000
+    return ref, sub
+
+
+def _check_rgb(rgb, ref):
+    """fp64 colour: bit-exact, and within north_star's 1e-5 per channel."""
+    assert float(np.abs(rgb - ref["rgb"]).max()) <= RGB_TOL
+    assert np.array_equal(rgb, ref["rgb"])
+
+
+@pytest.mark.gpu
+def test_config3_1m_triangles_4k_subsample_vs_oracle(ctx, config3, config3_ref):
+    import distributed_raytracer_amd as rt
+    W, H = W4K, H4K
+    ref, sub = config3_ref
     env = rt.Environment.from_file(config3, ctx)
     assert sum(len(m.face_v) for m in env.meshes) == 1_000_000
     ctx.profile_enable(True)
@@ -47,11 +71,38 @@ def test_config3_1m_triangles_4k_subsample_vs_oracle(ctx, config3):
     p = ctx.profile_read()
     ctx.profile_enable(False)
     assert p["stack_overflows"] == 0
-    cols = list(range(7, W, 8))  # every 8th column
-    ref = Oracle(load_scene(config3), use_rtree=True).trace_tiles(W, H, [(x, 0, 1, H) for x in cols], nthreads=16)
-    sub = np.concatenate([np.arange(x * H, (x + 1) * H) for x in cols])
-    assert ref["valid"].sum() > 10000
     assert np.array_equal(fb.valid[sub], ref["valid"])
     assert np.array_equal(fb.rgb8[sub], ref["rgb8"])
+    _check_rgb(fb.rgb[sub], ref)
     # culling: far fewer tests than brute force (8.3e12 primary alone)
     assert 0 < p["primary_tri_tests"] < W * H * 100
+
+
+@pytest.mark.gpu
+def test_config3_frame_group_8x2_vs_oracle(ctx, config3, config3_ref):
+    """The bench's path at configs[3]: the native frame group with 8 frames in flight, 2 per
+    k_trace launch, host output on; the last frame of a run that reuses every slot, through
+    the D2H (rgb8, valid) and the device fp64 rgb plane, on every 8th column."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W, H = W4K, H4K
+    ref, sub = config3_ref
+    env = rt.Environment.from_file(config3, ctx)
+    fr = env.mutable().to_frame()
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=8, batch=2, with_rgb=True, host_output=True)
+    try:
+        last = None
+        for _ in range(2 * 8 + 2):
+            last = g.render(fr)
+        g.wait()
+        g.flush()
+        torch.cuda.synchronize()
+        rgb8, valid = g.host_frame(last)
+        assert np.array_equal(valid[sub], ref["valid"])
+        assert np.array_equal(rgb8[sub], ref["rgb8"])
+        dev = g.frames[last % 8]
+        _check_rgb(dev.rgb.cpu().numpy()[sub], ref)
+    finally:
+        g.close()
+        ctx.set_grid()
