@@ -202,6 +202,9 @@ def parse():
                     help="variant: k_primary then k_shadow (default: one k_trace launch per frame)")
     ap.add_argument("--static-schedule", action="store_true",
                     help="ablation: round-robin work split instead of the dynamic work queues")
+    ap.add_argument("--lds-stream", action="store_true",
+                    help="meshes beyond the LDS: stream each leaf's triangles through a per-wave LDS window "
+                         "(MIRT_OPT_LDS_STREAM; same results)")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--profile-json", default="",
@@ -422,7 +425,8 @@ def main():
         rt._lib.MIRT_OPT_BRUTE_FORCE if a.brute_force else 0) | (
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
         rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0) | (
-        rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0) | (rt._lib.MIRT_OPT_NO_BOX_GATE if a.no_box_gate else 0)
+        rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0) | (rt._lib.MIRT_OPT_NO_BOX_GATE if a.no_box_gate else 0) | (
+        rt._lib.MIRT_OPT_LDS_STREAM if a.lds_stream else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses
@@ -731,6 +735,8 @@ def main():
                 rgb64 = g2.frames[0].rgb.cpu().numpy()
             finally:
                 g2.close()
+            count("parity_rgb", 1, batched=False)  # (the launches key partitions the kernel trace)
+            line["launches"] = launches
             line["parity"] = parity_check(valid, rgb8, a.scene, W, H, a.bounces,
                                           cams[(a.steps - 1) % len(cams)] if a.camera == "orbit" else None,
                                           lsets[(a.steps - 1) % len(lsets)] if a.lights == "orbit" else None,

@@ -37,6 +37,7 @@ MIRT_OPT_VIEWS = 256
 MIRT_OPT_REFLECT_CHAINS = 512
 MIRT_OPT_NO_LIGHT_TABLE = 1024
 MIRT_OPT_NO_BOX_GATE = 2048
+MIRT_OPT_LDS_STREAM = 4096
 
 D3 = C.c_double * 3
 

@@ -87,3 +87,15 @@
 #ifndef MIRT_BOX_GATE
 #define MIRT_BOX_GATE 1
 #endif
+// One-object frames of an HBM mesh (beyond the LDS) run k_trace instantiations that take the
+// object count and the segment shadow mode as constants (1), or the generic HBM kernel (0:
+// measurement builds).  MIRT_OPT_LDS_STREAM selects the one that streams the triangles through
+// LDS; MIRT_STREAM_SHADOW: its shadow segments stream too (1) or read HBM (0: the default —
+// at configs[3] streaming the shadow sweeps cost 11% (15 VGPR spills), primary-only
+// streaming ties the HBM kernel: DESIGN.md §4.6).
+#ifndef MIRT_HBM1
+#define MIRT_HBM1 1
+#endif
+#ifndef MIRT_STREAM_SHADOW
+#define MIRT_STREAM_SHADOW 0
+#endif

@@ -744,11 +744,48 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 // Packets with a lane whose object-space origin is beyond the cull limit (the inflation
 // argument needs a bounded origin) enter every child.
 //   GATE: candidates pass their face box (fbox) first (test_range; a trace's second pass).
+// ---------------------------------------------------------------- LDS triangle streaming
+// north_star's "triangle data streamed through LDS in batches", for a mesh beyond the LDS
+// (MIRT_OPT_LDS_STREAM, one-object frames, k_trace): each wave keeps a window of kStreamTris + 1
+// consecutive faces of the BVH-ordered triangle array in its own LDS slice.  A leaf the window
+// holds is tested from LDS; otherwise the wave first loads the window around the leaf (centred
+// on it, so leaves visited after it on either side in BVH order are likely inside) with vector
+// loads, 16 bytes per lane per load (8 KB in 8 loads), then tests it from LDS.  The records are
+// copied, not recomputed: the same bits are tested either way.
+constexpr uint32_t kStreamTris = 112;
+constexpr size_t kStreamSlice = (size_t)(kStreamTris + 1) * kTriD;  // doubles per wave (an odd base rounds down)
+constexpr size_t kStreamBytes = (kWG / 64) * kStreamSlice * sizeof(double);
+// each wave's window start (~0: none); k_trace resets it before its waves start
+__shared__ uint32_t g_stream_base[kWG / 64];
+extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
+__device__ __forceinline__ const double* stream_leaf(cdptr tri, uint32_t ntri, uint32_t first, uint32_t cnt) {
+    const uint32_t wave = threadIdx.x >> 6;
+    double* slice = g_lds_mesh + (size_t)wave * kStreamSlice;
+    uint32_t base = __builtin_amdgcn_readfirstlane(g_stream_base[wave]);
+    if (base == ~0u || first < base || first + cnt > base + kStreamTris + 1 || first + cnt > ntri) {
+        // an even start (16-byte aligned: 72-byte faces), at most ntri - kStreamTris, so the
+        // kStreamTris + 1 faces from it cover the leaf
+        base = first > kStreamTris / 2 ? first - kStreamTris / 2 : 0u;
+        if (ntri > kStreamTris && base > ntri - kStreamTris) base = ntri - kStreamTris;
+        base &= ~1u;
+        const uint32_t n = min(kStreamTris + 1, ntri - base), nd = n * kTriD;
+        const double2* src = (const double2*)(tri + (size_t)base * kTriD);
+        double2* dst = (double2*)slice;
+        asm volatile("" ::: "memory");  // every lane's reads of the previous window come first
+        for (uint32_t i = threadIdx.x & 63; i < nd / 2; i += 64) dst[i] = src[i];
+        if ((nd & 1) && (threadIdx.x & 63) == 0) slice[nd - 1] = tri[(size_t)base * kTriD + nd - 1];
+        if ((threadIdx.x & 63) == 0) g_stream_base[wave] = base;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slice is written before it is read
+    }
+    return slice + (size_t)(first - base) * kTriD;
+}
+
 template <bool REL, bool PREFILTER, bool SEG, bool LT3 = true, bool GATE = false, typename SrcPtr>
 __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V3 d, V3 neg, bool lane_on, Best& b,
                                           Visits& vis, float tmax = 0.0f, double resolve = 0.0, bool octant = true,
                                           const float* lt = nullptr, const SegPre* sp = nullptr,
-                                          const double* fbox = nullptr) {
+                                          const double* fbox = nullptr, bool stream = false) {
     // LDS-resident meshes (the host guarantees depth <= kBvhShallowDepth) use a one-VGPR stack
     constexpr bool DEEP = !__is_same(SrcPtr, const double*);
     const Ray32 r = ray32(ro, d);
@@ -766,9 +803,14 @@ __device__ __forceinline__ void bvh_sweep(const DevMesh& m, SrcPtr src, V3 ro, V
             const uint32_t first = ref & kBvhFirstMask, cnt = (ref & ~kBvhLeafBit) >> kBvhCountShift;
             ++vis.leaves;
             diag(SEG ? 14 : 6);
-            test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3, GATE>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro, d,
-                                                                 neg, b, vis.tests,
-                                                                 lt ? lt + (size_t)first * kLtD : nullptr, sp, live, fbox);
+            const float* lt_leaf = lt ? lt + (size_t)first * kLtD : nullptr;
+            if (DEEP && stream)  // an HBM mesh through the wave's LDS window (stream is a constant)
+                test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3, GATE>(stream_leaf((cdptr)src, m.ntri, first, cnt), m.fidx,
+                                                                     first, cnt, ro, d, neg, b, vis.tests, lt_leaf, sp, live,
+                                                                     fbox);
+            else
+                test_range<REL, PREFILTER, SEG ? 8 : 0, SEG, LT3, GATE>(src + (size_t)first * kTriD, m.fidx, first, cnt, ro,
+                                                                     d, neg, b, vis.tests, lt_leaf, sp, live, fbox);
             if (SEG) {
                 live = live && !(b.has() && b.d < resolve);
                 if (__ballot(live) == 0) break;
@@ -1108,7 +1150,7 @@ __device__ __forceinline__ void winner(const DevObject& ob, uint32_t pos, V3 ro,
 //   obj_sure (wave-uniform): the object's box is known to pass for every lane (a primary block
 //   inside the object-box certificate, block_obj_cert), so its gate is skipped.
 //   MIRT_OPT_NO_BOX_GATE: no boxes (brute-force semantics).
-template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false>
+template <bool REL, bool PREFILTER, bool BRUTE, bool COMMON = false, int HBM1 = 0>
 __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const double* __restrict__ lds, bool resident, V3 o, V3 d,
                                  bool lane_on, bool want_normal, Visits& vis, bool pass2, bool& redo,
                                  bool obj_sure = false, uint32_t* __restrict__ stk = nullptr, const ViewLeaf* vt = nullptr, uint32_t vn = 0,
@@ -1121,7 +1163,9 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
     V3 cam{fa.cam[0], fa.cam[1], fa.cam[2]};
     const bool gating = MIRT_BOX_GATE && !(fa.flags & MIRT_OPT_NO_BOX_GATE);
     bool again = false;
-    for (uint32_t oi = 0; oi < fa.n_objects; ++oi) {
+    // (HBM1: the one-object HBM-mesh kernels, launched by the host for those frames only)
+    const uint32_t nobj = HBM1 ? 1u : fa.n_objects;
+    for (uint32_t oi = 0; oi < nobj; ++oi) {
         const DevObject& ob = fa.obj[oi];
         V3 ro = sub(o, V3{ob.pos[0], ob.pos[1], ob.pos[2]});  // object.go:71
         V3 neg = scale(d, -1);  // triangle.go:38 rDir.Scale(-1)
@@ -1140,7 +1184,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
             else
                 bvh_sweep<false, PREFILTER, false, true, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f,
                                                                0.0, !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr,
-                                                               mesh_fbox(ob.m));
+                                                               mesh_fbox(ob.m), HBM1 == 2);
         } else if (BRUTE) {
             if (resident)
                 test_range<REL, PREFILTER>(lds, ob.m.fidx, 0, ntri, ro, d, neg, b, vis.tests);
@@ -1164,7 +1208,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
                                              !(fa.flags & MIRT_OPT_NO_OCTANT));
         } else {
             bvh_sweep<false, PREFILTER, false>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, 0.0f, 0.0,
-                                               !(fa.flags & MIRT_OPT_NO_OCTANT));
+                                               !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr, nullptr, HBM1 == 2);
         }
         uint32_t face = 0, pos = 0;
         bool got = lane_on && best_result(b, face, pos);
@@ -1214,7 +1258,7 @@ __device__ __forceinline__ Nearest trace_nearest(const FrameArgs& fa, const doub
 }
 // trace_nearest with its second pass in place, for callers without a work loop to retry in
 // (k_rays, the reflection chains, k_bounce's own shadows).
-template <bool REL, bool PREFILTER, bool BRUTE>
+template <bool REL, bool PREFILTER, bool BRUTE, int HBM1 = 0>
 __device__ __forceinline__ Nearest trace_nearest_settled(const FrameArgs& fa, const double* __restrict__ lds,
                                                          bool resident, V3 o, V3 d, bool lane_on, bool want_normal,
                                                          Visits& vis) {
@@ -1222,7 +1266,8 @@ __device__ __forceinline__ Nearest trace_nearest_settled(const FrameArgs& fa, co
     Nearest r;
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-        r = trace_nearest<REL, PREFILTER, BRUTE>(fa, lds, resident, o, d, lane_on, want_normal, vis, pass == 1, redo);
+        r = trace_nearest<REL, PREFILTER, BRUTE, false, HBM1>(fa, lds, resident, o, d, lane_on, want_normal, vis, pass == 1,
+                                                               redo);
         if (!redo) break;
     }
     return r;
@@ -1249,7 +1294,7 @@ __device__ __forceinline__ Nearest trace_nearest_settled(const FrameArgs& fa, co
 //   the work item again with pass2, where every candidate is gated before it counts.  The
 //   retry lives in the callers' own work loops, so the sweep's code is not wrapped in a second
 //   loop (that cost 12 spilled VGPRs in k_trace).
-template <bool PREFILTER, bool LT3 = true>
+template <bool PREFILTER, bool LT3 = true, int HBM1 = 0>
 __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const double* __restrict__ lds, bool resident,
                                                   uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d, V3 lpos, uint32_t li,
                                                   bool lane_on, Visits& vis, bool pass2, bool& redo,
@@ -1288,7 +1333,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
         else
             bvh_sweep<false, PREFILTER, true, LT3, true>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax,
                                                          resolve, !(fa.flags & MIRT_OPT_NO_OCTANT), nullptr, nullptr,
-                                                         mesh_fbox(ob.m));
+                                                         mesh_fbox(ob.m), false);
     } else if (MIRT_SHADOW_WIDE) {
         if (resident)
             bvh_wide<false, PREFILTER, true>(ob.m, lds, stk, cone, r, force, ro, d, neg, lane_on, b, vis, vis.overflow,
@@ -1335,7 +1380,7 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
                                                   !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
         else
             bvh_sweep<false, PREFILTER, true, LT3>(ob.m, (cdptr)ob.m.tri, ro, d, neg, lane_on, b, vis, tmax, resolve,
-                                                  !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp);
+                                                  !(fa.flags & MIRT_OPT_NO_OCTANT), lt, &sp, nullptr, HBM1 == 2 && MIRT_STREAM_SHADOW);
     }
     if (gating) {
         uint32_t face = 0, p = 0;
@@ -1377,13 +1422,14 @@ __device__ __forceinline__ bool shadow_lit_single(const FrameArgs& fa, const dou
 }
 // shadow_lit_single with its retry in place, for callers that hold per-lane chain state
 // (k_reflect, k_bounce with MIRT_BOUNCE_SHADE) rather than a work queue.
-template <bool PREFILTER, bool LT3 = true>
+template <bool PREFILTER, bool LT3 = true, int HBM1 = 0>
 __device__ __forceinline__ bool shadow_lit_single_settled(const FrameArgs& fa, const double* __restrict__ lds,
                                                           bool resident, uint32_t* __restrict__ stk, V3 hit, V3 o, V3 d,
                                                           V3 lpos, uint32_t li, bool lane_on, Visits& vis) {
     bool redo = false;
-    bool lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, false, redo);
-    if (redo) lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, true, redo);
+    bool lit = shadow_lit_single<PREFILTER, LT3, HBM1>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, false, redo);
+    if (redo)
+        lit = shadow_lit_single<PREFILTER, LT3, HBM1>(fa, lds, resident, stk, hit, o, d, lpos, li, lane_on, vis, true, redo);
     return lit;
 }
 
@@ -1684,7 +1730,7 @@ __device__ __forceinline__ uint64_t out_index(const XferArgs* xf, const BlockDes
     return (uint64_t)(k0 + lx - xf->k0) * xf->ch + (j - xf->y0);
 }
 
-template <bool REL, bool PREFILTER, bool BRUTE>
+template <bool REL, bool PREFILTER, bool BRUTE, int HBM1 = 0>
 __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                               const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                               const BlockDesc& bd, uint32_t q, WaveStats& ws, PhaseClock& pc,
@@ -1745,7 +1791,7 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
     }
     pc.lap(0);
     bool redo = false;
-    Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE>(fa, lds, resident, cam, d,
+    Nearest nh = trace_nearest<REL, PREFILTER, BRUTE, MIRT_PRIMARY_WIDE, HBM1>(fa, lds, resident, cam, d,
                                                                          active && !MIRT_EXP_NO_PRIMARY_TRACE, true, vis,
                                                                          pass2, redo, (classified & 4) != 0, stk, vt, vn, ls, lt, crect);
     pc.lap(1);
@@ -2091,7 +2137,7 @@ __device__ __forceinline__ void redo_mark(const WorkArgs& wa, uint32_t key) {
 //   vf: the chunk's frame within the launch (its view tables, k_trace), ~0u: none.
 //   pass2 / returns: shadow_lit_single's retry.  true = the item must run again with pass2
 //   (nothing was published: no lit bit, no count, no shading); false = done.
-template <bool PREFILTER, bool BRUTE, bool LT3 = true>
+template <bool PREFILTER, bool BRUTE, bool LT3 = true, int HBM1 = 0>
 __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, bool pass2,
@@ -2127,7 +2173,7 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
             if (vh) vt = wa.views + (size_t)q * wa.view_leaves;
         }
         bool redo = false;
-        is_lit = shadow_lit_single<PREFILTER, LT3>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, pass2, redo, vt,
+        is_lit = shadow_lit_single<PREFILTER, LT3, HBM1>(fa, lds, resident, stk, hit, o, d, lpos, l, active, vis, pass2, redo, vt,
                                                    wa.view_leaves, vh);
         if (redo && defer != ~0u) {  // k_trace: the block is traced again at the launch's end
             redo_mark(wa, defer);
@@ -2142,7 +2188,8 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
         }
     } else {
         bool redo = false;
-        Nearest r = trace_nearest<false, PREFILTER, BRUTE>(fa, lds, resident, o, d, active, false, vis, pass2, redo);
+        Nearest r = trace_nearest<false, PREFILTER, BRUTE, false, HBM1>(fa, lds, resident, o, d, active, false, vis, pass2,
+                                                                          redo);
         if (redo && defer != ~0u) {  // k_trace: the block is traced again at the launch's end
             redo_mark(wa, defer);
             redo = false;
@@ -2476,7 +2523,7 @@ __device__ __forceinline__ const FrameRec& frame_rec(const FrameRec* frames, uin
 // One recorded block traced again from its pixels (redo_mark), every query with its second pass
 // in place: primary_block's raygen, the nearest hit, one shadow query per light and phong
 // (shadow_item's arithmetic, lane by lane), and all of the block's outputs.
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+template <bool PREFILTER, bool BRUTE, bool RESIDENT, int HBM1 = 0>
 __device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes& out, const BlockDesc& bd,
                                            const XferArgs* xf) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2493,7 +2540,8 @@ __device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes&
                scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
     const V3 d = norm(sub(p, cam));
     Visits vis{0, 0, 0, 0};
-    const Nearest nh = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, g_lds_mesh, RESIDENT, cam, d, active, true, vis);
+    const Nearest nh =
+        trace_nearest_settled<false, PREFILTER, BRUTE, HBM1>(fa, g_lds_mesh, RESIDENT, cam, d, active, true, vis);
     const bool hit = active && nh.ok;
     const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
     uint32_t lit = 0;
@@ -2506,9 +2554,11 @@ __device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes&
         }
         bool is_lit;
         if (segment) {
-            is_lit = shadow_lit_single_settled<PREFILTER>(fa, g_lds_mesh, RESIDENT, nullptr, nh.hit, o, sd, lpos, l, hit, vis);
+            is_lit = shadow_lit_single_settled<PREFILTER, true, HBM1>(fa, g_lds_mesh, RESIDENT, nullptr, nh.hit, o, sd, lpos,
+                                                                        l, hit, vis);
         } else {
-            const Nearest r = trace_nearest_settled<false, PREFILTER, BRUTE>(fa, g_lds_mesh, RESIDENT, o, sd, hit, false, vis);
+            const Nearest r =
+                trace_nearest_settled<false, PREFILTER, BRUTE, HBM1>(fa, g_lds_mesh, RESIDENT, o, sd, hit, false, vis);
             is_lit = !r.ok || len(sub(lpos, nh.hit)) < len(sub(r.hit, nh.hit));
         }
         if (hit && is_lit) lit |= 1u << l;
@@ -2539,7 +2589,7 @@ __device__ __forceinline__ void redo_block(const FrameArgs& fa, const OutPlanes&
 // the work description read through the constant address space.
 typedef const __attribute__((address_space(4))) WorkArgs ConstWorkArgs;
 constexpr size_t kTraceWaOffset = kalign(sizeof(FrameRecs), alignof(WorkArgs));  // k_trace's second argument
-template <bool PREFILTER, bool BRUTE, bool RESIDENT>
+template <bool PREFILTER, bool BRUTE, bool RESIDENT, int HBM1 = 0>
 __device__ __attribute__((noinline)) void trace_redo_entry(const FrameRec* frames, const WorkArgs* wap, uint32_t e) {
     frames = uni_ptr(frames);
     const WorkArgs& wa = *(const WorkArgs*)(ConstWorkArgs*)uni_ptr(wap);
@@ -2551,12 +2601,12 @@ __device__ __attribute__((noinline)) void trace_redo_entry(const FrameRec* frame
     const BlockDesc bd{(uint32_t)__builtin_amdgcn_readfirstlane(qv[0]), (uint32_t)__builtin_amdgcn_readfirstlane(qv[1]),
                        (uint32_t)__builtin_amdgcn_readfirstlane(qv[2]), 0u};
     const FrameRec& fr = frame_rec(frames, f);
-    redo_block<PREFILTER, BRUTE, RESIDENT>(fr.fa, fr.out, bd, &fr.xf);
+    redo_block<PREFILTER, BRUTE, RESIDENT, HBM1>(fr.fa, fr.out, bd, &fr.xf);
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_store(&wa.bmap[f * wa.nblocks_frame + qbl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false>
+template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false, int HBM1 = 0>
 MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
     const FrameArgs& fa = recs.r[0].fa;
     // (recs is the first kernel argument: offset 0 of the kernarg segment; taking its address
@@ -2580,7 +2630,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
     __shared__ uint32_t s_vstate[VIEWS ? kMaxViewTables : 1];
     const ViewCache vc{s_vhead, s_vstate};
     // RESIDENT implies one object and no MIRT_OPT_NO_SEGMENT (is_resident): a constant there
-    const bool segment = RESIDENT ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
+    const bool segment = (RESIDENT || HBM1) ? !BRUTE : (!BRUTE && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT));
     WaveClock clock;
     uint32_t taken = 0;
     if (blockIdx.x == 0)  // the next frame's counter set (see mirt_internal.hpp)
@@ -2600,6 +2650,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
         __syncthreads();
     }
     if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
+    if (HBM1 == 2 && threadIdx.x < kWG / 64) g_stream_base[threadIdx.x] = ~0u;  // no window yet (read after the batch barrier)
     uint32_t* stk = wstk[threadIdx.x >> 6];
     WaveStats wp{0, 0, 0, 0, 0}, wsh{0, 0, 0, 0, 0};
     PhaseClock pc;
@@ -2723,7 +2774,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
                 const FrameRec& fr = frame_rec(frames, cf);
                 const uint32_t cp = __builtin_amdgcn_readfirstlane(chunk_pos[c]);
                 const uint32_t ck = __builtin_amdgcn_readfirstlane(chunk_key[c]);
-                shadow_item<PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64, l, wsh,
+                shadow_item<PREFILTER, BRUTE, true, HBM1>(fr.fa, wa, fr.out, lds, stk, RESIDENT, segment, chunk0 + (size_t)cp * 64, l, wsh,
                                               false, RESIDENT ? cf : ~0u, VIEWS ? &vc : nullptr, 64, &s_ring, cp, ck);
                 ic.record(wa, 1, wsh.tests - before.tests, wsh.nodes - before.nodes, 0);
                 pend = kNone;
@@ -2752,7 +2803,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
                     const uint64_t cost0 = wa.block_cost ? __builtin_amdgcn_s_memtime() : 0;
                     const uint32_t cls = __builtin_amdgcn_readfirstlane(bq_cull[t]);
                     const uint32_t key = f << 28 | __builtin_amdgcn_readfirstlane(bq_bl[t]);
-                    if (primary_block<false, PREFILTER, BRUTE>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc, false,
+                    if (primary_block<false, PREFILTER, BRUTE, HBM1>(fr.fa, wa, fr.out, lds, stk, RESIDENT, bd, 0, wp, pc, false,
                                                                use_frustum, frect[f], &lc, cls, vt, wa.view_leaves, &fr.fr,
                                                                key, &fr.xf))
                         redo_mark(wa, key);  // traced again, from its pixels, at the launch's end
@@ -2796,7 +2847,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
         // the deferred second passes (redo_mark): every other workgroup is done
         const uint32_t n = __hip_atomic_load(&wa.bgcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t e = threadIdx.x >> 6; e < n; e += kWG / 64)
-            trace_redo_entry<PREFILTER, BRUTE, RESIDENT>(
+            trace_redo_entry<PREFILTER, BRUTE, RESIDENT, HBM1>(
                 frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset), e);
         __syncthreads();
         if (threadIdx.x == 0 && n) {
@@ -3467,10 +3518,22 @@ hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uin
                         hipStream_t s) {
     const FrameArgs& fa = recs.r[0].fa;
     const bool resident = is_resident(fa);
-    const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0) : 0;
-#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), (R) ? dyn : 0, s, recs, wa)
+    // an HBM mesh streamed through LDS (MIRT_OPT_LDS_STREAM, the default options otherwise): one
+    // chunk slice per wave
+    // a one-object frame of an HBM mesh with segment shadows and the default test (HBM1 > 0: the
+    // kernel takes the object count and the shadow mode as constants), streamed through LDS or not
+    const bool one_hbm = !resident && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT) &&
+                         !(opts & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)) && MIRT_HBM1;
+    const bool stream = one_hbm && (fa.flags & MIRT_OPT_LDS_STREAM);
+    const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0)
+                                : (stream ? kStreamBytes : 0);
+#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), dyn, s, recs, wa)
     if (wa.views && resident && !(opts & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)))
         hipLaunchKernelGGL((k_trace<true, false, true, true>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
+    else if (stream)
+        hipLaunchKernelGGL((k_trace<true, false, false, false, 2>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
+    else if (one_hbm)
+        hipLaunchKernelGGL((k_trace<true, false, false, false, 1>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
     else
         MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE

@@ -1003,6 +1003,8 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     if (nf == 0 || nf > kMaxFrames) return fail(MIRT_E_INVALID, "1..8 frames per launch");
     const bool one_launch = !(c->flags & MIRT_OPT_SPLIT_KERNELS) && !bounces;
     if (nf > 1 && !one_launch) return fail(MIRT_E_INVALID, "several frames per launch need the single-kernel path");
+    // LDS streaming of HBM meshes is k_trace's (only its launch sizes the slices)
+    if (!one_launch) sl->h_frames[0].fa.flags &= ~MIRT_OPT_LDS_STREAM;
     const FrameArgs& fa = sl->h_frames[0].fa;
     const OutPlanes out = sl->h_frames[0].out;
     for (uint32_t k = 0; k < nf; ++k)  // the frames' light tables: built / waited for on s
@@ -1770,6 +1772,7 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_frame* f, uint32_t n, const double* 
     FrameArgs fa;
     uint64_t tris;
     fill_args(c, f, 1, 1, fa, tris);
+    fa.flags &= ~MIRT_OPT_LDS_STREAM;  // k_trace's option (k_rays has no slices)
     HIP_TRY(hipMemcpyAsync((void*)io.orig, orig, (size_t)n * 24, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync((void*)io.dir, dir, (size_t)n * 24, hipMemcpyHostToDevice, s));
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n + kWG - 1) / kWG, kWgPerCu * (uint64_t)c->cus));

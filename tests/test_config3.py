@@ -106,3 +106,72 @@ def test_config3_frame_group_8x2_vs_oracle(ctx, config3, config3_ref):
     finally:
         g.close()
         ctx.set_grid()
+
+
+@pytest.fixture(scope="module")
+def sphere6k(tmp_path_factory):
+    """A 6,400-face UV sphere (the configs[3] generator, 40 x 80 cells): beyond the LDS, so its
+    triangles and nodes are read from HBM, small enough for a full-frame oracle."""
+    import gen_sphere_obj as g
+    return g.write(str(tmp_path_factory.mktemp("sphere6k")), stacks=40, slices=80)
+
+
+@pytest.mark.gpu
+def test_hbm_mesh_kernels_and_lds_streaming_equal_oracle(ctx, sphere6k):
+    """Every kernel an HBM-resident mesh can take gives the oracle's frame, every pixel: the
+    one-object HBM k_trace (default), the same with the triangles streamed through each wave's
+    LDS window (MIRT_OPT_LDS_STREAM, north_star's LDS batch streaming), the generic k_trace
+    (MIRT_OPT_NO_SEGMENT) and the split kernels; and the streamed frame group, 4 frames per launch."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    from oracle.oracle import Oracle
+    from oracle.scene_py import load_scene
+    W, H = 160, 120
+    env = rt.Environment.from_file(sphere6k, ctx)
+    assert sum(len(m.face_v) for m in env.meshes) == 6400
+    ref = Oracle(load_scene(sphere6k), use_rtree=True).frame(W, H, nthreads=16)
+    assert ref["valid"].sum() > 1000
+    L = rt._lib
+    for opts in (0, L.MIRT_OPT_LDS_STREAM, L.MIRT_OPT_NO_SEGMENT, L.MIRT_OPT_SPLIT_KERNELS,
+                 L.MIRT_OPT_LDS_STREAM | L.MIRT_OPT_NO_OCTANT):
+        ctx.set_options(opts)
+        try:
+            fb = rt.draw(env, W, H)
+        finally:
+            ctx.set_options(0)
+        for k in ("valid", "face", "rgb", "rgb8"):
+            assert np.array_equal(getattr(fb, k), ref[k]), (opts, k)
+    ctx.set_options(L.MIRT_OPT_LDS_STREAM)
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=8, batch=4, with_rgb=True)
+    try:
+        fr = env.mutable().to_frame()
+        last = None
+        for _ in range(9):
+            last = g.render(fr)
+        g.wait()
+        g.flush()
+        torch.cuda.synchronize()
+        dev = g.frames[last % 8]
+        assert np.array_equal(dev.rgb.cpu().numpy(), ref["rgb"])
+        assert np.array_equal(dev.valid.cpu().numpy(), ref["valid"])
+    finally:
+        g.close()
+        ctx.set_options(0)
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
+def test_config3_lds_stream_4k_subsample_vs_oracle(ctx, config3, config3_ref):
+    """configs[3] with the triangles streamed through LDS: every 8th column, bit-exact."""
+    import distributed_raytracer_amd as rt
+    ref, sub = config3_ref
+    env = rt.Environment.from_file(config3, ctx)
+    ctx.set_options(rt._lib.MIRT_OPT_LDS_STREAM)
+    try:
+        fb = rt.draw(env, W4K, H4K)
+    finally:
+        ctx.set_options(0)
+    assert np.array_equal(fb.valid[sub], ref["valid"])
+    assert np.array_equal(fb.rgb8[sub], ref["rgb8"])
+    _check_rgb(fb.rgb[sub], ref)

@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # a bench "launch" (one frame's kernels) runs each once, or (reflection levels: k_shadow,
 # k_pack, k_bounce) a fixed number of times
 FRAME_KERNELS = ("k_trace", "k_primary", "k_shadow", "k_reflect", "k_pack", "k_bounce", "k_refl_fold")
-ORDER = ("warmup", "timed", "device_only", "profiled", "latency")
+ORDER = ("warmup", "timed", "device_only", "profiled", "latency", "parity_rgb")
 
 
 def bench_line(log: str) -> dict:
@@ -52,6 +52,11 @@ def regions(dispatches, launches: dict, kernel: str = "k_trace"):
     dispatched m times per launch: m consecutive dispatches per launch)."""
     names = [r for r in ORDER if launches.get(r)]
     total = sum(launches[r] for r in names)
+    if "parity_rgb" not in launches and len(dispatches) == total + 1:
+        # a bench line from before the parity re-trace was counted: it is the last dispatch
+        launches = dict(launches, parity_rgb=1)
+        names.append("parity_rgb")
+        total += 1
     m = len(dispatches) // total if total else 0
     if m < 1 or len(dispatches) != m * total:
         raise SystemExit(f"{len(dispatches)} {kernel} dispatches but the bench reports {total} launches {launches}")
