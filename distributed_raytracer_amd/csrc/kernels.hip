@@ -2660,49 +2660,8 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
     // overflow statistic (tests assert 0) and leaves, so the kernel always drains
     constexpr uint32_t kSpinLimit = 1u << 24;
     uint32_t spins = 0;
-    const uint32_t G = gridDim.x, w = blockIdx.x;
-    // Cost deal.  A workgroup lives as long as its waves' summed work, and the lattice gives
-    // each workgroup a Poisson-like count of the expensive (hit) blocks, so workgroups end over
-    // a wide range of times and the frame's tail runs on few CUs.  Blocks whose trace on this
-    // slot's previous launch took long were listed by cost bucket (deal_list); this launch
-    // deals them serpentine over the workgroups in bucket order (dearest first), so every
-    // workgroup gets an even share of the cost, and the lattice takes every other block.  The
-    // previous launch's stamps tell the lattice which blocks the list covers, so each block of
-    // the launch is queued exactly once whatever the list holds (another camera, another tile
-    // list: only the balance suffers).  The order of work never changes a result.
-    __shared__ uint32_t s_doff[kDealK + 1], s_dcnt[kDealK], s_dbase[kDealK], s_duse, s_nd;
-    __shared__ uint16_t s_dcost[kBlkQ];  // per queue entry of the batch: its trace time (block_cost's units)
-    // (the deal's arguments are read where they are used, through at_use: held across the work
-    // loop they cost k_trace VGPR spills)
-    auto dargs = []() {
-        return at_use((const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset));
-    };
-    const bool deal_on = wa.deal != nullptr;
-    if (deal_on) {
-        if (threadIdx.x == 0) {
-            const uint32_t id = wa.deal_id, par = id & 1u;
-            const uint32_t* hp = wa.deal + (par ^ 1u) * kDealHdr;  // the previous launch's header
-            const bool use = id > 1 && hp[0] == id - 1;
-            uint32_t acc = 0;
-            for (uint32_t k = 0; k < kDealK; ++k) {
-                s_doff[k] = acc;
-                acc += use ? hp[1 + k] : 0u;
-            }
-            s_doff[kDealK] = acc;
-            s_duse = use ? 1u : 0u;
-            // listed entries g = r G + (r even ? w : G - 1 - w), r = 0, 1, ... below the list's length
-            const uint32_t full = acc / G;
-            s_nd = acc ? full + (((full & 1u) ? G - 1 - w : w) < acc - full * G ? 1u : 0u) : 0u;
-            if (w == 0) wa.deal[par * kDealHdr] = id;  // (its counts were zeroed by the previous launch)
-        }
-        if (threadIdx.x < kDealK) s_dcnt[threadIdx.x] = 0;
-        __syncthreads();
-    } else if (threadIdx.x == 0) {
-        s_nd = 0;
-        s_duse = 0;  // (read by the staging below: the lattice alone)
-    }
-    if (!deal_on) __syncthreads();
-    const uint32_t mine = s_nd + (wa.nblocks > w ? (wa.nblocks - w + G - 1) / G : 0u);
+    const uint32_t G = gridDim.x;
+    const uint32_t mine = wa.nblocks > blockIdx.x ? (wa.nblocks - blockIdx.x + G - 1) / G : 0u;
     const size_t chunk0 = (size_t)blockIdx.x * wa.wg_cap;  // slot of the region's position 0
     auto lds_ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto lds_inc = [](uint32_t* p) {
@@ -2736,26 +2695,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
         u32x4 qv{0u, 0u, 0u, 0u};
         bool culled = false, ocert = false;
         if (t < nc) {
-            // the workgroup's listed blocks first, then its lattice w + k G (over every frame's blocks)
-            const uint32_t v = c0 + t, nd = s_nd;
-            uint32_t b;
-            bool skip = false;
-            if (v < nd) {
-                const WorkArgs* da = dargs();
-                const uint32_t g = v * G + ((v & 1u) ? G - 1 - w : w);
-                uint32_t k = 0;
-                while (k + 1 < kDealK && g >= s_doff[k + 1]) ++k;
-                b = da->deal[deal_list((da->deal_id & 1u) ^ 1u, k, da->deal_stride) + (g - s_doff[k])];
-                skip = b >= wa.nblocks;  // listed by a launch of more frames
-            } else {
-                b = w + (v - nd) * G;
-                if (s_duse) {  // dealt from the list
-                    const WorkArgs* da = dargs();
-                    skip = da->deal[deal_stamp((da->deal_id & 1u) ^ 1u, da->deal_stride) + b] == da->deal_id - 1;
-                }
-            }
-            if (skip) b = 0;
-            s_dcost[t] = 0;
+            const uint32_t b = blockIdx.x + (c0 + t) * G;  // over every frame's blocks
             qf = b / nbf;
             qbl = b - qf * nbf;
             qv = ((const u32x4*)wa.blocks)[(size_t)(qbl % kQShards) * wa.per_shard + qbl / kQShards];
@@ -2763,7 +2703,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
             // FrameRec::live: a block with no pixel in the frame's live rectangle is not queued
             const uint32_t px = qv[1] & 0xffffu, py = qv[1] >> 16, vw = (qv[2] >> 16) & 0xffu, vh = qv[2] >> 24;
             const uint32_t* lv = frame_rec(frames, qf).live;
-            if (!skip && px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1]) {
+            if (px < lv[2] && px + vw > lv[0] && py < lv[3] && py + vh > lv[1]) {
                 if (classify) {
                     culled = !block_may_meet(frame_rec(frames, qf).fr, frect[qf], px, py, vw, vh);
                     ocert = !culled && block_obj_cert(frame_rec(frames, qf), px, py, vw, vh);
@@ -2869,9 +2809,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
                         redo_mark(wa, key);  // traced again, from its pixels, at the launch's end
                     if (wa.block_cost && (threadIdx.x & 63) == 0) {  // this trace's time, for the slot's next frame
                         const uint64_t dc = (__builtin_amdgcn_s_memtime() - cost0) >> 6;
-                        const uint32_t cu = (uint32_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));
-                        wa.block_cost[bq_bl[t]] = (uint16_t)cu;
-                        s_dcost[t] = (uint16_t)cu;  // (the cost deal lists it at the batch's end)
+                        wa.block_cost[bq_bl[t]] = (uint16_t)(dc < 1 ? 1 : (dc > 65535 ? 65535 : dc));
                     }
                     ic.record(wa, 0, wp.tests - before.tests, wp.nodes - before.nodes, wp.hits - before.hits,
                               (pc.acc[0] - ph0) | ((pc.acc[1] - ph1) << 32));
@@ -2896,35 +2834,6 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
         // every wave is done with this batch (each chunk shaded, its ring position free)
         // before it is restaged; the next batch reuses the region from position 0
         __syncthreads();
-        if (dargs()->deal) {
-            // the batch's blocks that took long, listed by cost bucket for the next launch: one
-            // count atomic per bucket and workgroup, then the entries and their stamps
-            const uint32_t u = threadIdx.x;
-            uint32_t k = kDealK, i = 0;
-            const uint32_t cu = u < s_front ? s_dcost[u] : 0u;  // (queued entries: [0, s_front))
-            if (cu) {
-                const uint32_t lg = 31u - (uint32_t)__builtin_clz(cu);
-                if (lg + kDealK > kDealTopLg) {
-                    k = lg >= kDealTopLg ? 0u : kDealTopLg - lg;
-                    i = atomicAdd(&s_dcnt[k], 1u);
-                }
-            }
-            __syncthreads();
-            const WorkArgs* da = dargs();
-            uint32_t* const dl = da->deal;
-            const uint32_t id = da->deal_id, par = id & 1u;
-            if (u < kDealK) {
-                const uint32_t n = s_dcnt[u];
-                s_dbase[u] = n ? atomicAdd(&dl[par * kDealHdr + 1 + u], n) : 0u;
-            }
-            __syncthreads();
-            if (k < kDealK) {
-                const uint32_t bb = (uint32_t)bq_frame[u] * nbf + bq_bl[u];
-                dl[deal_list(par, k, da->deal_stride) + s_dbase[k] + i] = bb;
-                dl[deal_stamp(par, da->deal_stride) + bb] = id;
-            }
-            if (u < kDealK) s_dcnt[u] = 0;  // (read above, before the barrier; the next batch stages first)
-        }
     }
     if (mine == 0) clock.mark_staged();
     if (spins >= kSpinLimit) wp.overflow += 1;
@@ -2934,9 +2843,6 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
     if (wa.timeline && !MIRT_ITEM_TRACE) clock.record(wa, 0, taken);
     const bool last = launch_last(wa);
-    // every workgroup has read the previous launch's counts: they become the next launch's
-    if (last && threadIdx.x < kDealK && dargs()->deal)
-        dargs()->deal[((dargs()->deal_id & 1u) ^ 1u) * kDealHdr + 1 + threadIdx.x] = 0;
     if (last && wa.bgcnt) {
         // the deferred second passes (redo_mark): every other workgroup is done
         const uint32_t n = __hip_atomic_load(&wa.bgcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

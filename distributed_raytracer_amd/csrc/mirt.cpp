@@ -139,9 +139,6 @@ struct Slot {
     size_t gcnt_cap = 0;
     uint16_t* cost = nullptr; // per block of the table: last primary trace time (WorkArgs::block_cost)
     size_t cost_cap = 0;
-    uint32_t* deal = nullptr; // k_trace's cost deal (WorkArgs::deal): deal_words(deal_stride) words
-    size_t deal_cap = 0;
-    uint32_t deal_stride = 0, deal_id = 0;
     cnt_t* counters = nullptr;
     TileDesc* d_tiles = nullptr;
     TileDesc* h_tiles = nullptr;  // pinned staging
@@ -1043,22 +1040,17 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     // rank's share) keeps one block per wave rather than queueing heavy blocks on few waves
     const uint64_t want = std::max<uint64_t>((total + per_wg - 1) / per_wg, std::min<uint64_t>(total, (uint64_t)c->cus));
     const int pgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, max_wg));
-    // k_trace's cost deal (kernels.hip k_trace): with the queue-order costs, off with MIRT_NO_DEAL
-    static const bool no_deal = getenv("MIRT_NO_DEAL") != nullptr, no_cost = getenv("MIRT_NO_COST_ORDER") != nullptr;
-    const bool deal_on = one_launch && !no_cost && !no_deal;
     // k_trace: workgroup w's hit region holds the kHitRing ring positions and one chunk per
-    // block of a batch (a chunk that finds the ring full).  A workgroup owns ceil(total / G)
-    // lattice blocks, and with the cost deal up to ceil(total / G) listed ones besides.
-    const uint64_t own = (total + pgrid - 1) / pgrid;
-    wa.wg_cap = (uint32_t)((kHitRing + std::min<uint64_t>((uint64_t)kBlkQ, deal_on ? 2 * own : own)) * 64);
-    // k_trace (one launch): sized for any grid up to kWgPerCu per CU (G (R + 2 ceil(total / G)) <=
-    // 2 total + G (R + 2)): a launch whose grid differs from the slot's last one
+    // block it owns (a chunk that finds the ring full)
+    wa.wg_cap = (uint32_t)((kHitRing + (total + pgrid - 1) / pgrid) * 64);
+    // k_trace (one launch): sized for any grid up to kWgPerCu per CU (G (R + ceil(total / G)) <=
+    // total + G (R + 1)): a launch whose grid differs from the slot's last one
     // (MIRT_ADAPTIVE_GRID) never regrows the buffers (hipFree synchronises the device).  The split
     // kernels and the reflection levels use the kQShards regions only (no ring), which also size
     // every bounce-wave buffer below.
     const uint64_t hit_slots =
         one_launch ? std::max<uint64_t>({(uint64_t)kQShards * wa.hit_cap, (uint64_t)pgrid * wa.wg_cap,
-                                         (2 * total + (uint64_t)kWgPerCu * c->cus * (kHitRing + 2)) * 64})
+                                         (total + (uint64_t)kWgPerCu * c->cus * (kHitRing + 1)) * 64})
                    : (uint64_t)kQShards * wa.hit_cap;
     if ((r = dev_grow(sl->hits, sl->hits_cap, hit_slots)) != MIRT_OK) return r;
     if ((r = dev_grow(sl->litw, sl->litw_cap, hit_slots)) != MIRT_OK) return r;
@@ -1110,18 +1102,6 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         if ((r = dev_grow(sl->cost, sl->cost_cap, (size_t)sl->nblocks)) != MIRT_OK) return r;
         if (sl->cost_cap != cap0) HIP_TRY(hipMemsetAsync(sl->cost, 0, sl->cost_cap * sizeof(uint16_t), s));
         wa.block_cost = sl->cost;
-    }
-    if (deal_on) {
-        // a larger launch than any before on this slot: a fresh (zeroed) buffer, ids from 1
-        if (total > sl->deal_stride) {
-            if ((r = dev_grow(sl->deal, sl->deal_cap, deal_words(total))) != MIRT_OK) return r;
-            HIP_TRY(hipMemsetAsync(sl->deal, 0, deal_words(total) * sizeof(uint32_t), s));
-            sl->deal_stride = (uint32_t)total;
-            sl->deal_id = 0;
-        }
-        wa.deal = sl->deal;
-        wa.deal_stride = sl->deal_stride;
-        wa.deal_id = ++sl->deal_id;
     }
     wa.hits = sl->hits;
     wa.litw = sl->litw;

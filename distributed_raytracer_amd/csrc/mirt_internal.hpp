@@ -364,24 +364,7 @@ struct WorkArgs {
     // hits per group of kPackGroup blocks (k_pack's prefix sums)
     uint32_t* bmap;
     uint32_t* bgcnt;
-    // k_trace's cost deal (nullptr: every block on the lattice; kernels.hip k_trace, DESIGN.md
-    // §4.4): the slot's deal buffer (deal_stamp / deal_list below), the words per stamp array and
-    // list, and this launch's id on the slot (1, 2, ...; the parity picks the buffer half)
-    uint32_t* deal;
-    uint32_t deal_stride;
-    uint32_t deal_id;
 };
-// Cost deal buffer (u32 words), two halves used by alternate launches of a slot: per half a
-// header of kDealHdr words ([0] the launch id that wrote it, [1 + k] the entries of bucket k),
-// then per half a stamp per block (the id of the launch that listed it) and kDealK lists of
-// block indices.  A block whose primary trace took >= 2^(kDealTopLg - k) x 64 cycles goes to
-// bucket k (k < kDealK); cheaper blocks are not listed.
-constexpr uint32_t kDealK = 6, kDealTopLg = 12, kDealHdr = 32;
-__host__ __device__ constexpr size_t deal_stamp(uint32_t p, size_t S) { return 2 * (size_t)kDealHdr + p * S; }
-__host__ __device__ constexpr size_t deal_list(uint32_t p, uint32_t k, size_t S) {
-    return 2 * (size_t)kDealHdr + 2 * S + ((size_t)p * kDealK + k) * S;
-}
-__host__ __device__ constexpr size_t deal_words(size_t S) { return deal_list(2, 0, S); }
 constexpr uint32_t kPackGroup = 64;  // source chunks per k_pack workgroup (and per counted group)
 // Reflections in waves of bounces (configs[4] extension, kernels.hip k_bounce): level lv's
 // hit records form region sets like the primary's (kQShards regions of hit_cap slots, region
