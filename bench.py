@@ -203,8 +203,11 @@ def parse():
     ap.add_argument("--static-schedule", action="store_true",
                     help="ablation: round-robin work split instead of the dynamic work queues")
     ap.add_argument("--lds-stream", action="store_true",
-                    help="meshes beyond the LDS: stream each leaf's triangles through a per-wave LDS window "
-                         "(MIRT_OPT_LDS_STREAM; same results)")
+                    help="(the default since round 5: meshes beyond the LDS stream each leaf's triangles "
+                         "through a per-wave LDS window; accepted for older command lines)")
+    ap.add_argument("--no-lds-stream", action="store_true",
+                    help="ablation: meshes beyond the LDS read straight from HBM with scalar loads "
+                         "(MIRT_OPT_NO_LDS_STREAM; same results)")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
     ap.add_argument("--profile-json", default="",
@@ -426,7 +429,7 @@ def main():
         rt._lib.MIRT_OPT_STATIC_SCHEDULE if a.static_schedule else 0) | (rt._lib.MIRT_OPT_SPLIT_KERNELS if a.split_kernels else 0) | (
         rt._lib.MIRT_OPT_VIEWS if a.views else 0) | (rt._lib.MIRT_OPT_NO_LIGHT_TABLE if a.no_light_table else 0) | (
         rt._lib.MIRT_OPT_REFLECT_CHAINS if a.reflect_chains else 0) | (rt._lib.MIRT_OPT_NO_BOX_GATE if a.no_box_gate else 0) | (
-        rt._lib.MIRT_OPT_LDS_STREAM if a.lds_stream else 0)
+        rt._lib.MIRT_OPT_LDS_STREAM if a.lds_stream else 0) | (rt._lib.MIRT_OPT_NO_LDS_STREAM if a.no_lds_stream else 0)
     ctx.set_options(opts)
     env = rt.Environment.from_file(a.scene, ctx)
     import dataclasses

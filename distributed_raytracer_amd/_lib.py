@@ -38,6 +38,7 @@ MIRT_OPT_REFLECT_CHAINS = 512
 MIRT_OPT_NO_LIGHT_TABLE = 1024
 MIRT_OPT_NO_BOX_GATE = 2048
 MIRT_OPT_LDS_STREAM = 4096
+MIRT_OPT_NO_LDS_STREAM = 8192
 
 D3 = C.c_double * 3
 

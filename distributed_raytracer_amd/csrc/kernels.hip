@@ -3518,13 +3518,13 @@ hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uin
                         hipStream_t s) {
     const FrameArgs& fa = recs.r[0].fa;
     const bool resident = is_resident(fa);
-    // an HBM mesh streamed through LDS (MIRT_OPT_LDS_STREAM, the default options otherwise): one
-    // chunk slice per wave
+    // an HBM mesh streamed through LDS (the default; MIRT_OPT_NO_LDS_STREAM reads it with scalar
+    // loads): one chunk slice per wave
     // a one-object frame of an HBM mesh with segment shadows and the default test (HBM1 > 0: the
     // kernel takes the object count and the shadow mode as constants), streamed through LDS or not
     const bool one_hbm = !resident && fa.n_objects == 1 && !(fa.flags & MIRT_OPT_NO_SEGMENT) &&
                          !(opts & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)) && MIRT_HBM1;
-    const bool stream = one_hbm && (fa.flags & MIRT_OPT_LDS_STREAM);
+    const bool stream = one_hbm && !(fa.flags & MIRT_OPT_NO_LDS_STREAM);
     const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0)
                                 : (stream ? kStreamBytes : 0);
 #define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), dyn, s, recs, wa)

@@ -17,7 +17,7 @@ namespace mirt {
 constexpr int kWG = MIRT_WG;  // threads per workgroup of the trace kernels
 // persistent workgroups resident per CU (LDS-bound: each holds the mesh; one workgroup of
 // 12 or 16 waves per CU when built with MIRT_WG 768 / 1024)
-constexpr int kWgPerCu = kWG >= 768 ? 1 : 2;
+constexpr int kWgPerCu = kWG >= 768 ? 1 : 1024 / kWG;  // 16 waves per CU at 128 VGPRs
 constexpr int kBlk = 8;
 // Doubles per triangle record in HBM and LDS: P1, E1 = P2-P1, E2 = P3-P1 (72 B).
 constexpr int kTriD = 9;

@@ -262,8 +262,11 @@ int mirt_profile_read(mirt_ctx *ctx, mirt_profile *out);
 #define MIRT_OPT_NO_BOX_GATE 2048u  /* ablation: skip the reference's Box.Intersect of the face and object boxes
                                        (box.go:29-68), i.e. brute-force semantics; DESIGN.md §4.2 */
 #define MIRT_OPT_LDS_STREAM 4096u   /* meshes beyond the LDS: each wave streams the BVH-ordered triangles of the
-                                       leaves it tests through an LDS slice in chunks of 112 faces (k_trace;
-                                       same results) */
+                                       leaves its primary rays test through an LDS slice in chunks of 112 faces
+                                       (k_trace; same results).  The default since ABI 7's
+                                       round-5 build: the flag is accepted and changes nothing */
+#define MIRT_OPT_NO_LDS_STREAM 8192u /* ablation: meshes beyond the LDS read by the primary rays straight from
+                                       HBM with scalar loads (the round-4 default; same results) */
 int mirt_set_options(mirt_ctx *ctx, uint32_t flags);
 /*
  * Launch shape of the frame kernel: every workgroup owns at least min_blocks_per_wg 8x8

@@ -119,9 +119,11 @@ def sphere6k(tmp_path_factory):
 @pytest.mark.gpu
 def test_hbm_mesh_kernels_and_lds_streaming_equal_oracle(ctx, sphere6k):
     """Every kernel an HBM-resident mesh can take gives the oracle's frame, every pixel: the
-    one-object HBM k_trace (default), the same with the triangles streamed through each wave's
-    LDS window (MIRT_OPT_LDS_STREAM, north_star's LDS batch streaming), the generic k_trace
-    (MIRT_OPT_NO_SEGMENT) and the split kernels; and the streamed frame group, 4 frames per launch."""
+    one-object HBM k_trace with the primary rays' triangles streamed through each wave's LDS
+    window (the default: north_star's LDS batch streaming; MIRT_OPT_LDS_STREAM is accepted and
+    changes nothing), the same reading the triangles with scalar loads (MIRT_OPT_NO_LDS_STREAM),
+    the generic k_trace (MIRT_OPT_NO_SEGMENT) and the split kernels; and the streamed frame
+    group, 4 frames per launch."""
     import torch
     import distributed_raytracer_amd as rt
     from distributed_raytracer_amd.framebuffer import NativeFrameGroup
@@ -133,8 +135,8 @@ def test_hbm_mesh_kernels_and_lds_streaming_equal_oracle(ctx, sphere6k):
     ref = Oracle(load_scene(sphere6k), use_rtree=True).frame(W, H, nthreads=16)
     assert ref["valid"].sum() > 1000
     L = rt._lib
-    for opts in (0, L.MIRT_OPT_LDS_STREAM, L.MIRT_OPT_NO_SEGMENT, L.MIRT_OPT_SPLIT_KERNELS,
-                 L.MIRT_OPT_LDS_STREAM | L.MIRT_OPT_NO_OCTANT):
+    for opts in (0, L.MIRT_OPT_NO_LDS_STREAM, L.MIRT_OPT_LDS_STREAM, L.MIRT_OPT_NO_SEGMENT, L.MIRT_OPT_SPLIT_KERNELS,
+                 L.MIRT_OPT_NO_OCTANT, L.MIRT_OPT_NO_LDS_STREAM | L.MIRT_OPT_NO_OCTANT):
         ctx.set_options(opts)
         try:
             fb = rt.draw(env, W, H)
@@ -142,7 +144,7 @@ def test_hbm_mesh_kernels_and_lds_streaming_equal_oracle(ctx, sphere6k):
             ctx.set_options(0)
         for k in ("valid", "face", "rgb", "rgb8"):
             assert np.array_equal(getattr(fb, k), ref[k]), (opts, k)
-    ctx.set_options(L.MIRT_OPT_LDS_STREAM)
+    ctx.set_options(0)
     g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=8, batch=4, with_rgb=True)
     try:
         fr = env.mutable().to_frame()
@@ -162,12 +164,13 @@ def test_hbm_mesh_kernels_and_lds_streaming_equal_oracle(ctx, sphere6k):
 
 
 @pytest.mark.gpu
-def test_config3_lds_stream_4k_subsample_vs_oracle(ctx, config3, config3_ref):
-    """configs[3] with the triangles streamed through LDS: every 8th column, bit-exact."""
+def test_config3_scalar_load_path_4k_subsample_vs_oracle(ctx, config3, config3_ref):
+    """configs[3] with the triangles read by scalar loads instead of streamed through LDS
+    (MIRT_OPT_NO_LDS_STREAM, the round-4 default): every 8th column, bit-exact."""
     import distributed_raytracer_amd as rt
     ref, sub = config3_ref
     env = rt.Environment.from_file(config3, ctx)
-    ctx.set_options(rt._lib.MIRT_OPT_LDS_STREAM)
+    ctx.set_options(rt._lib.MIRT_OPT_NO_LDS_STREAM)
     try:
         fb = rt.draw(env, W4K, H4K)
     finally:
