@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--view", default="default", choices=("default", "away"))
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--host-output", action="store_true", help="the root copies every frame to pinned host memory (the bench's D2H)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +33,7 @@ def main():
         mut = rt.EnvMutables(mut.objects, mut.lights, rt.Camera.new(c.pos, tuple(-np.asarray(c.forward)), c.fov))
     fr = mut.to_frame()
     W, H = (int(x) for x in a.size.split("x"))
-    g = NativeFrameGroup(ctx, W, H, 0, 1, a.tile or None, inflight=a.inflight, batch=a.batch)
+    g = NativeFrameGroup(ctx, W, H, 0, 1, a.tile or None, inflight=a.inflight, batch=a.batch, host_output=a.host_output)
     for _ in range(20):
         g.render(fr)
     g.flush()
@@ -47,7 +48,7 @@ def main():
     g.flush()
     torch.cuda.synchronize()
     print(json.dumps({"tile": a.tile, "inflight": a.inflight, "batch": a.batch, "view": a.view, "size": a.size,
-                      "rehearse": os.environ.get("MIRT_GROUP_REHEARSE", "1"),
+                      "rehearse": os.environ.get("MIRT_GROUP_REHEARSE", "1"), "host_output": a.host_output,
                       "frame_interval_us": round((time.perf_counter() - t0) / a.frames * 1e6, 1),
                       "host_enqueue_us": round((t1 - t0) / a.frames * 1e6, 1),
                       "call_us_p10_50_90": [round(float(np.percentile(calls, q)) * 1e6, 1) for q in (10, 50, 90)]}))
