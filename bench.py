@@ -220,14 +220,16 @@ def parse():
 
 
 def resolve_shape(a) -> None:
-    """Frames in flight F and frames per launch B.  Measured on one MI355X (profiles/
-    r02_shape_sweep.txt): at the driver's 20 frames the whole 1080p frame runs best as 4 in
-    flight x 1 per launch, D2H included (long runs: 8 x 2-4 are a few % faster on the device);
+    """Frames in flight F and frames per launch B.  Measured on one MI355X: the whole 1080p frame
+    runs best as 8 in flight x 1 per launch on 4 streams, each frame's D2H fused into the next
+    launch on its stream (round 5: 300 frames 0.056 vs 0.060 ms at 4 x 1 with the
+    copy kernel between the traces, profiles/r05_ab_fused_copy.txt; earlier shapes:
+    profiles/r02_shape_sweep.txt);
     a rank's 1/N share needs more frames per launch (each workgroup then owns enough blocks
     to hide its heaviest block's chain).  An unset batch keeps at least two launches' worth of
     batch slots so launches overlap."""
     multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
-    F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "4"))
+    F = a.inflight if a.inflight is not None else int(os.environ.get("MIRT_INFLIGHT", "16" if multi else "8"))
     B = a.batch if a.batch is not None else int(os.environ.get("MIRT_BATCH", "4" if multi else "1"))
     F = max(1, min(F, 32))
     if a.split_kernels or a.bounces:

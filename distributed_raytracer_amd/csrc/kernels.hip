@@ -2606,8 +2606,59 @@ __device__ __attribute__((noinline)) void trace_redo_entry(const FrameRec* frame
         __hip_atomic_store(&wa.bmap[f * wa.nblocks_frame + qbl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Bytes [a, b) of src -> dst with the same alignment on both sides (same layout): head
+// bytes, 16-byte words, tail bytes; one wave.
+__device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t a,
+                                          uint64_t b, uint32_t lane) {
+    const uint64_t a16 = min(b, (a + 15) & ~15ull), b16 = max(a16, b & ~15ull);
+    if (a + lane < a16) dst[a + lane] = src[a + lane];
+    for (uint64_t i = a16 + 16 * lane; i < b16; i += 16 * 64) *(uint4*)(dst + i) = *(const uint4*)(src + i);
+    if (b16 + lane < b) dst[b16 + lane] = src[b16 + lane];
+}
+// One column x of frame f of a host copy job (k_copy_rect_host, k_trace's fused copy): one wave.
+__device__ __forceinline__ void copy_column(const HostCopyJobs& jobs, uint32_t f, uint32_t x, uint32_t H, uint32_t lane) {
+    const uint32_t* C = jobs.cur[f];
+    uint32_t a = 1, b = 0;  // this frame's hit rows [a, b) (empty: a > b)
+    if (x >= C[0] && x < C[2]) {
+        const uint8_t* v = jobs.valid[f] + (uint64_t)x * H;
+        bool found = false;
+        for (uint32_t y0 = C[1]; y0 < C[3]; y0 += 64) {  // first hit row, upwards
+            const uint32_t y = y0 + lane;
+            const uint64_t m = __ballot(y < C[3] && v[y] != 0);
+            if (m) {
+                a = y0 + (uint32_t)__builtin_ctzll(m);
+                found = true;
+                break;
+            }
+        }
+        // last hit row, downwards from the rectangle's end (row a is a hit: it stops there)
+        for (uint32_t y1 = C[3]; found; y1 -= 64) {
+            const uint64_t m = __ballot(lane < y1 - a && v[y1 - 1 - lane] != 0);
+            if (m) {
+                b = y1 - (uint32_t)__builtin_ctzll(m);
+                break;
+            }
+        }
+    }
+    const uint32_t prev = jobs.spans[f][x];
+    const uint32_t a0 = prev & 0xffffu, b0 = prev >> 16;
+    uint32_t u0 = a0, u1 = b0;
+    if (a < b) {
+        u0 = a0 < b0 ? min(a, a0) : a;
+        u1 = a0 < b0 ? max(b, b0) : b;
+    }
+    if (u0 < u1) {
+        const uint64_t p0 = (uint64_t)x * H + u0, p1 = (uint64_t)x * H + u1;
+        copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1, lane);
+        copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1, lane);
+    }
+    if (lane == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
+}
+// k_trace's third argument (FusedCopy), read in place from the kernarg segment.
+constexpr size_t kTraceFcOffset = kalign(kTraceWaOffset + sizeof(WorkArgs), alignof(FusedCopy));
+static_assert(kTraceFcOffset + sizeof(FusedCopy) <= 32 * 1024, "k_trace arguments exceed the measured kernarg size");
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false, int HBM1 = 0>
-MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
+MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const FusedCopy fc) {
     const FrameArgs& fa = recs.r[0].fa;
     // (recs is the first kernel argument: offset 0 of the kernarg segment; taking its address
     // would copy it to scratch)
@@ -2648,6 +2699,15 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa) {
         build_view(frame_rec(frames, f), q - f * wa.nviews, wa.views + (size_t)q * wa.view_leaves, wa.view_heads + q, lds,
                    wa.view_tag);
         __syncthreads();
+    }
+    if (fc.n) {
+        // the host copy of an earlier launch's frames on this stream (a column per wave; that
+        // launch has ended: stream order), before this workgroup's tracing: fire and forget
+        const FusedCopy* cp = at_use((const FusedCopy*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceFcOffset));
+        const uint32_t nw = gridDim.x * (kWG / 64), gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        for (uint32_t f = 0; f < cp->n; ++f)
+            for (uint32_t x = cp->jobs.rect[f][0] + gw; x < cp->jobs.rect[f][2]; x += nw)
+                copy_column(cp->jobs, f, x, cp->H, threadIdx.x & 63);
     }
     if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
     if (HBM1 == 2 && threadIdx.x < kWG / 64) g_stream_base[threadIdx.x] = ~0u;  // no window yet (read after the batch barrier)
@@ -3514,7 +3574,7 @@ hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPl
     return hipGetLastError();
 }
 
-hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uint32_t opts,
+hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, const FusedCopy& fc, int grid, uint32_t opts,
                         hipStream_t s) {
     const FrameArgs& fa = recs.r[0].fa;
     const bool resident = is_resident(fa);
@@ -3527,13 +3587,13 @@ hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uin
     const bool stream = one_hbm && !(fa.flags & MIRT_OPT_NO_LDS_STREAM);
     const size_t dyn = resident ? std::max(mesh_lds_bytes(fa), wa.views ? kViewScratchBytes : (size_t)0)
                                 : (stream ? kStreamBytes : 0);
-#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), dyn, s, recs, wa)
+#define K_TRACE(P, B, R) hipLaunchKernelGGL((k_trace<P, B, R>), dim3(grid), dim3(kWG), dyn, s, recs, wa, fc)
     if (wa.views && resident && !(opts & (MIRT_OPT_BRUTE_FORCE | MIRT_OPT_NO_PREFILTER)))
-        hipLaunchKernelGGL((k_trace<true, false, true, true>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
+        hipLaunchKernelGGL((k_trace<true, false, true, true>), dim3(grid), dim3(kWG), dyn, s, recs, wa, fc);
     else if (stream)
-        hipLaunchKernelGGL((k_trace<true, false, false, false, 2>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
+        hipLaunchKernelGGL((k_trace<true, false, false, false, 2>), dim3(grid), dim3(kWG), dyn, s, recs, wa, fc);
     else if (one_hbm)
-        hipLaunchKernelGGL((k_trace<true, false, false, false, 1>), dim3(grid), dim3(kWG), dyn, s, recs, wa);
+        hipLaunchKernelGGL((k_trace<true, false, false, false, 1>), dim3(grid), dim3(kWG), dyn, s, recs, wa, fc);
     else
         MIRT_DISPATCH(K_TRACE);
 #undef K_TRACE
@@ -3704,15 +3764,6 @@ hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t m
     return hipGetLastError();
 }
 
-// Bytes [a, b) of src -> dst with the same alignment on both sides (same layout): head
-// bytes, 16-byte words, tail bytes; one wave.
-__device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t a,
-                                          uint64_t b, uint32_t lane) {
-    const uint64_t a16 = min(b, (a + 15) & ~15ull), b16 = max(a16, b & ~15ull);
-    if (a + lane < a16) dst[a + lane] = src[a + lane];
-    for (uint64_t i = a16 + 16 * lane; i < b16; i += 16 * 64) *(uint4*)(dst + i) = *(const uint4*)(src + i);
-    if (b16 + lane < b) dst[b16 + lane] = src[b16 + lane];
-}
 // grid x: groups of 4 columns (one wave each), z: frame.  Column x holds rows contiguously
 // in both planes (x * H + y).  The column's hit span is found from the valid plane inside
 // this frame's hit rectangle (64 rows per step, from each end inwards: the rows inside the
@@ -3722,44 +3773,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8
 __global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint32_t H) {
     const uint32_t f = blockIdx.z, lane = threadIdx.x & 63;
     const uint32_t* R = jobs.rect[f];
-    const uint32_t* C = jobs.cur[f];
-    for (uint32_t x = R[0] + blockIdx.x * 4 + (threadIdx.x >> 6); x < R[2]; x += gridDim.x * 4) {
-        uint32_t a = 1, b = 0;  // this frame's hit rows [a, b) (empty: a > b)
-        if (x >= C[0] && x < C[2]) {
-            const uint8_t* v = jobs.valid[f] + (uint64_t)x * H;
-            bool found = false;
-            for (uint32_t y0 = C[1]; y0 < C[3]; y0 += 64) {  // first hit row, upwards
-                const uint32_t y = y0 + lane;
-                const uint64_t m = __ballot(y < C[3] && v[y] != 0);
-                if (m) {
-                    a = y0 + (uint32_t)__builtin_ctzll(m);
-                    found = true;
-                    break;
-                }
-            }
-            // last hit row, downwards from the rectangle's end (row a is a hit: it stops there)
-            for (uint32_t y1 = C[3]; found; y1 -= 64) {
-                const uint64_t m = __ballot(lane < y1 - a && v[y1 - 1 - lane] != 0);
-                if (m) {
-                    b = y1 - (uint32_t)__builtin_ctzll(m);
-                    break;
-                }
-            }
-        }
-        const uint32_t prev = jobs.spans[f][x];
-        const uint32_t a0 = prev & 0xffffu, b0 = prev >> 16;
-        uint32_t u0 = a0, u1 = b0;
-        if (a < b) {
-            u0 = a0 < b0 ? min(a, a0) : a;
-            u1 = a0 < b0 ? max(b, b0) : b;
-        }
-        if (u0 < u1) {
-            const uint64_t p0 = (uint64_t)x * H + u0, p1 = (uint64_t)x * H + u1;
-            copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1, lane);
-            copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1, lane);
-        }
-        if (lane == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
-    }
+    for (uint32_t x = R[0] + blockIdx.x * 4 + (threadIdx.x >> 6); x < R[2]; x += gridDim.x * 4) copy_column(jobs, f, x, H, lane);
 }
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
                                  hipStream_t s) {

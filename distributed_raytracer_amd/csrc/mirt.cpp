@@ -977,7 +977,8 @@ bool frames_batchable(const FrameRec& a, const FrameRec& b) {
 }
 
 int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now = 0);
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now = 0,
+                  const FusedCopy* fcopy = nullptr);
 
 // Enqueue primary -> shadow -> shade for a tile list on stream s.
 int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32_t H, const mirt_tile* tiles,
@@ -998,7 +999,8 @@ int enqueue_trace(mirt_ctx* c, Slot* sl, const mirt_frame* f, uint32_t W, uint32
 // Launch the nf frames staged in sl->h_frames (k_trace: one launch for all of them; the
 // split kernels and reflections take one frame).
 int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, const mirt_tile* tiles, uint32_t n,
-                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now) {
+                  uint32_t bounces, hipStream_t s, const volatile int* cancel, uint32_t max_wg_now,
+                  const FusedCopy* fcopy) {
     int r = MIRT_OK;
     if (nf == 0 || nf > kMaxFrames) return fail(MIRT_E_INVALID, "1..8 frames per launch");
     const bool one_launch = !(c->flags & MIRT_OPT_SPLIT_KERNELS) && !bounces;
@@ -1174,7 +1176,8 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
         wa.frames = nullptr;
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));  // the profile brackets k_trace alone
         HT(2);
-        HIP_TRY(launch_trace(*(const FrameRecs*)sl->h_frames, wa, pgrid, c->flags, s));
+        static const FusedCopy no_copy{};
+        HIP_TRY(launch_trace(*(const FrameRecs*)sl->h_frames, wa, fcopy ? *fcopy : no_copy, pgrid, c->flags, s));
         HT(3);
         if (prof) {
             HIP_TRY(hipEventRecord(pr.ev[1], s));
@@ -2252,6 +2255,21 @@ struct mirt_group {
     // lone frame, the first of a burst), the fixed grid otherwise
     uint32_t adaptive_grid = 0;
     int d2h_cus = 0;                    // CUs reserved for the host copies (0: copies on the frame stream)
+    // Fused host copies (whole-screen groups of one rank with FB >= 8 launches in flight, or any
+    // even FB with MIRT_FUSED_COPY=1; =0: off): FB / 2 streams (half_streams), so the F frame
+    // slots cover two launches per stream, and a batch's host copy runs inside the next k_trace
+    // launch on its stream (its first waves, reading framebuffers that launch does not write)
+    // instead of as a kernel between the stream's traces; its ev_done is recorded after that
+    // launch.
+    bool half_streams = false;
+    bool fused_copy = false;
+    struct PendingCopy {
+        bool on = false;
+        uint32_t hs = 0;                // the batch's host ring slot (its ev_done)
+        uint32_t cols = 0;
+        FusedCopy fc{};
+    };
+    std::vector<PendingCopy> pend;     // per stream
     hipStream_t copy_stream = nullptr;
     std::vector<HostFrame> hfb;
     uint32_t* d_spans = nullptr;        // host output: per frame slot and column, the hit span the host holds
@@ -2725,6 +2743,8 @@ void mirt_group_destroy(mirt_group* g) {
     delete g;
 }
 
+static int update_fused_copy(mirt_group* g);
+
 int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world, uint32_t W, uint32_t H,
                       uint32_t tile, uint32_t tile_h, uint32_t inflight, const mirt_outputs* fbs, mirt_group** out) {
     if (!c || !out) return fail(MIRT_E_INVALID, "NULL context or out");
@@ -2817,6 +2837,7 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     }
     int r = group_plan(g.get());
     if (r != MIRT_OK) return r;
+    if ((r = update_fused_copy(g.get())) != MIRT_OK) return r;  // the stream mapping (half_streams)
     if (world > 1) {
         if (!rccl().ok) return fail(MIRT_E_DEVICE, rccl().err);
         HIP_TRY(stream_with_queue(c->cus, &g->comm_stream));
@@ -2874,6 +2895,38 @@ int mirt_group_failed_ranks(const mirt_group* g, uint64_t* mask) {
 
 static int group_flush(mirt_group* g);
 
+// The host copies still waiting for their stream's next launch (fused copies): as their own
+// kernels now, each followed by its batch's ev_done.
+static int flush_pending_copies(mirt_group* g) {
+    if (!g->fused_copy) return MIRT_OK;
+    for (uint32_t b = 0; b < g->pend.size(); ++b) {
+        mirt_group::PendingCopy& p = g->pend[b];
+        if (!p.on) continue;
+        p.on = false;
+        HIP_TRY(launch_copy_rect_host(p.fc.jobs, p.fc.n, g->H, p.cols, g->streams[b]));
+        HIP_TRY(hipEventRecord(g->ev_done[p.hs], g->streams[b]));
+    }
+    return MIRT_OK;
+}
+// Whether this group runs FB / 2 streams and fuses its host copies into its launches (see
+// mirt_group::fused_copy).  A change of the stream mapping drains the group first.
+static int update_fused_copy(mirt_group* g) {
+    const char* e = getenv("MIRT_FUSED_COPY");
+    const bool force_off = e && e[0] == '0', force_on = e && e[0] == '1';
+    const bool half = !g->tiled && g->world <= 1 && g->FB >= 2 && g->FB % 2 == 0 && !force_off &&
+                      (force_on || g->FB >= 8);
+    const bool fused = half && g->host_out && !g->copy_stream && !g->d2h_sdma;
+    int r;
+    if (g->fused_copy && (!fused || half != g->half_streams) && (r = flush_pending_copies(g)) != MIRT_OK) return r;
+    if (half != g->half_streams && g->nb)
+        for (hipStream_t s : g->streams)
+            if (s) HIP_TRY(hipStreamSynchronize(s));
+    g->half_streams = half;
+    g->fused_copy = fused;
+    if (g->pend.size() < g->FB) g->pend.assign(g->FB, mirt_group::PendingCopy());
+    return MIRT_OK;
+}
+
 int mirt_group_set_host_output(mirt_group* g, int enable) {
     if (!g) return fail(MIRT_E_INVALID, "NULL group");
     if (g->rank != 0) return fail(MIRT_E_INVALID, "only the root holds framebuffers");
@@ -2900,6 +2953,7 @@ int mirt_group_set_host_output(mirt_group* g, int enable) {
             HIP_TRY(hipStreamWaitEvent(g->copy_stream, g->ev_traced[0], 0));
         }
     }
+    if (!enable && (r = flush_pending_copies(g)) != MIRT_OK) return r;
     g->host_out = enable != 0;
     if (g->host_out && g->hfb.empty()) {
         if (!g->fb[0].rgb8 || !g->fb[0].valid)
@@ -2915,7 +2969,7 @@ int mirt_group_set_host_output(mirt_group* g, int enable) {
             memset(hf.valid, 0, n);
         }
     }
-    return MIRT_OK;
+    return update_fused_copy(g);
 }
 
 int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_id) {
@@ -2997,7 +3051,7 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
 static int group_flush(mirt_group* g) {
     if (g->bn == 0) return MIRT_OK;
     mirt_ctx* c = g->c;
-    const uint32_t bs = (uint32_t)(g->nb % g->FB);  // the stream and its device slot
+    const uint32_t bs = (uint32_t)(g->nb % (g->half_streams ? g->FB / 2 : g->FB));  // the stream and its device slot
     const uint32_t hs = (uint32_t)(g->nb % g->HB);  // the host ring slot: records and events
     hipStream_t s = g->streams[bs];
     const bool is_root = g->rank == 0;
@@ -3103,8 +3157,22 @@ static int group_flush(mirt_group* g) {
             if (fuse) share_xfer(sh.tiles, br.rect[i], jobs.tag[i], sl->h_frames[i].xf);
             if (narrow[i]) memcpy(sl->h_frames[i].live, br.rect[i], sizeof(br.rect[i]));
         }
+        // fused host copies: this launch's first waves copy the stream's previous batch to the host
+        // (k_trace launches only: before a reflection or split-kernel launch it runs on its own)
+        const bool one_launch = !g->bbounces && !(c->flags & MIRT_OPT_SPLIT_KERNELS);
+        if (g->fused_copy && g->pend[bs].on && !one_launch) {
+            mirt_group::PendingCopy& p = g->pend[bs];
+            p.on = false;
+            HIP_TRY(launch_copy_rect_host(p.fc.jobs, p.fc.n, g->H, p.cols, s));
+            HIP_TRY(hipEventRecord(g->ev_done[p.hs], s));
+        }
+        const FusedCopy* fcp = (g->fused_copy && g->pend[bs].on) ? &g->pend[bs].fc : nullptr;
         int r = launch_frames(c, sl, n, g->W, g->H, sh.tiles.data(), (uint32_t)sh.tiles.size(), g->bbounces, s, nullptr,
-                              max_wg_now);
+                              max_wg_now, fcp);
+        if (fcp && r == MIRT_OK) {  // that batch is in host memory once this launch has ended
+            g->pend[bs].on = false;
+            HIP_TRY(hipEventRecord(g->ev_done[g->pend[bs].hs], s));
+        }
         if (r != MIRT_OK) {
             (void)hipStreamSynchronize(s);
             return r;
@@ -3198,6 +3266,18 @@ static int group_flush(mirt_group* g) {
             HIP_TRY(hipEventRecord(g->ev_done[hs], g->copy_stream));
             ++g->nb;
             return MIRT_OK;
+        } else if (cols && g->fused_copy) {
+            // copied by the stream's next launch (or flush_pending_copies), which records ev_done
+            mirt_group::PendingCopy& p = g->pend[bs];
+            p.on = true;
+            p.hs = hs;
+            p.cols = cols;
+            p.fc.jobs = hj;
+            p.fc.n = n;
+            p.fc.H = g->H;
+            HT(5);
+            ++g->nb;
+            return MIRT_OK;
         } else if (cols) {
             HIP_TRY(launch_copy_rect_host(hj, n, g->H, cols, s));
         }
@@ -3219,7 +3299,7 @@ int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
     g->B = frames_per_launch;
     g->FB = g->F / g->B;
     group_ring(g);
-    return MIRT_OK;
+    return update_fused_copy(g);
 }
 
 int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
@@ -3273,6 +3353,7 @@ int mirt_group_wait(mirt_group* g, void* stream) {
     if (g->broken) return fail(MIRT_E_PEER, "the group lost rank(s) " + ranks_text(g->failed_mask));
     HIP_TRY(hipSetDevice(g->c->device));
     int r = group_flush(g);
+    if (r == MIRT_OK) r = flush_pending_copies(g);
     if (r != MIRT_OK) return r;
     const uint64_t used = std::min<uint64_t>(g->nb, g->HB);
     for (uint64_t b = 0; b < used; ++b) {
@@ -3313,6 +3394,7 @@ int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
                                         "slot until frame index + inflight)");
     int r;
     if (g->bn && index >= g->k - g->bn && (r = group_flush(g)) != MIRT_OK) return r;
+    if ((r = flush_pending_copies(g)) != MIRT_OK) return r;
     // the batch holding the frame: the latest launched batch whose slot lists j
     for (uint32_t b = 0; b < g->HB; ++b) {
         const BatchRec& br = g->binfo[b];

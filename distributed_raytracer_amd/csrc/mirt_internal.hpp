@@ -438,7 +438,8 @@ hipError_t launch_primary(const FrameArgs& fa, const WorkArgs& wa, const OutPlan
                           hipStream_t s);
 hipError_t launch_shadow(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
                          hipStream_t s);
-hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, int grid, uint32_t opts,
+struct FusedCopy;
+hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, const FusedCopy& fc, int grid, uint32_t opts,
                         hipStream_t s);
 hipError_t launch_rays(const FrameArgs& fa, const RayIO& io, int grid, uint32_t opts, hipStream_t s);
 hipError_t launch_reflect(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out, int grid, uint32_t opts,
@@ -489,6 +490,15 @@ struct HostCopyJobs {
     uint32_t rect[kMaxFrames][4];  // columns to visit: x0, -, x1, - (half-open)
     uint32_t cur[kMaxFrames][4];   // this frame's hit rectangle (where to look for hits)
 };
+// k_trace's third argument: a host copy of an EARLIER launch's frames on the same stream (the
+// frame group's fused host output, mirt.cpp group_flush), done by the launch's first waves
+// (n = 0: none).
+struct FusedCopy {
+    HostCopyJobs jobs;
+    uint32_t n;
+    uint32_t H;
+};
+
 // Miss values into whole planes before a frame is traced (mirt_group, whole screen): per
 // frame up to kFillPlanes byte ranges, each set to one byte value (0, or 0xff for the int32
 // -1 of face / object).

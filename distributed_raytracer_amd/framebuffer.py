@@ -491,6 +491,9 @@ class NativeFrameGroup:
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
             wg_factor = float(os.environ.get("MIRT_WG_FACTOR", "4"))
             launches = max(1, self.F // self.B)  # launches in flight
+            fc = os.environ.get("MIRT_FUSED_COPY", "")
+            if world == 1 and not tile and launches % 2 == 0 and fc != "0" and (fc == "1" or launches >= 8):
+                launches //= 2  # F / B / 2 streams, fused host copies (mirt.cpp update_fused_copy)
             ctx.set_grid(int(os.environ.get("MIRT_MIN_BLOCKS", "32")), max(1, int(wg_factor * cus / launches)))
         uid = (C.c_uint8 * 128)()
         if world > 1:

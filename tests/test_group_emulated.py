@@ -201,6 +201,38 @@ def test_host_output_frames(ctx, views, tile, emulate, wait, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight,batch", [(4, 1), (8, 1), (8, 2)])
+def test_host_output_fused_copies(ctx, views, inflight, batch, monkeypatch):
+    """Fused host copies (MIRT_FUSED_COPY=1, mirt.cpp update_fused_copy): a batch's copy runs in
+    the next k_trace launch on its stream, or as its own kernel when the caller asks for the frame
+    first (host_frame, wait).  Host frames read right after each render (every copy flushed on
+    demand) and a run of frames read only after a wait (copies fused into later launches): every
+    host frame equals the oracle over moving, emptying and refilling hit rectangles."""
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_FUSED_COPY", "1")
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=inflight, batch=batch, host_output=True)
+    try:
+        prev = None
+        for name in ORDER * 2:
+            idx = g.render(views[name][0])
+            if prev is not None:
+                rgb8, valid = g.host_frame(prev[0])
+                _check(valid, rgb8, views[prev[1]][1], f"host frame {prev[0]} ({prev[1]})")
+            prev = (idx, name)
+        g.wait()
+        run = []
+        for name in ORDER * 3:
+            run.append((g.render(views[name][0]), name))
+        g.wait()
+        for idx, name in run[-inflight:]:  # the frames whose host slots still hold them
+            rgb8, valid = g.host_frame(idx)
+            _check(valid, rgb8, views[name][1], f"host frame {idx} ({name})")
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("inflight", [2, 4])
 def test_host_output_runahead_reserved_copy_cus(ctx, views, inflight, monkeypatch):
     """Host run-ahead 4 (MIRT_RUNAHEAD) with the host copies on a stream of reserved CUs

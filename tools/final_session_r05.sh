@@ -4,7 +4,7 @@
 #                                            configs[3], configs[4], the driver command's profile
 #   bash tools/final_session_r05.sh extra    the N-rank rehearsal table, configs[3]/[4] profiles
 set -u
-TAG=r05f
+TAG=${TAG:-r05f}
 OUT=gpurun_out/final_$TAG; mkdir -p $OUT
 case ${1:-main} in
   main)
