@@ -2254,6 +2254,14 @@ struct mirt_group {
     // chip shared among them; 2 the whole chip for a launch issued when none is running (a
     // lone frame, the first of a burst), the fixed grid otherwise
     uint32_t adaptive_grid = 0;
+    // Lone-frame hold (whole-screen groups of one rank; MIRT_LONE_HOLD=0 turns it off): a full
+    // batch submitted while the group's last launch has ended is held, not launched.  The next
+    // mirt_trace_frame launches it with the fixed grid (a burst has begun); mirt_group_wait or
+    // mirt_group_frame_host launch it alone with the whole chip (kWgPerCu per CU), which a
+    // caller that waits on each frame (a BulkTrace order) gets.
+    bool lone_hold = false;
+    bool held = false;                  // the open batch is full and held
+    bool lone_next = false;             // the next group_flush launches with the whole chip
     int d2h_cus = 0;                    // CUs reserved for the host copies (0: copies on the frame stream)
     // Fused host copies (whole-screen groups of one rank with FB >= 8 launches in flight, or any
     // even FB with MIRT_FUSED_COPY=1; =0: off): FB / 2 streams (half_streams), so the F frame
@@ -2810,6 +2818,10 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
         HIP_TRY(hipEventCreateWithFlags(&g->ev_done[j], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&g->ev_comm, hipEventDisableTiming));
+    {
+        const char* lh = getenv("MIRT_LONE_HOLD");
+        g->lone_hold = world == 1 && !g->tiled && !(lh && !strcmp(lh, "0"));
+    }
     if (g->d2h_cus) HIP_TRY(stream_with_queue(c->cus, &g->copy_stream, c->cus - g->d2h_cus, c->cus));
     g->binfo.assign(ring, BatchRec());
     group_ring(g.get());
@@ -3034,6 +3046,7 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
     g->emu_drop = 0;
     for (uint32_t i = 0; i < g->bn; ++i) lt_unpin(g->c, g->stage[i].fa.ltab);  // the open batch is dropped
     g->bn = 0;
+    g->held = g->lone_next = false;
     g->nb = 0;
     for (BatchRec& br : g->binfo) br = BatchRec();
     for (uint64_t& f : g->slot_frame) f = ~0ull;
@@ -3050,6 +3063,8 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
 // bytes copied on the device), and on the root the trailer check and one unpack launch.
 static int group_flush(mirt_group* g) {
     if (g->bn == 0) return MIRT_OK;
+    const bool lone = g->lone_next;
+    g->held = g->lone_next = false;
     mirt_ctx* c = g->c;
     const uint32_t bs = (uint32_t)(g->nb % (g->half_streams ? g->FB / 2 : g->FB));  // the stream and its device slot
     const uint32_t hs = (uint32_t)(g->nb % g->HB);  // the host ring slot: records and events
@@ -3091,6 +3106,7 @@ static int group_flush(mirt_group* g) {
         else if (running == 0)
             max_wg_now = (uint32_t)(kWgPerCu * (uint64_t)c->cus);
     }
+    if (lone) max_wg_now = (uint32_t)(kWgPerCu * (uint64_t)c->cus);
     // Blocks outside a frame's hit rectangle (every ray misses) are not traced: a share's
     // packed plane is only read inside the rectangle (k_pack_rect), and the whole-screen
     // planes get their miss values first, one fill per batch (FrameRec::live).
@@ -3302,6 +3318,15 @@ int mirt_group_set_batch(mirt_group* g, uint32_t frames_per_launch) {
     return update_fused_copy(g);
 }
 
+// Nothing of the group runs: no batch launched yet, or the last one complete (its ev_done
+// recorded, no host copy of it pending: a pending copy means a burst is going on).
+static bool group_idle(const mirt_group* g) {
+    if (g->nb == 0) return true;
+    for (const mirt_group::PendingCopy& p : g->pend)
+        if (p.on) return false;
+    return hipEventQuery(g->ev_done[(g->nb - 1) % g->HB]) == hipSuccess;
+}
+
 int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     if (!g || !f) return fail(MIRT_E_INVALID, "NULL group or frame");
     if (g->broken) {  // the caller must exclude the failed ranks first
@@ -3318,6 +3343,10 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     uint64_t tris = 0;
     frame_record(c, f, g->W, g->H, OutPlanes{}, rec, tris);
     HT(1);
+    if (g->held && (r = group_flush(g)) != MIRT_OK) {  // a held batch: a burst has begun
+        lt_unpin(c, rec.fa.ltab);
+        return r;
+    }
     // split kernels and reflection frames run one frame per launch
     if (g->bn > 0 && (g->bbounces || f->max_bounces || (c->flags & MIRT_OPT_SPLIT_KERNELS) ||
                       !frames_batchable(g->stage[0], rec)))
@@ -3344,7 +3373,16 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     g->bbounces = f->max_bounces;
     if (index) *index = g->k;
     ++g->k;
-    if (g->bn == g->B || g->bbounces || (c->flags & MIRT_OPT_SPLIT_KERNELS)) return group_flush(g);
+    if (g->bn == g->B || g->bbounces || (c->flags & MIRT_OPT_SPLIT_KERNELS)) {
+        // the group has nothing running: hold the batch until the caller waits (a lone frame,
+        // launched with the whole chip) or submits again (launched then, with the fixed grid)
+        if (g->lone_hold && g->bn == g->B && !g->bbounces && !(c->flags & MIRT_OPT_SPLIT_KERNELS) &&
+            group_idle(g)) {
+            g->held = true;
+            return MIRT_OK;
+        }
+        return group_flush(g);
+    }
     return MIRT_OK;
 }
 
@@ -3352,6 +3390,7 @@ int mirt_group_wait(mirt_group* g, void* stream) {
     if (!g) return fail(MIRT_E_INVALID, "NULL group");
     if (g->broken) return fail(MIRT_E_PEER, "the group lost rank(s) " + ranks_text(g->failed_mask));
     HIP_TRY(hipSetDevice(g->c->device));
+    g->lone_next = g->held;  // a held batch runs alone: the whole chip
     int r = group_flush(g);
     if (r == MIRT_OK) r = flush_pending_copies(g);
     if (r != MIRT_OK) return r;
@@ -3393,6 +3432,7 @@ int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
         return fail(MIRT_E_INVALID, "frame " + std::to_string(index) + " is not held (enqueued frames keep their " +
                                         "slot until frame index + inflight)");
     int r;
+    g->lone_next = g->held && index >= g->k - g->bn;
     if (g->bn && index >= g->k - g->bn && (r = group_flush(g)) != MIRT_OK) return r;
     if ((r = flush_pending_copies(g)) != MIRT_OK) return r;
     // the batch holding the frame: the latest launched batch whose slot lists j

@@ -143,6 +143,44 @@ def test_adaptive_grid_lone_and_burst_frames(ctx, views, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hold,host_output", [("1", False), ("1", True), ("0", True)])
+def test_lone_hold_lone_and_burst_frames(ctx, views, hold, host_output, monkeypatch):
+    """Lone-frame hold (MIRT_LONE_HOLD, mirt.cpp mirt_trace_frame): a frame submitted while the
+    group runs nothing is held; a wait launches it alone on the whole chip, a further submit
+    launches it with the fixed grid.  Lone frames (render + wait), bursts and host frames read
+    between renders (mirt_group_frame_host on a held frame) all equal the oracle, with the fused
+    host copies (8 in flight) carrying copies across both launch shapes."""
+    import torch
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_LONE_HOLD", hold)
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=8, host_output=host_output)
+    try:
+        for rep in range(2):
+            for k, name in enumerate(ORDER):
+                idx = g.render(views[name][0])
+                if k % 3 == 0:  # a lone frame: its wait launches it
+                    if host_output:
+                        rgb8, valid = g.host_frame(idx)  # the held frame, launched by this call
+                        _check(valid, rgb8, views[name][1], f"host frame {idx} ({name})")
+                    g.wait()
+                    torch.cuda.synchronize()
+                    got = g.frames[idx % 8]
+                    _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[name][1], f"frame {idx} ({name})")
+            g.wait()
+            torch.cuda.synchronize()
+            for k in range(len(ORDER) - 3, len(ORDER)):
+                idx = rep * len(ORDER) + k
+                got = g.frames[idx % 8]
+                _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), views[ORDER[k]][1], f"frame {idx} ({ORDER[k]})")
+                if host_output:
+                    rgb8, valid = g.host_frame(idx)
+                    _check(valid, rgb8, views[ORDER[k]][1], f"host frame {idx} ({ORDER[k]})")
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 def test_bench_path_full_frame(ctx, views):
     """The bench's own configuration (whole screen, 8 frames in flight, 2 frames per
     k_trace launch, frame records staged per launch): every pixel of each frame, valid,
