@@ -3376,8 +3376,7 @@ int mirt_trace_frame(mirt_group* g, const mirt_frame* f, uint64_t* index) {
     if (g->bn == g->B || g->bbounces || (c->flags & MIRT_OPT_SPLIT_KERNELS)) {
         // the group has nothing running: hold the batch until the caller waits (a lone frame,
         // launched with the whole chip) or submits again (launched then, with the fixed grid)
-        if (g->lone_hold && g->bn == g->B && !g->bbounces && !(c->flags & MIRT_OPT_SPLIT_KERNELS) &&
-            group_idle(g)) {
+        if (g->lone_hold && group_idle(g)) {
             g->held = true;
             return MIRT_OK;
         }
