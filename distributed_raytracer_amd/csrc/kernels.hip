@@ -2619,25 +2619,31 @@ __device__ __forceinline__ void copy_span(const uint8_t* __restrict__ src, uint8
 __device__ __forceinline__ void copy_column(const HostCopyJobs& jobs, uint32_t f, uint32_t x, uint32_t H, uint32_t lane) {
     const uint32_t* C = jobs.cur[f];
     uint32_t a = 1, b = 0;  // this frame's hit rows [a, b) (empty: a > b)
-    if (x >= C[0] && x < C[2]) {
-        const uint8_t* v = jobs.valid[f] + (uint64_t)x * H;
-        bool found = false;
-        for (uint32_t y0 = C[1]; y0 < C[3]; y0 += 64) {  // first hit row, upwards
-            const uint32_t y = y0 + lane;
-            const uint64_t m = __ballot(y < C[3] && v[y] != 0);
-            if (m) {
-                a = y0 + (uint32_t)__builtin_ctzll(m);
-                found = true;
-                break;
+    if (x >= C[0] && x < C[2] && C[1] < C[3]) {
+        // the column's rows [C[1], C[3]) of the valid plane in aligned 8-byte words, 512 rows per
+        // wave-wide step and the steps' loads independent (no chain of dependent loads through the
+        // rectangle: an edge column's few hit rows can lie anywhere in it)
+        const uint64_t x0 = (uint64_t)x * H, beg = x0 + C[1], end = x0 + C[3];
+        const uint8_t* plane = jobs.valid[f];
+        uint32_t lo = ~0u, hi = 0;  // this lane's first / last hit row + 1 (none: lo = ~0u)
+#pragma unroll 4
+        for (uint64_t p = (beg & ~7ull) + 8 * lane; p < end; p += 8 * 64) {
+            uint64_t w = *(const uint64_t*)(plane + p);
+            if (p < beg) w &= ~0ull << (8 * (beg - p));
+            if (end - p < 8) w &= (1ull << (8 * (end - p))) - 1;
+            if (w) {
+                const uint32_t r = (uint32_t)((int64_t)p - (int64_t)x0);
+                lo = min(lo, r + (uint32_t)__builtin_ctzll(w) / 8);
+                hi = max(hi, r + (uint32_t)(63 - __builtin_clzll(w)) / 8 + 1);
             }
         }
-        // last hit row, downwards from the rectangle's end (row a is a hit: it stops there)
-        for (uint32_t y1 = C[3]; found; y1 -= 64) {
-            const uint64_t m = __ballot(lane < y1 - a && v[y1 - 1 - lane] != 0);
-            if (m) {
-                b = y1 - (uint32_t)__builtin_ctzll(m);
-                break;
-            }
+        for (int o = 32; o; o >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+        }
+        if (lo != ~0u) {
+            a = lo;
+            b = hi;
         }
     }
     const uint32_t prev = jobs.spans[f][x];
