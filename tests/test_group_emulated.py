@@ -181,6 +181,42 @@ def test_lone_hold_lone_and_burst_frames(ctx, views, hold, host_output, monkeypa
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [2, 8])
+def test_host_output_odd_height(ctx, env, py_scene, inflight, monkeypatch):
+    """The host copy's span search reads the valid plane in aligned 8-byte words: with an odd
+    screen height (333 x 201) the columns start at every byte alignment and the last column's
+    words run past the plane's end (masked).  Host frames over moving and emptying hit
+    rectangles, lone frames (waited one by one) and bursts (fused copies at 8 in flight) equal
+    the oracle on every pixel."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    from oracle.oracle import Oracle
+    from scenes import with_camera
+    W2, H2 = 333, 201
+    base = env.mutable()
+    frames = []
+    for name, (pos, d, fov) in _cameras(base).items():
+        mut = rt.EnvMutables(base.objects, base.lights, rt.Camera.new(pos, d, fov))
+        ref = Oracle(with_camera(py_scene, pos, d, fov), use_rtree=True).frame(W2, H2, nthreads=8)
+        frames.append((name, mut.to_frame(), ref))
+    g = NativeFrameGroup(ctx, W2, H2, 0, 1, None, inflight=inflight, host_output=True)
+    try:
+        seq = frames + frames[::-1] + frames
+        for k, (name, fr, ref) in enumerate(seq):  # lone frames
+            idx = g.render(fr)
+            rgb8, valid = g.host_frame(idx)
+            _check(valid, rgb8, ref, f"lone host frame {k} ({name})")
+        run = [(g.render(fr), name, ref) for name, fr, ref in seq]  # a burst
+        g.wait()
+        for idx, name, ref in run[-inflight:]:
+            rgb8, valid = g.host_frame(idx)
+            _check(valid, rgb8, ref, f"host frame {idx} ({name})")
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 def test_bench_path_full_frame(ctx, views):
     """The bench's own configuration (whole screen, 8 frames in flight, 2 frames per
     k_trace launch, frame records staged per launch): every pixel of each frame, valid,
