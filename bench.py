@@ -210,6 +210,13 @@ def parse():
                          "(MIRT_OPT_NO_LDS_STREAM; same results)")
     ap.add_argument("--brute-force", action="store_true",
                     help="test every triangle for every ray (the north star's brute force; no BVH culling)")
+    ap.add_argument("--box", type=int, default=0,
+                    help="measure the box drop-in instead (mirt_box_trace_tile, DESIGN.md §5.4): one worker process "
+                         "with N device entries (entry i on device i %% devices present) serving the reference "
+                         "master's BulkTrace orders, --inflight frames in flight, from the native caller "
+                         "worker_c/box_bench (one thread per order, as gRPC serves each in a goroutine)")
+    ap.add_argument("--box-workers", type=int, default=1,
+                    help="--box: the master's partition into this many rectangles per frame (master/main.go:54-91)")
     ap.add_argument("--profile-json", default="",
                     help="per-launch counters of the dominant kernel from rocprofv3 passes of this command "
                          "(tools/roofline.py writes it; used only when its launch shape equals this run's); "
@@ -395,8 +402,60 @@ def load_profile(path: str, shape: dict):
     return pj
 
 
+def box_main(a) -> None:
+    """--box N: the box drop-in under the reference master's traffic.  The
+    native caller worker_c/box_bench keeps --inflight frames in flight, each frame's
+    --box-workers rectangles (master/main.go:54-91) served concurrently by mirt_box_trace_tile
+    into host buffers (rgb8: what TraceResults carries); ms_per_step = wall time / frames.  The
+    last frame, assembled as the master draws it, is checked against the oracle (rgb8, every
+    pixel)."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "worker_c", "box_bench")
+    if not os.path.exists(exe):
+        raise SystemExit(f"{exe} is missing: run __graft_entry__.build()")
+    W, H = a.width, a.height
+    F = a.inflight
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "frame.bin")
+        cmd = [exe, a.scene, str(W), str(H), str(a.box), str(a.box_workers), str(F), str(a.steps), str(a.warmup), out]
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            raise SystemExit(f"box_bench failed ({p.returncode}): {p.stderr[-2000:]}")
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+        rgb8 = np.fromfile(out, np.uint8).reshape(W * H, 3)
+        timers = [ln for ln in p.stderr.splitlines() if ln.startswith("box_timers")]
+    ms = r["ms_per_frame"]
+    line = {
+        "metric": METRIC, "value": round(r["rays_per_frame"] / (ms / 1e3) / 1e6, 3), "unit": "Mrays/s", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: the reference's own example/scene.json, static frame-0 camera",
+        "config": {"workload": f"box drop-in: {os.path.basename(a.scene)} {W}x{H} served as the reference master's "
+                               f"BulkTrace orders ({r['orders_per_frame']} per frame) by one worker process of "
+                               f"{a.box} device entries",
+                   "width": W, "height": H, "box_entries": a.box, "master_workers": a.box_workers,
+                   "orders_per_frame": r["orders_per_frame"], "transport": {1: "rccl", 2: "device copies", 3: "host"}.get(
+                       r["transport"], r["transport"]), "devices_present": r["devices"],
+                   "outputs": "rgb8 into the caller's host buffer (TraceResults colours)"},
+        "frames_in_flight": F, "rays_per_frame": r["rays_per_frame"], "hits_per_frame": r["hits_per_frame"],
+        "caller": "worker_c/box_bench (native threads, one per order)",
+    }
+    if timers:  # MIRT_BOX_TIMERS=1: host time per phase of an order (warmup orders included)
+        line["box_timers"] = timers[-1]
+    if not a.no_parity:
+        from oracle.oracle import Oracle
+        from oracle.scene_py import load_scene
+        ref = Oracle(load_scene(a.scene), use_rtree=True).frame(W, H, nthreads=HOST_CORES)
+        line["parity"] = {"pixels_checked": W * H, "bit_exact": bool(np.array_equal(rgb8, ref["rgb8"])),
+                          "frame": "last timed frame, orders assembled on the host as master/main.go:164-176 draws them"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     a = parse()
+    if a.box:
+        return box_main(a)
     import torch
     import torch.distributed as dist
 

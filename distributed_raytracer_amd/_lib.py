@@ -157,6 +157,7 @@ SIGNATURES = {
     "mirt_debug_fp64": (C.c_int, [_P, C.c_int, C.c_uint32, _P, _P, _P]),
     "mirt_debug_timeline": (C.c_int, [_P, _P, C.c_uint32]),
     "mirt_debug_counters": (C.c_int, [_P, _P, C.c_uint32]),
+    "mirt_debug_kernarg_layout": (C.c_int, [_P, C.c_uint32]),
     "mirt_debug_light_table": (C.c_int, [_P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, _P]),
     "mirt_debug_light_table_gpu": (C.c_int, [_P, _P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, _P]),
     "mirt_set_light_cache": (C.c_int, [_P, C.c_uint64]),

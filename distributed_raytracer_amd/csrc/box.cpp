@@ -14,9 +14,13 @@
 // "host" transport instead copies every device's strips straight into a pinned host buffer
 // over each device's own PCIe link.  Every transport gives the same bytes.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -101,13 +105,26 @@ struct BoxCall {
 
 }  // namespace
 
+// MIRT_BOX_TIMERS=1: host time per phase of the box's orders, summed over calls and printed by
+// mirt_box_destroy (diagnostic).
+struct BoxTimers {
+    bool on = false;
+    std::atomic<uint64_t> ns[6] = {};  // hit rect, enqueue, transfer + wait, expand, whole call, calls
+};
+inline uint64_t box_now() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct mirt_box {
+    BoxTimers tm;
     std::vector<int> dev;              // per entry
     std::vector<mirt_ctx*> ctx;        // per entry
     std::vector<ncclComm_t> comm;      // per entry (RCCL transport)
     int transport = MIRT_BOX_RCCL;
     uint32_t strip = 8;
-    std::mutex mu;                     // the call pool, and the order of RCCL groups on the comms
+    std::mutex mu;                     // the call pool and the settings
+    std::mutex rccl_mu;                // the order of RCCL groups on the comms (issue only)
     std::vector<std::unique_ptr<BoxCall>> calls;
     std::vector<BoxCall*> free_calls;
 };
@@ -179,21 +196,81 @@ struct Deal {
     uint32_t strips_of(uint32_t d) const { return d < active ? (nst - d + active - 1) / active : 0; }
 };
 
-int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t w, uint32_t h, uint32_t W, uint32_t H,
-              const mirt_outputs* hout, const volatile int* cancel, mirt_stats* st, BoxCall* k) {
-    bool want[kPlanes];
-    bool any = false;
-    for (int p = 0; p < kPlanes; ++p) any |= (want[p] = host_plane(hout, p) != nullptr);
+// Miss value of plane p, byte-wise (tracer.go:88-90: colour zero and Trace false; face and
+// object -1, i.e. 0xff bytes).
+uint8_t miss_byte(int p) { return (p == 3 || p == 4) ? 0xff : 0; }
+
+// The order's planes in the caller's buffers: the pixels inside I (the order's part of the
+// frame's hit rectangle) from the pinned staging buffer, which holds I's planes column-major
+// over I's height; every other pixel of the order gets its miss value (no GPU work or transfer
+// for them: their rays cannot meet the object).
+void expand_order(const bool want[kPlanes], const mirt_outputs* hout, const uint8_t* stage, uint32_t x, uint32_t y,
+                  uint32_t w, uint32_t h, const uint32_t I[4]) {
+    const uint32_t iw = I[2] - I[0], ih = I[3] - I[1];
+    const uint64_t ipx = (uint64_t)iw * ih;
+    for (int p = 0; p < kPlanes; ++p) {
+        if (!want[p]) continue;
+        const size_t e = kElem[p], col = (size_t)h * e;
+        uint8_t* dst = (uint8_t*)host_plane(hout, p);
+        const uint8_t mb = miss_byte(p);
+        if (ipx == 0) {
+            memset(dst, mb, (size_t)w * col);
+            continue;
+        }
+        const uint8_t* src = stage + plane_offset(want, ipx, p);
+        const uint32_t c0 = I[0] - x, c1 = I[2] - x, r0 = I[1] - y, r1 = I[3] - y;
+        memset(dst, mb, (size_t)c0 * col);
+        for (uint32_t c = c0; c < c1; ++c) {
+            uint8_t* d = dst + (size_t)c * col;
+            memset(d, mb, (size_t)r0 * e);
+            memcpy(d + (size_t)r0 * e, src + (size_t)(c - c0) * ih * e, (size_t)ih * e);
+            memset(d + (size_t)r1 * e, mb, (size_t)(h - r1) * e);
+        }
+        memset(dst + (size_t)c1 * col, mb, (size_t)(w - c1) * col);
+    }
+}
+
+// Trace the rectangle (x, y, w, h) of frame f on the box's entries and land its requested
+// planes (column-major over h, back to back at plane_offset) in the call's pinned staging
+// buffer k->host; returns once they are there.  One entry traces the rectangle as one tile;
+// several deal it in `strip`-px column strips (strip s to entry s % active) and the strips are
+// assembled on device 0 (RCCL send/recv or device copies) or copied by every entry straight
+// into the staging buffer (host transport).
+int box_trace_rect(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t w, uint32_t h, uint32_t W,
+                   uint32_t H, const bool want[kPlanes], const volatile int* cancel, BoxCall* k, uint32_t& active_out) {
     Deal dl;
-    dl.sw = b->strip;
-    dl.nst = (w + dl.sw - 1) / dl.sw;
-    dl.active = std::min<uint32_t>((uint32_t)b->dev.size(), dl.nst);
-    const uint64_t npx = (uint64_t)w * h;
-    const int dev0 = b->dev[0];
     int tr;
     {
         std::lock_guard<std::mutex> g(b->mu);
         tr = b->transport;
+        dl.sw = b->strip;
+    }
+    dl.nst = (w + dl.sw - 1) / dl.sw;
+    dl.active = std::min<uint32_t>((uint32_t)b->dev.size(), dl.nst);
+    active_out = dl.active;
+    const uint64_t npx = (uint64_t)w * h;
+    const size_t total = plane_offset(want, npx, kPlanes);
+    const int dev0 = b->dev[0];
+    int r;
+    if ((r = grow_on(dev0, k->host, k->host_cap, std::max<size_t>(total, 16), true)) != MIRT_OK) return r;
+    const uint64_t te0 = b->tm.on ? box_now() : 0;
+    if (dl.active == 1) {
+        // one entry: the rectangle is one tile, already the order's i*h + j layout
+        if ((r = grow_on(dev0, k->buf[0], k->buf_cap[0], std::max<size_t>(total, 16))) != MIRT_OK) return r;
+        const mirt_tile t{x, y, w, h};
+        uint64_t pixels = 0;
+        if ((r = trace_tiles_enqueue(b->ctx[0], f, W, H, &t, 1, planes_at(k->buf[0], want, npx), k->s[0], cancel,
+                                     k->sum, &pixels)) != MIRT_OK)
+            return r;
+        BOX_HIP(hipSetDevice(dev0));
+        BOX_HIP(hipMemcpyAsync(k->host, k->buf[0], total, hipMemcpyDeviceToHost, k->s[0]));
+        const uint64_t te1 = b->tm.on ? box_now() : 0;
+        BOX_HIP(hipStreamSynchronize(k->s[0]));
+        if (b->tm.on) {
+            b->tm.ns[1] += te1 - te0;
+            b->tm.ns[2] += box_now() - te1;
+        }
+        return MIRT_OK;
     }
     std::vector<uint64_t> px(dl.active), roff(dl.active, 0);
     std::vector<size_t> bytes(dl.active);
@@ -208,7 +285,6 @@ int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t
         }
     }
     // 1. every entry traces its strips (each strip column-major, back to back)
-    int r;
     std::vector<mirt_tile> tiles;
     for (uint32_t d = 0; d < dl.active; ++d) {
         if ((r = grow_on(b->dev[d], k->buf[d], k->buf_cap[d], std::max<size_t>(bytes[d], 16))) != MIRT_OK) return r;
@@ -223,28 +299,41 @@ int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t
         BOX_HIP(hipEventRecord(k->ev[d], k->s[d]));
     }
     if (cancel && *cancel) return set_error(MIRT_E_CANCELLED, "cancelled");
-    // 2. the entries' planes to device 0 (RCCL or device copies), assembled into the order's layout
-    const uint8_t* src0 = k->buf[0];
-    if (any && dl.active == 1) {
-        // one entry traced every strip back to back: already the order's i*h + j layout
-        BOX_HIP(hipSetDevice(dev0));
-        for (int p = 0; p < kPlanes; ++p)
-            if (want[p])
-                BOX_HIP(hipMemcpyAsync(host_plane(hout, p), src0 + plane_offset(want, npx, p), npx * kElem[p],
-                                       hipMemcpyDeviceToHost, k->s[0]));
-    } else if (any && tr != MIRT_BOX_HOST) {
-        if (dl.active > 1 && (r = grow_on(dev0, k->recv, k->recv_cap, std::max<uint64_t>(rtotal, 16))) != MIRT_OK)
-            return r;
-        if ((r = grow_on(dev0, k->tile, k->tile_cap, plane_offset(want, npx, kPlanes))) != MIRT_OK) return r;
-        if (tr == MIRT_BOX_RCCL && dl.active > 1) {
-            const Rccl& R = rccl();
-            std::lock_guard<std::mutex> g(b->mu);  // every comm sees the groups in one order
-            BOX_RCCL(R.group_start());
-            for (uint32_t d = 1; d < dl.active; ++d) {
-                BOX_RCCL(R.send(k->buf[d], bytes[d], ncclUint8, 0, b->comm[d], k->s[d]));
-                BOX_RCCL(R.recv(k->recv + roff[d], bytes[d], ncclUint8, (int)d, b->comm[0], k->s[0]));
+    // 2. the strips into the staging buffer in the order's layout
+    auto place = [&](uint32_t d, const uint8_t* src, uint8_t* base, hipMemcpyKind kind, hipStream_t s) -> int {
+        const uint32_t m = dl.strips_of(d);
+        const bool last_partial = (w % dl.sw) != 0 && (dl.nst - 1) % dl.active == d;
+        const uint32_t full = last_partial ? m - 1 : m;
+        for (int p = 0; p < kPlanes; ++p) {
+            if (!want[p]) continue;
+            const size_t e = kElem[p], col = (size_t)dl.sw * h * e;
+            const uint8_t* sp = src + plane_offset(want, px[d], p);
+            uint8_t* dp = base + plane_offset(want, npx, p);
+            if (full) BOX_HIP(hipMemcpy2DAsync(dp + d * col, (size_t)dl.active * col, sp, col, col, full, kind, s));
+            if (last_partial) {
+                const size_t sl = dl.nst - 1;
+                BOX_HIP(hipMemcpyAsync(dp + sl * col, sp + (size_t)full * col, (size_t)(w - sl * dl.sw) * h * e, kind, s));
             }
-            BOX_RCCL(R.group_end());
+        }
+        return MIRT_OK;
+    };
+    if (tr != MIRT_BOX_HOST) {
+        if ((r = grow_on(dev0, k->recv, k->recv_cap, std::max<uint64_t>(rtotal, 16))) != MIRT_OK) return r;
+        if ((r = grow_on(dev0, k->tile, k->tile_cap, std::max<size_t>(total, 16))) != MIRT_OK) return r;
+        if (tr == MIRT_BOX_RCCL) {
+            const Rccl& R = rccl();
+            // every comm sees the groups in one order; the lock covers the issue only (the
+            // group runs asynchronously on the call's streams)
+            std::lock_guard<std::mutex> g(b->rccl_mu);
+            BOX_RCCL(R.group_start());
+            ncclResult_t rr = ncclSuccess;
+            for (uint32_t d = 1; d < dl.active && rr == ncclSuccess; ++d) {
+                rr = R.send(k->buf[d], bytes[d], ncclUint8, 0, b->comm[d], k->s[d]);
+                if (rr == ncclSuccess) rr = R.recv(k->recv + roff[d], bytes[d], ncclUint8, (int)d, b->comm[0], k->s[0]);
+            }
+            const ncclResult_t re = R.group_end();  // always closed, also after a failed send/recv
+            if (rr == ncclSuccess) rr = re;
+            if (rr != ncclSuccess) return set_error(MIRT_E_DEVICE, std::string("box RCCL gather: ") + R.error_string(rr));
         } else {
             BOX_HIP(hipSetDevice(dev0));
             for (uint32_t d = 1; d < dl.active; ++d) {
@@ -253,66 +342,61 @@ int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t
             }
         }
         BOX_HIP(hipSetDevice(dev0));
-        for (uint32_t d = 0; d < dl.active; ++d) {
-            const uint8_t* src = d == 0 ? src0 : k->recv + roff[d];
-            const uint32_t m = dl.strips_of(d);
-            const bool last_partial = (w % dl.sw) != 0 && (dl.nst - 1) % dl.active == d;
-            const uint32_t full = last_partial ? m - 1 : m;
-            for (int p = 0; p < kPlanes; ++p) {
-                if (!want[p]) continue;
-                const size_t e = kElem[p], col = (size_t)dl.sw * h * e;
-                const uint8_t* sp = src + plane_offset(want, px[d], p);
-                uint8_t* dp = k->tile + plane_offset(want, npx, p);
-                if (full)
-                    BOX_HIP(hipMemcpy2DAsync(dp + d * col, (size_t)dl.active * col, sp, col, col, full,
-                                             hipMemcpyDeviceToDevice, k->s[0]));
-                if (last_partial) {
-                    const size_t s = dl.nst - 1;
-                    BOX_HIP(hipMemcpyAsync(dp + s * col, sp + (size_t)full * col, (size_t)(w - s * dl.sw) * h * e,
-                                           hipMemcpyDeviceToDevice, k->s[0]));
-                }
-            }
-        }
-        for (int p = 0; p < kPlanes; ++p)
-            if (want[p])
-                BOX_HIP(hipMemcpyAsync(host_plane(hout, p), k->tile + plane_offset(want, npx, p), npx * kElem[p],
-                                       hipMemcpyDeviceToHost, k->s[0]));
-    } else if (any) {
-        // host transport: each entry's strips over its own link into the pinned order
-        if ((r = grow_on(dev0, k->host, k->host_cap, plane_offset(want, npx, kPlanes), true)) != MIRT_OK) return r;
+        for (uint32_t d = 0; d < dl.active; ++d)
+            if ((r = place(d, d == 0 ? k->buf[0] : k->recv + roff[d], k->tile, hipMemcpyDeviceToDevice, k->s[0])) !=
+                MIRT_OK)
+                return r;
+        BOX_HIP(hipMemcpyAsync(k->host, k->tile, total, hipMemcpyDeviceToHost, k->s[0]));
+    } else {
+        // host transport: each entry's strips over its own link into the pinned staging buffer
         for (uint32_t d = 0; d < dl.active; ++d) {
             BOX_HIP(hipSetDevice(b->dev[d]));
-            const uint32_t m = dl.strips_of(d);
-            const bool last_partial = (w % dl.sw) != 0 && (dl.nst - 1) % dl.active == d;
-            const uint32_t full = last_partial ? m - 1 : m;
-            for (int p = 0; p < kPlanes; ++p) {
-                if (!want[p]) continue;
-                const size_t e = kElem[p], col = (size_t)dl.sw * h * e;
-                const uint8_t* sp = k->buf[d] + plane_offset(want, px[d], p);
-                uint8_t* dp = k->host + plane_offset(want, npx, p);
-                if (full)
-                    BOX_HIP(hipMemcpy2DAsync(dp + d * col, (size_t)dl.active * col, sp, col, col, full,
-                                             hipMemcpyDeviceToHost, k->s[d]));
-                if (last_partial) {
-                    const size_t s = dl.nst - 1;
-                    BOX_HIP(hipMemcpyAsync(dp + s * col, sp + (size_t)full * col, (size_t)(w - s * dl.sw) * h * e,
-                                           hipMemcpyDeviceToHost, k->s[d]));
-                }
-            }
+            if ((r = place(d, k->buf[d], k->host, hipMemcpyDeviceToHost, k->s[d])) != MIRT_OK) return r;
         }
     }
-    // 3. wait, then the statistics of every entry
+    const uint64_t te1 = b->tm.on ? box_now() : 0;
     for (uint32_t d = 0; d < dl.active; ++d) {
         BOX_HIP(hipSetDevice(b->dev[d]));
         BOX_HIP(hipStreamSynchronize(k->s[d]));
     }
-    if (any && dl.active > 1 && tr == MIRT_BOX_HOST)
-        for (int p = 0; p < kPlanes; ++p)
-            if (want[p]) memcpy(host_plane(hout, p), k->host + plane_offset(want, npx, p), npx * kElem[p]);
+    if (b->tm.on) {
+        b->tm.ns[1] += te1 - te0;
+        b->tm.ns[2] += box_now() - te1;
+    }
+    return MIRT_OK;
+}
+
+// One order: only its part inside the frame's hit rectangle is traced and crosses PCIe; the
+// rest of the caller's planes is filled with miss values on the host.
+int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t w, uint32_t h, uint32_t W, uint32_t H,
+              const mirt_outputs* hout, const volatile int* cancel, mirt_stats* st, BoxCall* k) {
+    bool want[kPlanes];
+    for (int p = 0; p < kPlanes; ++p) want[p] = host_plane(hout, p) != nullptr;
+    const uint64_t t0 = b->tm.on ? box_now() : 0;
+    uint32_t R[4];
+    int r = frame_hit_rect(b->ctx[0], f, W, H, R);
+    if (r != MIRT_OK) return r;
+    if (b->tm.on) b->tm.ns[0] += box_now() - t0;
+    uint32_t I[4] = {std::max(x, R[0]), std::max(y, R[1]), std::min(x + w, R[2]), std::min(y + h, R[3])};
+    if (I[0] >= I[2] || I[1] >= I[3]) I[0] = I[2] = x, I[1] = I[3] = y;  // no pixel of the order can hit
+    uint32_t active = 0;
+    if (I[2] > I[0]) {
+        r = box_trace_rect(b, f, I[0], I[1], I[2] - I[0], I[3] - I[1], W, H, want, cancel, k, active);
+        if (r != MIRT_OK) return r;
+    }
+    if (cancel && *cancel) return set_error(MIRT_E_CANCELLED, "cancelled");
+    const uint64_t tx = b->tm.on ? box_now() : 0;
+    expand_order(want, hout, k->host, x, y, w, h, I);
+    if (b->tm.on) {
+        const uint64_t t1 = box_now();
+        b->tm.ns[3] += t1 - tx;
+        b->tm.ns[4] += t1 - t0;
+        b->tm.ns[5] += 1;
+    }
     if (st) {
         memset(st, 0, sizeof(*st));
-        st->primary_rays = npx;
-        for (uint32_t d = 0; d < dl.active; ++d) {
+        st->primary_rays = (uint64_t)w * h;
+        for (uint32_t d = 0; d < active; ++d) {
             const cnt_t* s = k->sum + (size_t)d * kStatN;
             st->hits += s[kStatHits];
             st->shadow_rays += s[kStatShadowRays];
@@ -320,7 +404,6 @@ int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t
             st->reflection_rays += s[kStatReflRays];
         }
     }
-    if (cancel && *cancel) return set_error(MIRT_E_CANCELLED, "cancelled");
     return MIRT_OK;
 }
 
@@ -336,6 +419,12 @@ int mirt_device_count(void) {
 
 void mirt_box_destroy(mirt_box* b) {
     if (!b) return;
+    if (b->tm.on && b->tm.ns[5]) {
+        const double n = (double)b->tm.ns[5];
+        fprintf(stderr, "box_timers_us_per_order hit_rect %.2f enqueue %.2f wait %.2f expand %.2f call %.2f (%llu orders)\n",
+                b->tm.ns[0] / n / 1e3, b->tm.ns[1] / n / 1e3, b->tm.ns[2] / n / 1e3, b->tm.ns[3] / n / 1e3,
+                b->tm.ns[4] / n / 1e3, (unsigned long long)b->tm.ns[5]);
+    }
     for (auto& k : b->calls) call_free(b, k.get());
     if (!b->comm.empty() && rccl().ok)
         for (ncclComm_t c : b->comm)
@@ -349,6 +438,10 @@ int mirt_box_create(const int* devices, uint32_t n, mirt_box** out) {
     *out = nullptr;
     if (n < 1 || n > 64) return set_error(MIRT_E_INVALID, "a box drives 1..64 device entries");
     std::unique_ptr<mirt_box, void (*)(mirt_box*)> b(new mirt_box(), mirt_box_destroy);
+    {
+        const char* e = getenv("MIRT_BOX_TIMERS");
+        b->tm.on = e && *e && strcmp(e, "0") != 0;
+    }
     const int count = mirt_device_count();
     for (uint32_t i = 0; i < n; ++i) {
         const int d = devices ? devices[i] : (int)i;

@@ -44,4 +44,8 @@ int trace_tiles_enqueue(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H
                         uint32_t n, const OutPlanes& out, hipStream_t s, const volatile int* cancel,
                         cnt_t* h_summary, uint64_t* pixels);
 
+// The frame's conservative hit rectangle {x0, y0, x1, y1} (half-open) on a W x H screen: every
+// pixel outside it misses (mirt.cpp hit_rect; the whole screen without the block pre-test).
+int frame_hit_rect(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, uint32_t out[4]);
+
 }  // namespace mirt

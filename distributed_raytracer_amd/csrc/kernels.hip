@@ -2289,25 +2289,12 @@ __device__ __forceinline__ void stats_add(WaveStats& a, const WaveStats& b) {
     a.overflow += b.overflow;
 }
 
-// The split kernels' parameters (fa, wa, then a third) in the kernarg segment, read through
-// the constant address space by their out-of-line second passes.
-template <typename T>
-__device__ __forceinline__ const T& kconst(const char* p) {
-    return *(const T*)(const __attribute__((address_space(4))) T*)p;
-}
+// Kernel arguments: the split kernels take theirs by value (the compiler places them); k_trace
+// reads its records and its second and third arguments at the offsets kTraceWaOffset /
+// kTraceFcOffset below, which tests/test_kernarg_layout.py checks against the code object's
+// metadata.  A segment past 4 KB is not a hazard: the vertex-light soups pass with FrameArgs
+// 32 and 224 bytes larger (split kernels' segments of 4096 and 4288 bytes).
 constexpr size_t kalign(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
-constexpr size_t kSplitWaOff = kalign(sizeof(FrameArgs), alignof(WorkArgs));
-// The split kernels' explicit arguments (FrameArgs, WorkArgs, a third of at most 64 bytes) and
-// the ~256 bytes of hidden arguments stay inside 4 KB: with FrameArgs 32 bytes larger (4.1 KB in
-// all) k_primary faulted on one vertex-light soup (round 5), while k_trace's 30 KB segment runs
-// every test; the cause was not isolated, the layout that passes is kept.
-static_assert(kSplitWaOff + sizeof(WorkArgs) + 64 + 256 <= 4096, "split kernels' kernarg segment above 4 KB");
-__device__ __forceinline__ const FrameArgs& split_fa(const char* ka) { return kconst<FrameArgs>(ka); }
-__device__ __forceinline__ const WorkArgs& split_wa(const char* ka) { return kconst<WorkArgs>(ka + kSplitWaOff); }
-template <typename T>
-__device__ __forceinline__ const T& split_third(const char* ka) {
-    return kconst<T>(ka + kalign(kSplitWaOff + sizeof(WorkArgs), alignof(T)));
-}
 
 // The split kernels' deferred second passes (as k_trace's): a work item whose
 // first pass asks for one records itself (two words) and publishes nothing; the launch's last
@@ -2622,7 +2609,9 @@ __device__ __forceinline__ void copy_column(const HostCopyJobs& jobs, uint32_t f
     if (x >= C[0] && x < C[2] && C[1] < C[3]) {
         // the column's rows [C[1], C[3]) of the valid plane in aligned 8-byte words, 512 rows per
         // wave-wide step and the steps' loads independent (no chain of dependent loads through the
-        // rectangle: an edge column's few hit rows can lie anywhere in it)
+        // rectangle: an edge column's few hit rows can lie anywhere in it).  The plane is 8-byte
+        // aligned (mirt_group_create checks caller planes; library planes are hipMalloc'ed), so the
+        // last word stays inside the page of the plane's last byte; its bytes past `end` are masked.
         const uint64_t x0 = (uint64_t)x * H, beg = x0 + C[1], end = x0 + C[3];
         const uint8_t* plane = jobs.valid[f];
         uint32_t lo = ~0u, hi = 0;  // this lane's first / last hit row + 1 (none: lo = ~0u)
@@ -2663,6 +2652,19 @@ __device__ __forceinline__ void copy_column(const HostCopyJobs& jobs, uint32_t f
 // k_trace's third argument (FusedCopy), read in place from the kernarg segment.
 constexpr size_t kTraceFcOffset = kalign(kTraceWaOffset + sizeof(WorkArgs), alignof(FusedCopy));
 static_assert(kTraceFcOffset + sizeof(FusedCopy) <= 32 * 1024, "k_trace arguments exceed the measured kernarg size");
+}  // namespace mirt
+// The layout above as the device code assumes it; tests/test_kernarg_layout.py checks it against
+// the code object's argument metadata for every kernel instantiation.
+extern "C" int mirt_debug_kernarg_layout(uint64_t* out, uint32_t n) {
+    using namespace mirt;
+    const uint64_t v[8] = {sizeof(FrameRecs), kTraceWaOffset,   sizeof(WorkArgs),  kTraceFcOffset,
+                           sizeof(FusedCopy), sizeof(FrameArgs), sizeof(OutPlanes), sizeof(BounceArgs)};
+    if (!out) return MIRT_E_INVALID;
+    const uint32_t k = n < 8 ? n : 8;
+    for (uint32_t i = 0; i < k; ++i) out[i] = v[i];
+    return (int)k;
+}
+namespace mirt {
 template <bool PREFILTER, bool BRUTE, bool RESIDENT, bool VIEWS = false, int HBM1 = 0>
 MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const FusedCopy fc) {
     const FrameArgs& fa = recs.r[0].fa;

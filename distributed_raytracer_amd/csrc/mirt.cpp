@@ -230,6 +230,10 @@ struct mirt_ctx {
     size_t lt_cap = (size_t)4 << 30;    // mirt_set_light_cache
     uint64_t lt_clock = 0;
     uint64_t lt_stat[6] = {0, 0, 0, 0, 0, 0};  // builds, hits, evictions, fallbacks, reused buffers, entries
+    // frame groups on this context: mirt_mesh_release launches their staged (open or held)
+    // batches before it frees a mesh their records point at
+    std::mutex groups_mu;
+    std::vector<mirt_group*> groups;
 };
 
 namespace {
@@ -1541,8 +1545,20 @@ int mirt_mesh_upload(mirt_ctx* c, const double* v, uint32_t nv, const double* vn
     return MIRT_OK;
 }
 
+static int group_launch_staged(mirt_group* g);
+
 int mirt_mesh_release(mirt_ctx* c, uint32_t id) {
     if (!c) return fail(MIRT_E_INVALID, "NULL context");
+    {
+        // a frame group's staged records (an open batch, or one held by the lone-frame hold)
+        // point at the mesh and its light tables: they are launched first, so the device sync
+        // below covers them (a frame submitted before the release is traced, not dropped)
+        std::lock_guard<std::mutex> gl(c->groups_mu);
+        for (mirt_group* grp : c->groups) {
+            int r = group_launch_staged(grp);
+            if (r != MIRT_OK) return r;
+        }
+    }
     std::lock_guard<std::mutex> g(c->mu);
     if (id >= c->meshes.size() || !c->meshes[id].live) return fail(MIRT_E_INVALID, "unknown mesh id");
     HIP_TRY(hipSetDevice(c->device));
@@ -2709,7 +2725,15 @@ void mirt_group_destroy(mirt_group* g) {
             g_ht[7] / g->k, g_ht[8] / g->k, g_ht[9] / g->k, g_ht[10] / g->k, g_ht[11] / g->k);
 #endif
     (void)hipSetDevice(g->c->device);
-    for (uint32_t i = 0; i < g->bn; ++i) lt_unpin(g->c, g->stage[i].fa.ltab);  // never launched
+    {
+        std::lock_guard<std::mutex> gl(g->c->groups_mu);
+        auto& v = g->c->groups;
+        v.erase(std::remove(v.begin(), v.end(), g), v.end());
+    }
+    // frames submitted and not launched yet (an open batch, or one held by the lone-frame hold)
+    // are traced before the group goes, as mirt_group_wait would; a broken group drops them
+    if (g->bn && (g->broken || group_launch_staged(g) != MIRT_OK))
+        for (uint32_t i = 0; i < g->bn; ++i) lt_unpin(g->c, g->stage[i].fa.ltab);  // never launched
     g->bn = 0;
     if (g->comm) {
         // a broken group (a peer stopped answering) may have RCCL work that never ends
@@ -2770,6 +2794,12 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             if (fbs[j].rgb || fbs[j].face || fbs[j].object)
                 return fail(MIRT_E_INVALID, "tiled frame groups produce rgb8 / valid / rgbv only (rgb, face and "
                                             "object planes need tile == 0)");
+    // the host copy (kernels.hip copy_column) scans valid planes in aligned 8-byte words: with
+    // the plane 8-byte aligned, the last word never leaves the page that holds the plane's last
+    // byte, and the bytes past it are masked off
+    if (is_root && fbs)
+        for (uint32_t j = 0; j < inflight; ++j)
+            if ((uintptr_t)fbs[j].valid & 7) return fail(MIRT_E_INVALID, "valid planes must be 8-byte aligned");
     HIP_TRY(hipSetDevice(c->device));
     std::unique_ptr<mirt_group, void (*)(mirt_group*)> g(new mirt_group(), mirt_group_destroy);
     g->c = c;
@@ -2863,6 +2893,10 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             if (r == MIRT_E_TIMEOUT) g->broken = true;
             return r;
         }
+    }
+    {
+        std::lock_guard<std::mutex> gl(c->groups_mu);
+        c->groups.push_back(g.get());
     }
     *out = g.release();
     return MIRT_OK;
@@ -3056,6 +3090,15 @@ int mirt_group_exclude(mirt_group* g, uint64_t alive, const uint8_t* new_unique_
     g->failed_mask = 0;
     g->broken = false;
     return group_plan(g);
+}
+
+// The staged records (an open batch, or a batch the lone-frame hold keeps) launched now: a held
+// batch runs alone with the whole chip, as mirt_group_wait would run it.
+static int group_launch_staged(mirt_group* g) {
+    if (g->bn == 0) return MIRT_OK;
+    HIP_TRY(hipSetDevice(g->c->device));
+    g->lone_next = g->held;
+    return group_flush(g);
 }
 
 // Launch the open batch on its slot's stream: every share's trace, then (tiled) the pack
@@ -3431,8 +3474,11 @@ int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
         return fail(MIRT_E_INVALID, "frame " + std::to_string(index) + " is not held (enqueued frames keep their " +
                                         "slot until frame index + inflight)");
     int r;
-    g->lone_next = g->held && index >= g->k - g->bn;
-    if (g->bn && index >= g->k - g->bn && (r = group_flush(g)) != MIRT_OK) return r;
+    // the frame's own open batch, or a held batch whatever frame is asked for (a pipelined
+    // caller reading frame k - 1 must not leave frame k held while it works on the host)
+    if (g->held || (g->bn && index >= g->k - g->bn)) {
+        if ((r = group_launch_staged(g)) != MIRT_OK) return r;
+    }
     if ((r = flush_pending_copies(g)) != MIRT_OK) return r;
     // the batch holding the frame: the latest launched batch whose slot lists j
     for (uint32_t b = 0; b < g->HB; ++b) {
@@ -3456,3 +3502,24 @@ int mirt_group_frame_host(mirt_group* g, uint64_t index, mirt_outputs* out) {
 }
 
 }  // extern "C"
+
+namespace mirt {
+
+// The frame's hit rectangle on a W x H screen (hit_rect: conservative, every pixel outside it
+// misses), for callers outside the frame group (box.cpp: an order traces and copies only its
+// part inside the rectangle).  Frames without the block pre-test give the whole screen.
+int frame_hit_rect(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H, uint32_t out[4]) {
+    int r = check_frame(c, f);
+    if (r != MIRT_OK) return r;
+    std::unique_ptr<FrameRec> rec(new FrameRec());
+    uint64_t tris = 0;
+    {
+        std::lock_guard<std::mutex> g(c->mu);  // the mesh table
+        fill_args(c, f, W, H, rec->fa, tris);
+        frustum_args(c, f, rec->fa, rec->fr, rec->ocert);
+    }
+    hit_rect(*rec, W, H, out);
+    return MIRT_OK;
+}
+
+}  // namespace mirt

@@ -168,6 +168,9 @@ struct FrameArgs {
     // BVH position (kernels.hip SegPre, mirt.cpp light_table); NULL: no fp32 pre-classification
     const float* ltab;
     uint32_t ltab_n, ltab_pad;  // records per light (= obj[0]'s ntri)
+#ifdef MIRT_FA_PAD
+    uint8_t fa_pad[MIRT_FA_PAD];  // kernarg-layout experiments only
+#endif
 };
 
 // A tiled frame group's share in full-height strips (k_trace only, FrameRec::xf): the rgbv

@@ -52,6 +52,24 @@ class RGB:
         return int(0xFFFF * self.r), int(0xFFFF * self.g), int(0xFFFF * self.b), 0xFFFF
 
 
+def _upload_mesh(fn, handle, vertices, normals, face_v, face_n, face_mat, materials) -> int:
+    """mirt_mesh_upload / mirt_box_mesh_upload: one mesh from numpy arrays; returns its id."""
+    v = np.ascontiguousarray(vertices, np.float64).reshape(-1, 3)
+    vn = np.ascontiguousarray(normals, np.float64).reshape(-1, 3)
+    fv = np.ascontiguousarray(face_v, np.uint32).reshape(-1, 3)
+    fn_ = np.ascontiguousarray(face_n, np.uint32).reshape(-1, 3)
+    fm = np.ascontiguousarray(face_mat, np.uint32).reshape(-1)
+    mats = np.ascontiguousarray(materials, np.float64).reshape(-1, 10)
+    marr = (L.Material * max(1, len(mats)))()
+    for i, m in enumerate(mats):
+        marr[i] = L.Material(_d3(m[0:3]), _d3(m[3:6]), _d3(m[6:9]), float(m[9]))
+    mid = C.c_uint32()
+    L.check(fn(handle, v.ctypes.data if len(v) else None, len(v), vn.ctypes.data if len(vn) else None, len(vn),
+               fv.ctypes.data if len(fv) else None, fn_.ctypes.data if len(fn_) else None,
+               fm.ctypes.data if len(fm) else None, len(fm), marr, len(mats), C.byref(mid)))
+    return mid.value
+
+
 # --------------------------------------------------------------------- context
 class Context:
     """One libmirt context bound to one HIP device (one process per GPU)."""
@@ -83,26 +101,13 @@ class Context:
         except Exception:
             pass
 
-    _upload_fn = "mirt_mesh_upload"
-    _trace_tile_fn = "mirt_trace_tile"
+    def _trace_tile_call(self):
+        """(C entry, handle) that trace_tile calls: a Context traces on its GPU."""
+        return L.lib().mirt_trace_tile, self.handle
 
     def upload_mesh(self, vertices, normals, face_v, face_n, face_mat, materials) -> int:
-        v = np.ascontiguousarray(vertices, np.float64).reshape(-1, 3)
-        vn = np.ascontiguousarray(normals, np.float64).reshape(-1, 3)
-        fv = np.ascontiguousarray(face_v, np.uint32).reshape(-1, 3)
-        fn = np.ascontiguousarray(face_n, np.uint32).reshape(-1, 3)
-        fm = np.ascontiguousarray(face_mat, np.uint32).reshape(-1)
-        mats = np.ascontiguousarray(materials, np.float64).reshape(-1, 10)
-        marr = (L.Material * max(1, len(mats)))()
-        for i, m in enumerate(mats):
-            marr[i] = L.Material(_d3(m[0:3]), _d3(m[3:6]), _d3(m[6:9]), float(m[9]))
-        mid = C.c_uint32()
-        L.check(getattr(L.lib(), self._upload_fn)(
-            self.handle, v.ctypes.data if len(v) else None, len(v),
-            vn.ctypes.data if len(vn) else None, len(vn),
-            fv.ctypes.data if len(fv) else None, fn.ctypes.data if len(fn) else None,
-            fm.ctypes.data if len(fm) else None, len(fm), marr, len(mats), C.byref(mid)))
-        return mid.value
+        return _upload_mesh(L.lib().mirt_mesh_upload, self.handle, vertices, normals, face_v, face_n, face_mat,
+                            materials)
 
     def release_mesh(self, mesh_id: int) -> None:
         L.check(L.lib().mirt_mesh_release(self.handle, mesh_id))
@@ -176,61 +181,78 @@ class Context:
 
 
 # --------------------------------------------------------------------- scene
-class Box(Context):
+class Box:
     """One process driving several GPUs behind BulkTrace (mirt.h mirt_box_*): an order is cut
     into `strip`-px column strips dealt round robin over the devices and assembled on the first
-    (RCCL over xGMI, device copies when devices repeat, or per-device D2H).  Usable wherever a
-    Context is (Environment.from_file / from_gob, trace_tile, draw, Tracer.bulk_trace); entries
-    may repeat a device, so one GPU can stand in for a box."""
+    (RCCL over xGMI, device copies when devices repeat, or per-device D2H).  It serves orders:
+    Environment.from_file / from_gob, trace_tile, draw, Tracer.bulk_trace.  It is NOT a Context:
+    every per-device call (trace_rays, frame groups, light cache, profiling) raises
+    MIRT_E_INVALID on a Box (its handle is a mirt_box, never a mirt_ctx); use box.entry(i) for
+    those.  Entries may repeat a device, so one GPU can stand in for a box."""
 
-    _upload_fn = "mirt_box_mesh_upload"
-    _trace_tile_fn = "mirt_box_trace_tile"
-
-    def __init__(self, devices: Sequence[int]):  # noqa: super().__init__ makes a single-GPU context
+    def __init__(self, devices: Sequence[int]):
         devs = (C.c_int * len(devices))(*[int(d) for d in devices])
-        self._h = C.c_void_p()
-        L.check(L.lib().mirt_box_create(devs, len(devices), C.byref(self._h)))
+        self._bh = C.c_void_p()
+        L.check(L.lib().mirt_box_create(devs, len(devices), C.byref(self._bh)))
         self.devices = [int(d) for d in devices]
         self.device = self.devices[0]
         self._lock = threading.Lock()
-        self._streams = []
+
+    @property
+    def box_handle(self) -> C.c_void_p:
+        if not self._bh:
+            raise L.MirtError(L.MIRT_E_INVALID, "box destroyed")
+        return self._bh
+
+    @property
+    def handle(self) -> C.c_void_p:
+        """A Box has no mirt_ctx handle: per-device entry points fail cleanly, never on a mirt_box."""
+        raise L.MirtError(L.MIRT_E_INVALID, "a Box serves orders (trace_tile / draw / bulk_trace); "
+                                            "use box.entry(i) for per-device calls")
 
     def close(self) -> None:
-        if self._h:
-            L.lib().mirt_box_destroy(self._h)
-            self._h = C.c_void_p()
+        if self._bh:
+            L.lib().mirt_box_destroy(self._bh)
+            self._bh = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _trace_tile_call(self):
+        return L.lib().mirt_box_trace_tile, self.box_handle
+
+    def upload_mesh(self, vertices, normals, face_v, face_n, face_mat, materials) -> int:
+        return _upload_mesh(L.lib().mirt_box_mesh_upload, self.box_handle, vertices, normals, face_v, face_n,
+                            face_mat, materials)
 
     def release_mesh(self, mesh_id: int) -> None:
-        L.check(L.lib().mirt_box_mesh_release(self.handle, mesh_id))
+        L.check(L.lib().mirt_box_mesh_release(self.box_handle, mesh_id))
 
     def set_options(self, flags: int) -> None:
-        L.check(L.lib().mirt_box_set_options(self.handle, flags))
+        L.check(L.lib().mirt_box_set_options(self.box_handle, flags))
 
     @property
     def transport(self) -> int:
-        return int(L.lib().mirt_box_transport(self.handle))
+        return int(L.lib().mirt_box_transport(self.box_handle))
 
     def set_transport(self, transport: int) -> None:
-        L.check(L.lib().mirt_box_set_transport(self.handle, int(transport)))
+        L.check(L.lib().mirt_box_set_transport(self.box_handle, int(transport)))
 
     def set_strip(self, strip: int) -> None:
-        L.check(L.lib().mirt_box_set_strip(self.handle, int(strip)))
+        L.check(L.lib().mirt_box_set_strip(self.box_handle, int(strip)))
 
     def entry(self, i: int) -> "Context":
         """Entry i's context (profiling, light-cache statistics), owned by the box."""
-        h = L.lib().mirt_box_ctx(self.handle, int(i))
+        h = L.lib().mirt_box_ctx(self.box_handle, int(i))
         if not h:
             raise L.MirtError(L.MIRT_E_INVALID, f"no box entry {i}")
         c = Context.__new__(Context)
         c._h, c.device, c._lock, c._streams = C.c_void_p(h), self.devices[i], threading.Lock(), []
         c.close = lambda: None  # the box destroys its entries
         return c
-
-    def _unsupported(self, *a, **k):
-        raise L.MirtError(L.MIRT_E_INVALID, "a Box traces orders (trace_tile / draw / bulk_trace); "
-                                            "use box.entry(i) for per-device calls")
-
-    stream_create = set_grid = profile_enable = profile_read = debug_fp64 = _unsupported
 
 
 @dataclass
@@ -457,8 +479,9 @@ def trace_tile(env: Environment, x: int, y: int, w: int, h: int, W: int, H: int,
     out = L.Outputs(rgb.ctypes.data, rgb8.ctypes.data, valid.ctypes.data, face.ctypes.data, obj.ctypes.data)
     st = L.Stats()
     # a Context traces the tile on its GPU; a Box deals it over the box's GPUs (mirt_box_trace_tile)
-    L.check(getattr(L.lib(), env.ctx._trace_tile_fn)(env.ctx.handle, C.byref(fr), x, y, w, h, W, H, C.byref(out),
-                                                     C.byref(cancel) if cancel is not None else None, C.byref(st)))
+    fn, handle = env.ctx._trace_tile_call()
+    L.check(fn(handle, C.byref(fr), x, y, w, h, W, H, C.byref(out), C.byref(cancel) if cancel is not None else None,
+               C.byref(st)))
     del keep
     return TileResult(rgb, rgb8, valid, face, obj, {k: getattr(st, k) for k, _ in L.Stats._fields_})
 

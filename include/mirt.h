@@ -201,6 +201,8 @@ double mirt_go_minmax(int op, double a, double b);
 int mirt_mesh_upload(mirt_ctx *ctx, const double *v, uint32_t nv, const double *vn, uint32_t nn,
                      const uint32_t *fv, const uint32_t *fn, const uint32_t *fmat, uint32_t nf,
                      const mirt_material *mats, uint32_t nm, uint32_t *mesh_id);
+/* Waits for the device; frames a group on this context staged and has not launched yet (an open
+ * batch, a held lone frame) are launched first, so they never read a freed mesh. */
 int mirt_mesh_release(mirt_ctx *ctx, uint32_t mesh_id);
 
 /*
@@ -320,6 +322,18 @@ int mirt_debug_timeline(mirt_ctx *ctx, uint64_t *out, uint32_t max_records);
 int mirt_debug_counters(mirt_ctx *ctx, uint64_t *out, uint32_t n);
 
 /*
+ * Diagnostic (host only, no device): the kernel-argument layout the library was compiled
+ * with, as the device code assumes it.  k_trace reads its second and third arguments at
+ * hand-computed offsets of the kernarg segment; a CPU test compares these with the code
+ * object's own argument metadata (.args[].offset / .size) for every instantiation.
+ *   [0] sizeof(FrameRecs)  [1] k_trace's WorkArgs offset  [2] sizeof(WorkArgs)
+ *   [3] k_trace's FusedCopy offset  [4] sizeof(FusedCopy)  [5] sizeof(FrameArgs)
+ *   [6] sizeof(OutPlanes)  [7] sizeof(BounceArgs)
+ * Returns the number of words written (<= n).
+ */
+int mirt_debug_kernarg_layout(uint64_t *out, uint32_t n);
+
+/*
  * Diagnostic (host only, no device): the light-table records the library builds for the
  * shadow segments of a one-object frame (kernels.hip SegPre): for n triangles given as
  * P1, E1 = P2 - P1, E2 = P3 - P1 (9 doubles each, the kernels' order), a mesh whose
@@ -373,7 +387,13 @@ void mirt_object_bounds(const double *v, uint32_t nv, const double pos[3], doubl
  * whole screen straight into the framebuffer (no tiles, no RCCL); world == 1 with tile > 0
  * rehearses the tiled path on one GPU.
  *   mirt_group_unique_id: rank 0 makes the RCCL id (128 bytes) every rank passes in.
- *   mirt_trace_frame:     enqueue the next frame (asynchronous; *index = its number).
+ *   mirt_trace_frame:     enqueue the next frame (asynchronous; *index = its number).  Lone-frame
+ *                         hold (world == 1, tile == 0; MIRT_LONE_HOLD=0 turns it off): a batch
+ *                         completed while the group has nothing running is HELD, not launched,
+ *                         and runs at the next mirt_trace_frame (with the fixed grid: a burst has
+ *                         begun) or at mirt_group_wait / mirt_group_frame_host (any index) /
+ *                         mirt_mesh_release / mirt_group_destroy (alone, with the whole chip).  A
+ *                         submitted frame is always traced; none of these calls drops it.
  *   mirt_group_wait:      make `stream` wait for every enqueued frame (NULL: host wait).
  *   mirt_plan_tiles:      rank's tiles of the deal (returns the count; out may be NULL).
  */

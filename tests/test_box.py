@@ -170,3 +170,28 @@ def test_box_entry_profiles_and_options(box8, box_env):
     assert b.stats["tri_tests"] > a.stats["tri_tests"]
     e3 = box8.entry(3)
     assert e3.device == 0 and e3.light_cache_stats()["cap"] > 0
+
+
+def test_box_is_not_a_context(box8, box_env):
+    """A Box's handle is a mirt_box: every per-device entry point (trace_rays, the light cache,
+    profiling, frame groups, async tiles) raises MIRT_E_INVALID instead of reading a mirt_box
+    as a mirt_ctx; its entries still serve those calls."""
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd import _lib
+    from distributed_raytracer_amd.framebuffer import trace_tiles_device
+
+    class Planes:
+        def outputs(self):
+            return _lib.Outputs()
+    assert not isinstance(box8, rt.Context)
+    o = np.zeros((4, 3))
+    d = np.tile([0.0, 0.0, -1.0], (4, 1))
+    calls = [lambda: rt.trace_rays(o, d, box_env), lambda: box8.handle,
+             lambda: trace_tiles_device(box8, box_env.mutable().to_frame(), 8, 8, [(0, 0, 8, 8)], Planes())]
+    for call in calls:
+        with pytest.raises(rt.MirtError) as e:
+            call()
+        assert e.value.code == rt._lib.MIRT_E_INVALID
+    for name in ("light_cache_stats", "profile_enable", "stream_create", "debug_timeline", "set_grid"):
+        assert not hasattr(box8, name), name
+    assert box8.entry(0).light_cache_stats()["cap"] > 0

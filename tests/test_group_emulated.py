@@ -418,3 +418,42 @@ def test_group_argument_errors(ctx):
     finally:
         g.close()
         ctx.set_grid()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["mesh_release", "destroy", "host_frame_of_previous"])
+def test_held_frame_is_launched_not_dropped(ctx, views, how, monkeypatch):
+    """A frame the lone-frame hold keeps (submitted to an idle group) is traced by every call
+    that can follow it: mirt_mesh_release launches it before freeing the mesh its record points
+    at, mirt_group_destroy before the group goes, and mirt_group_frame_host of the PREVIOUS frame
+    (a pipelined caller) before it waits.  The framebuffer then equals the oracle without any
+    mirt_group_wait."""
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    monkeypatch.setenv("MIRT_LONE_HOLD", "1")
+    env2 = rt.Environment.from_file(SCENE, ctx)  # a mesh of its own (the scene's default camera), released below
+    mut = env2.mutable()
+    ref = views["default"][1]
+    g = NativeFrameGroup(ctx, W, H, 0, 1, None, inflight=2, host_output=(how == "host_frame_of_previous"))
+    planes = g.frames
+    try:
+        if how == "host_frame_of_previous":
+            i0 = g.render(mut.to_frame())
+            g.wait()
+            i1 = g.render(mut.to_frame())  # held: the group is idle
+            rgb8, valid = g.host_frame(i0)
+            _check(valid, rgb8, ref, "host frame 0")
+        else:
+            i1 = g.render(mut.to_frame())  # held
+            if how == "mesh_release":
+                for mid in env2.mesh_ids:
+                    ctx.release_mesh(mid)
+            else:
+                g.close()
+        torch.cuda.synchronize()
+        got = planes[i1 % 2]
+        _check(got.valid.cpu().numpy(), got.rgb8.cpu().numpy(), ref, f"{how}: held frame {i1}")
+    finally:
+        g.close()
+        ctx.set_grid()
