@@ -46,6 +46,10 @@
 #ifndef MIRT_WAVES_PER_EU
 #define MIRT_WAVES_PER_EU 4
 #endif
+// k_shadow's occupancy (the split kernels' shadow items: reflection levels, configs[4]).
+#ifndef MIRT_SHADOW_WAVES_PER_EU
+#define MIRT_SHADOW_WAVES_PER_EU MIRT_WAVES_PER_EU
+#endif
 // k_reflect's occupancy (chains option; 2 waves: no spill but 30% slower).
 #ifndef MIRT_REFLECT_WAVES_PER_EU
 #define MIRT_REFLECT_WAVES_PER_EU 4

@@ -504,9 +504,18 @@ struct PhaseClock {
     }
 };
 
+// threadIdx.x made opaque to the compiler: the kernels' end (statistics, summary) recomputes its
+// byte offsets instead of keeping the start's 64-bit copy live through the whole work loop (that
+// copy was k_trace's only spilled VGPR pair)
+__device__ __forceinline__ uint32_t tid_fresh() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], int stat_tests, int stat_nodes,
                                             int stat_leaves, int stat_hits, const WaveStats& w) {
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t tid = tid_fresh();
+    const uint32_t wave = tid >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[wave][0] = w.tests;
         red[wave][1] = w.nodes;
@@ -520,11 +529,11 @@ __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], in
         const cnt_t old = atomicAdd(&counters[cnt_stat(kStatOverflow, 0)], w.overflow);
         asm volatile("" ::"v"(old));
     }
-    if (threadIdx.x < 4) {
+    if (tid < 4) {
         cnt_t sum = 0;
-        for (int k = 0; k < kWG / 64; ++k) sum += red[k][threadIdx.x];
-        const int stat = threadIdx.x == 0 ? stat_tests : threadIdx.x == 1 ? stat_nodes
-                       : threadIdx.x == 2 ? stat_leaves : stat_hits;  // < 0: not recorded
+        for (int k = 0; k < kWG / 64; ++k) sum += red[k][tid];
+        const int stat = tid == 0 ? stat_tests : tid == 1 ? stat_nodes
+                       : tid == 2 ? stat_leaves : stat_hits;  // < 0: not recorded
         if (sum && stat >= 0) {
             const cnt_t old = atomicAdd(&counters[cnt_stat(stat, blockIdx.x % kStatShards)], sum);
             asm volatile("" ::"v"(old));
@@ -762,7 +771,9 @@ __device__ __forceinline__ const double* stream_leaf(cdptr tri, uint32_t ntri, u
     const uint32_t wave = threadIdx.x >> 6;
     double* slice = g_lds_mesh + (size_t)wave * kStreamSlice;
     uint32_t base = __builtin_amdgcn_readfirstlane(g_stream_base[wave]);
+    diag(23);  // leaves served through the window (MIRT_DIAG builds)
     if (base == ~0u || first < base || first + cnt > base + kStreamTris + 1 || first + cnt > ntri) {
+        diag(31);  // window reloads (8 KB each)
         // an even start (16-byte aligned: 72-byte faces), at most ntri - kStreamTris, so the
         // kStreamTris + 1 faces from it cover the leaf
         base = first > kStreamTris / 2 ? first - kStreamTris / 2 : 0u;
@@ -1485,8 +1496,9 @@ __device__ __forceinline__ bool launch_last(const WorkArgs& wa) {
 }
 // The frame's statistics totals, by the launch's last workgroup.
 __device__ __forceinline__ void frame_summary(const FrameArgs& fa, const WorkArgs& wa, bool last) {
-    if (!last || threadIdx.x >= kStatN) return;
-    const int st = threadIdx.x;
+    const uint32_t tid = tid_fresh();
+    if (!last || tid >= kStatN) return;
+    const int st = (int)tid;
     cnt_t sum = 0;
     for (int sh = 0; sh < kStatShards; ++sh)
         sum += atomicAdd(&wa.counters[cnt_stat(st == kStatShadowRays ? kStatHits : st, sh)], (cnt_t)0);
@@ -2427,7 +2439,8 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
 // Work item: the 64 slots of one hit block x one light.  Tickets of shard q enumerate
 // (light, chunk) of region q.
 template <bool PREFILTER, bool BRUTE, bool RESIDENT>
-MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(MIRT_SHADOW_WAVES_PER_EU)))
+void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     double* const lds = g_lds_mesh;  // RESIDENT: the mesh (dynamic LDS sized at launch)
     __shared__ uint32_t wstk[kWG / 64][MIRT_SHADOW_WIDE ? kBvhStack : 1];
     __shared__ cnt_t red[kWG / 64][4];
@@ -2466,6 +2479,7 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
             k = dyn ? peers + ticket_resolve(nxt) : k + peers;
         }
     }
+#ifndef MIRT_EXP_NO_SPLIT_REDO
     if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
         const uint32_t last = split_redo_last(wa);
         for (uint32_t e = threadIdx.x >> 6; e < (last & 0x7fffffffu); e += kWG / 64) {
@@ -2475,6 +2489,7 @@ MIRT_TRACE_KERNEL void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes
         }
         split_redo_reset(wa, last);
     }
+#endif
     stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, ws);
     if (wa.timeline) clock.record(wa, 1, taken);
     if (!wa.bounces) frame_fold(fa, wa);  // otherwise the reflection fold is the frame's last kernel

@@ -294,19 +294,31 @@ void slot_free(Slot* s) {
     if (s->stream) (void)hipStreamDestroy(s->stream);
 }
 
-int slot_acquire(mirt_ctx* c, Slot*& out) {
+// tiles (optional): the call's tile list; a free slot whose cached block table is that list's
+// is preferred (concurrent BulkTrace orders of different rectangles keep their tables)
+int slot_acquire(mirt_ctx* c, Slot*& out, const mirt_tile* tiles = nullptr, uint32_t n = 0) {
     {
         std::lock_guard<std::mutex> g(c->mu);
         out = nullptr;
-        // prefer a free slot whose previous asynchronous work has already completed
+        // prefer a free slot whose previous asynchronous work has already completed, and among
+        // those one that holds this tile list's block table
+        size_t pick = c->free_slots.size();
         for (size_t i = 0; i < c->free_slots.size(); ++i) {
             Slot* s = c->free_slots[i];
             if (!s->pending || hipEventQuery(s->done) == hipSuccess) {
                 s->pending = false;
-                out = s;
-                c->free_slots.erase(c->free_slots.begin() + (long)i);
-                break;
+                const bool same = tiles && s->blocks_key.size() == n &&
+                                  memcmp(s->blocks_key.data(), tiles, sizeof(mirt_tile) * n) == 0;
+                if (pick == c->free_slots.size()) pick = i;
+                if (same || !tiles) {
+                    pick = i;
+                    break;
+                }
             }
+        }
+        if (pick < c->free_slots.size()) {
+            out = c->free_slots[pick];
+            c->free_slots.erase(c->free_slots.begin() + (long)pick);
         }
         if (!out && (c->free_slots.empty() || c->slots.size() < kMaxIdleBlockSlots)) {
             c->slots.emplace_back(new Slot());
@@ -1630,7 +1642,7 @@ int mirt_trace_tiles_async(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
     Slot* sl = nullptr;
-    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    if ((r = slot_acquire(c, sl, tiles, n)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     hipStream_t s = (hipStream_t)stream;  // NULL is the HIP null stream, as in the HIP API
     OutPlanes out{dout->rgb, dout->rgb8, dout->valid, dout->face, dout->object, dout->rgbv};
@@ -1651,7 +1663,8 @@ int mirt_trace_tile(mirt_ctx* c, const mirt_frame* f, uint32_t x, uint32_t y, ui
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
     Slot* sl = nullptr;
-    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    const mirt_tile key{x, y, w, h};
+    if ((r = slot_acquire(c, sl, &key, 1)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     const uint64_t npx = (uint64_t)w * h;
     // device staging for the requested planes: rgb(24) rgb8(3) valid(1) face(4) object(4) rgbv(4)
@@ -2017,7 +2030,7 @@ int trace_tiles_enqueue(mirt_ctx* c, const mirt_frame* f, uint32_t W, uint32_t H
     int r = check_frame(c, f);
     if (r != MIRT_OK) return r;
     Slot* sl = nullptr;
-    if ((r = slot_acquire(c, sl)) != MIRT_OK) return r;
+    if ((r = slot_acquire(c, sl, tiles, n)) != MIRT_OK) return r;
     SlotGuard guard{c, sl};
     uint64_t tris = 0;
     if ((r = enqueue_trace(c, sl, f, W, H, tiles, n, out, s, cancel, pixels, &tris)) != MIRT_OK) {
