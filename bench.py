@@ -411,7 +411,10 @@ def load_profile(path: str, shape: dict):
         pj = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if any(pj.get("shape", {}).get(k) != v for k, v in shape.items()):
+    ps = pj.get("shape", {})
+    # the same shape both ways: a profile of a variant (a key this run lacks, e.g. moving lights)
+    # is never cited for the plain command
+    if any(ps.get(k) != v for k, v in shape.items()) or any(k not in shape for k in ps):
         return None
     return pj
 

@@ -128,7 +128,9 @@ def main():
                   "inflight": line["frames_in_flight"], "batch": line["frames_per_launch"], "steps": line["steps"],
                   "warmup": line["warmup"], "d2h": line["config"].get("d2h", "").startswith("rgb8"),
                   "kernel": kname, "scene": line["config"].get("scene"), "bounces": line["config"].get("bounces", 0),
-                  "options": line["config"].get("options", 0), "camera": line["config"].get("camera", "static")},
+                  "options": line["config"].get("options", 0), "camera": line["config"].get("camera", "static"),
+                  **({"lights": line["config"]["light_motion"]}
+                     if line["config"].get("light_motion", "static") != "static" else {})},
         "frames_per_launch": alg["frames_per_launch"],
         "launches": launches,
         "stats_avg_ns_all_launches": stats_avg.get(kname),
