@@ -98,7 +98,9 @@ def roofline_block(pj, pj_path, kname, ms, dev_ms, achieved, k_tests, frames_per
     # the committed profile of this command is of this build (the profiled region's HIP events
     # bracket launches slowed by the profiling itself, 1.7x in r05j); the HIP-event median of
     # the profiled region otherwise, and always as a cross-check
-    timed_ns = ((pj or {}).get("avg_ns_by_region") or {}).get("timed")
+    # (only where one launch of the profiled kernel is the unit: a reflection frame's figure spans
+    # all its kernels, whose per-kernel launches the profile averages separately)
+    timed_ns = ((pj or {}).get("avg_ns_by_region") or {}).get("timed") if alg_kernel in (None, kname) else None
     hip_median_achieved = achieved
     if timed_ns:
         launch_src = (f"rocprofv3 kernel-trace average of the timed region's launches "

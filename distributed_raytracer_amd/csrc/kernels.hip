@@ -759,9 +759,14 @@ __device__ __forceinline__ uint32_t children_entered(const NodeRegs& nd, const R
 // consecutive faces of the BVH-ordered triangle array in its own LDS slice.  A leaf the window
 // holds is tested from LDS; otherwise the wave first loads the window around the leaf (centred
 // on it, so leaves visited after it on either side in BVH order are likely inside) with vector
-// loads, 16 bytes per lane per load (8 KB in 8 loads), then tests it from LDS.  The records are
-// copied, not recomputed: the same bits are tested either way.
-constexpr uint32_t kStreamTris = 112;
+// loads, 16 bytes per lane per load (1.8 KB in 2 loads), then tests it from LDS.  The records are
+// copied, not recomputed: the same bits are tested either way.  Window size (round 6, configs[3],
+// three runs each, profiles/r06_ab_stream_window.txt): 112 faces (8 KB) 1.112 ms device per frame
+// at an 84% window hit rate, 48 faces 1.094, 32 faces 1.098, 24 faces 1.085, 16 faces 1.095.
+#ifndef MIRT_STREAM_TRIS
+#define MIRT_STREAM_TRIS 24
+#endif
+constexpr uint32_t kStreamTris = MIRT_STREAM_TRIS;  // even
 constexpr size_t kStreamSlice = (size_t)(kStreamTris + 1) * kTriD;  // doubles per wave (an odd base rounds down)
 constexpr size_t kStreamBytes = (kWG / 64) * kStreamSlice * sizeof(double);
 // each wave's window start (~0: none); k_trace resets it before its waves start

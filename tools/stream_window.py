@@ -31,12 +31,14 @@ def main():
     torch.cuda.synchronize()
     c = ctx.debug_counters() / n
     served, reloads = float(c[23]), float(c[31])
+    tris = int(os.environ.get("STREAM_TRIS", "24"))  # the build's MIRT_STREAM_TRIS
     out = {"scene": scene, "width": W, "height": H, "frames": n,
            "primary_leaves_per_frame": float(c[6]), "shadow_leaves_per_frame": float(c[14]),
            "window_leaves_served_per_frame": served, "window_reloads_per_frame": reloads,
            "window_hit_rate": (served - reloads) / served if served else None,
-           "reload_bytes_per_frame": reloads * 113 * 72,
-           "note": "wave-level counts (one per wave per leaf); a reload copies 113 faces x 72 B into the wave's LDS slice"}
+           "window_faces": tris + 1, "reload_bytes_per_frame": reloads * (tris + 1) * 72,
+           "note": f"wave-level counts (one per wave per leaf); a reload copies {tris + 1} faces x 72 B into the "
+                   f"wave's LDS slice"}
     print(json.dumps(out))
     g.close()
 
