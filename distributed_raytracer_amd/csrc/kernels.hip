@@ -2663,9 +2663,19 @@ __device__ __forceinline__ void copy_column(const HostCopyJobs& jobs, uint32_t f
         u1 = a0 < b0 ? max(b, b0) : b;
     }
     if (u0 < u1) {
-        const uint64_t p0 = (uint64_t)x * H + u0, p1 = (uint64_t)x * H + u1;
-        copy_span(jobs.rgb8[f], jobs.hrgb8[f], 3 * p0, 3 * p1, lane);
-        copy_span(jobs.valid[f], jobs.hvalid[f], p0, p1, lane);
+        // the spans widened to whole 16-byte words inside the column: the device plane is current at
+        // every pixel of the frame (misses included), so the extra bytes are this frame's too, and
+        // the head and tail single-byte stores over PCIe go (they remain only at a column's ends)
+        const uint64_t c0 = (uint64_t)x * H, p0 = c0 + u0, p1 = c0 + u1;
+        auto widen = [](uint64_t a, uint64_t b, uint64_t lo, uint64_t hi, uint64_t& wa, uint64_t& wb) {
+            wa = max(lo, a & ~15ull);
+            wb = min(hi, (b + 15) & ~15ull);
+        };
+        uint64_t a, b;
+        widen(3 * p0, 3 * p1, 3 * c0, 3 * (c0 + H), a, b);
+        copy_span(jobs.rgb8[f], jobs.hrgb8[f], a, b, lane);
+        widen(p0, p1, c0, c0 + H, a, b);
+        copy_span(jobs.valid[f], jobs.hvalid[f], a, b, lane);
     }
     if (lane == 0) jobs.spans[f][x] = a < b ? (a | (b << 16)) : 0u;
 }
@@ -3605,7 +3615,13 @@ hipError_t launch_refl_fold(const FrameArgs& fa, const WorkArgs& wa, const OutPl
 hipError_t launch_trace(const FrameRecs& recs, const WorkArgs& wa, const FusedCopy& fc, int grid, uint32_t opts,
                         hipStream_t s) {
     const FrameArgs& fa = recs.r[0].fa;
-    const bool resident = is_resident(fa);
+    // MIRT_FORCE_STREAM=1 (experiment): LDS-sized meshes too take the streamed HBM path, whose
+    // workgroups hold ~23 KB of LDS instead of the whole mesh
+    static const bool force_stream = [] {
+        const char* e = getenv("MIRT_FORCE_STREAM");
+        return e && e[0] == '1';
+    }();
+    const bool resident = is_resident(fa) && !force_stream;
     // an HBM mesh streamed through LDS (the default; MIRT_OPT_NO_LDS_STREAM reads it with scalar
     // loads): one chunk slice per wave
     // a one-object frame of an HBM mesh with segment shadows and the default test (HBM1 > 0: the
