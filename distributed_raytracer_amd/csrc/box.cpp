@@ -109,7 +109,7 @@ struct BoxCall {
 // mirt_box_destroy (diagnostic).
 struct BoxTimers {
     bool on = false;
-    std::atomic<uint64_t> ns[6] = {};  // hit rect, enqueue, transfer + wait, expand, whole call, calls
+    std::atomic<uint64_t> ns[6] = {};  // hit rect, enqueue, host fill + GPU wait, host fill + copy, whole call, calls
 };
 inline uint64_t box_now() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -200,33 +200,46 @@ struct Deal {
 // object -1, i.e. 0xff bytes).
 uint8_t miss_byte(int p) { return (p == 3 || p == 4) ? 0xff : 0; }
 
-// The order's planes in the caller's buffers: the pixels inside I (the order's part of the
-// frame's hit rectangle) from the pinned staging buffer, which holds I's planes column-major
-// over I's height; every other pixel of the order gets its miss value (no GPU work or transfer
-// for them: their rays cannot meet the object).
-void expand_order(const bool want[kPlanes], const mirt_outputs* hout, const uint8_t* stage, uint32_t x, uint32_t y,
-                  uint32_t w, uint32_t h, const uint32_t I[4]) {
-    const uint32_t iw = I[2] - I[0], ih = I[3] - I[1];
-    const uint64_t ipx = (uint64_t)iw * ih;
+// The order's planes in the caller's buffers, in two steps.  fill_misses: every pixel outside I
+// (the order's part of the frame's hit rectangle) gets its miss value — no GPU work or transfer
+// for them, their rays cannot meet the object; it needs no GPU result, so it runs while the GPU
+// traces I.  copy_hits: I's pixels from the pinned staging buffer, which holds I's planes
+// column-major over I's height, once they are there.
+void fill_misses(const bool want[kPlanes], const mirt_outputs* hout, uint32_t x, uint32_t y, uint32_t w, uint32_t h,
+                 const uint32_t I[4]) {
+    const bool empty = I[2] <= I[0] || I[3] <= I[1];
     for (int p = 0; p < kPlanes; ++p) {
         if (!want[p]) continue;
         const size_t e = kElem[p], col = (size_t)h * e;
         uint8_t* dst = (uint8_t*)host_plane(hout, p);
         const uint8_t mb = miss_byte(p);
-        if (ipx == 0) {
+        if (empty) {
             memset(dst, mb, (size_t)w * col);
             continue;
         }
-        const uint8_t* src = stage + plane_offset(want, ipx, p);
         const uint32_t c0 = I[0] - x, c1 = I[2] - x, r0 = I[1] - y, r1 = I[3] - y;
         memset(dst, mb, (size_t)c0 * col);
         for (uint32_t c = c0; c < c1; ++c) {
             uint8_t* d = dst + (size_t)c * col;
             memset(d, mb, (size_t)r0 * e);
-            memcpy(d + (size_t)r0 * e, src + (size_t)(c - c0) * ih * e, (size_t)ih * e);
             memset(d + (size_t)r1 * e, mb, (size_t)(h - r1) * e);
         }
         memset(dst + (size_t)c1 * col, mb, (size_t)(w - c1) * col);
+    }
+}
+void copy_hits(const bool want[kPlanes], const mirt_outputs* hout, const uint8_t* stage, uint32_t x, uint32_t y,
+               uint32_t h, const uint32_t I[4]) {
+    const uint32_t iw = I[2] - I[0], ih = I[3] - I[1];
+    const uint64_t ipx = (uint64_t)iw * ih;
+    if (ipx == 0) return;
+    for (int p = 0; p < kPlanes; ++p) {
+        if (!want[p]) continue;
+        const size_t e = kElem[p], col = (size_t)h * e;
+        uint8_t* dst = (uint8_t*)host_plane(hout, p);
+        const uint8_t* src = stage + plane_offset(want, ipx, p);
+        const uint32_t c0 = I[0] - x, r0 = I[1] - y;
+        for (uint32_t c = 0; c < iw; ++c)
+            memcpy(dst + (size_t)(c0 + c) * col + (size_t)r0 * e, src + (size_t)c * ih * e, (size_t)ih * e);
     }
 }
 
@@ -236,8 +249,10 @@ void expand_order(const bool want[kPlanes], const mirt_outputs* hout, const uint
 // several deal it in `strip`-px column strips (strip s to entry s % active) and the strips are
 // assembled on device 0 (RCCL send/recv or device copies) or copied by every entry straight
 // into the staging buffer (host transport).
+template <class HostWork>
 int box_trace_rect(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t w, uint32_t h, uint32_t W,
-                   uint32_t H, const bool want[kPlanes], const volatile int* cancel, BoxCall* k, uint32_t& active_out) {
+                   uint32_t H, const bool want[kPlanes], const volatile int* cancel, BoxCall* k, uint32_t& active_out,
+                   HostWork&& while_tracing) {
     Deal dl;
     int tr;
     {
@@ -265,6 +280,7 @@ int box_trace_rect(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uin
         BOX_HIP(hipSetDevice(dev0));
         BOX_HIP(hipMemcpyAsync(k->host, k->buf[0], total, hipMemcpyDeviceToHost, k->s[0]));
         const uint64_t te1 = b->tm.on ? box_now() : 0;
+        while_tracing();
         BOX_HIP(hipStreamSynchronize(k->s[0]));
         if (b->tm.on) {
             b->tm.ns[1] += te1 - te0;
@@ -355,6 +371,7 @@ int box_trace_rect(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uin
         }
     }
     const uint64_t te1 = b->tm.on ? box_now() : 0;
+    while_tracing();
     for (uint32_t d = 0; d < dl.active; ++d) {
         BOX_HIP(hipSetDevice(b->dev[d]));
         BOX_HIP(hipStreamSynchronize(k->s[d]));
@@ -380,16 +397,25 @@ int box_trace(mirt_box* b, const mirt_frame* f, uint32_t x, uint32_t y, uint32_t
     uint32_t I[4] = {std::max(x, R[0]), std::max(y, R[1]), std::min(x + w, R[2]), std::min(y + h, R[3])};
     if (I[0] >= I[2] || I[1] >= I[3]) I[0] = I[2] = x, I[1] = I[3] = y;  // no pixel of the order can hit
     uint32_t active = 0;
+    // the misses are written while the GPU traces I (the wait below then overlaps that host work)
+    uint64_t fill_ns = 0;
+    auto fill = [&] {
+        const uint64_t tf = b->tm.on ? box_now() : 0;
+        fill_misses(want, hout, x, y, w, h, I);
+        if (b->tm.on) fill_ns = box_now() - tf;
+    };
     if (I[2] > I[0]) {
-        r = box_trace_rect(b, f, I[0], I[1], I[2] - I[0], I[3] - I[1], W, H, want, cancel, k, active);
+        r = box_trace_rect(b, f, I[0], I[1], I[2] - I[0], I[3] - I[1], W, H, want, cancel, k, active, fill);
         if (r != MIRT_OK) return r;
+    } else {
+        fill();
     }
     if (cancel && *cancel) return set_error(MIRT_E_CANCELLED, "cancelled");
     const uint64_t tx = b->tm.on ? box_now() : 0;
-    expand_order(want, hout, k->host, x, y, w, h, I);
+    copy_hits(want, hout, k->host, x, y, h, I);
     if (b->tm.on) {
         const uint64_t t1 = box_now();
-        b->tm.ns[3] += t1 - tx;
+        b->tm.ns[3] += t1 - tx + fill_ns;
         b->tm.ns[4] += t1 - t0;
         b->tm.ns[5] += 1;
     }
@@ -421,7 +447,7 @@ void mirt_box_destroy(mirt_box* b) {
     if (!b) return;
     if (b->tm.on && b->tm.ns[5]) {
         const double n = (double)b->tm.ns[5];
-        fprintf(stderr, "box_timers_us_per_order hit_rect %.2f enqueue %.2f wait %.2f expand %.2f call %.2f (%llu orders)\n",
+        fprintf(stderr, "box_timers_us_per_order hit_rect %.2f enqueue %.2f fill_and_wait %.2f fill_and_copy %.2f call %.2f (%llu orders)\n",
                 b->tm.ns[0] / n / 1e3, b->tm.ns[1] / n / 1e3, b->tm.ns[2] / n / 1e3, b->tm.ns[3] / n / 1e3,
                 b->tm.ns[4] / n / 1e3, (unsigned long long)b->tm.ns[5]);
     }

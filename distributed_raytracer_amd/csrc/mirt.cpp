@@ -259,7 +259,9 @@ int dev_grow(T*& p, size_t& cap, size_t need) {
 }
 
 // Up to this many slots are created before a caller blocks on a busy one, so a caller
-// enqueueing frames back to back runs ahead of the GPU instead of waiting per frame.
+// enqueueing frames back to back runs ahead of the GPU instead of waiting per frame.  (32 for a
+// box's concurrent orders: slower, each new slot's buffers are allocated inside the run,
+// profiles/r06_box_lines.txt.)
 constexpr size_t kMaxIdleBlockSlots = 8;
 
 // First use of a slot: its event and counters.  The slot's own stream is created only by
