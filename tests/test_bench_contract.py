@@ -7,9 +7,13 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DRIVER = "profiles/r04h_bench_bench.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5 (profile ABI 6)
-LINES = [DRIVER, "profiles/r04f_bench_bench.log", "profiles/r04f_bench_bench500.log", "profiles/r04d_bench_orbit.log", "profiles/r04d_bench_brute.log",
-         "profiles/r04f_bench_config3.log", "profiles/r04f_bench_config4.log", "profiles/r03z_bench_driver_cmd.log"]
+# round 6, final build (adfb06f513c82a80): every line ran after its command's profile was committed
+DRIVER = "profiles/r06f_bench_driver_1.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
+PROFILED = [DRIVER, "profiles/r06f_bench_driver_2.log", "profiles/r06f_bench_driver_3.log",
+            "profiles/r06f_bench_orbit.log", "profiles/r06f_bench_lights.log", "profiles/r06f_bench_config3.log",
+            "profiles/r06f_bench_config3ns.log", "profiles/r06f_bench_config4.log"]
+UNPROFILED = ["profiles/r06f_bench_bench500.log", "profiles/r06f_bench_orbit500.log"]  # 500 frames: no PMC of that shape
+LINES = PROFILED + UNPROFILED
 
 
 def _line(path):
@@ -35,17 +39,23 @@ def test_bench_line_contract(path):
     # value = rays per frame / ms per frame with the D2H
     assert abs(d["value"] - d["rays_per_frame"] / d["ms_per_step"] / 1e3) / d["value"] < 2e-3
     assert abs(d["device_mrays_s"] - d["rays_per_frame"] / d["device_ms_per_frame"] / 1e3) / d["value"] < 2e-3
+    assert d["parity"]["bit_exact"] is True and d["parity"]["pixels_checked"] == d["config"]["width"] * d["config"]["height"]
+    assert d["parity"]["rgb_f64"]["bit_exact"] is True  # the device fp64 colour plane too
     r = d["roofline"]
+    if path in UNPROFILED:  # no PMC of this shape: the algorithmic figure, and it says so
+        assert r["bound"] == "hbm" and r["traffic"] is None and "algorithmic roofline only" in r["note"]
+        return
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "source", "algorithmic"):
         assert k in r, k
     # the physical roof: VALU-busy SIMD cycles per frame (committed PMC of this command's shape)
     assert r["bound"] == "valu" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert abs(r["achieved"] - r["valu_busy_cycles_per_frame"] / (d["ms_per_step"] * 1e-3) / 1e9) / r["achieved"] < 2e-3
-    assert os.path.exists(os.path.join(ROOT, r["source"])) and isinstance(r["traffic"], int)
+    assert os.path.exists(os.path.join(ROOT, r["source"])) and isinstance(r["traffic"], int) and r["traffic"] > 0
+    prof = json.load(open(os.path.join(ROOT, r["source"])))
+    assert prof["build_id"] == d["build_id"]  # the profile of this very build
     a = r["algorithmic"]
     assert a["bound"] == "hbm" and a["unit"] == "GB/s" and a["bytes_per_unit"] == 72
     assert ("LDS-resident" in a["kind"]) == (d["config"]["triangles"] <= 1024)
-    assert d["parity"]["bit_exact"] is True and d["parity"]["pixels_checked"] == d["config"]["width"] * d["config"]["height"]
 
 
 def test_driver_line_cpu_baseline():
@@ -57,7 +67,7 @@ def test_driver_line_cpu_baseline():
 
 # configs[4] runs 17 kernels per frame: under the kernel trace its ms_per_step is ~20% longer than
 # unprofiled, so its line is held to the contract and its shape only
-PROFILED_LINES = [p for p in LINES if "config4" not in p]
+PROFILED_LINES = [p for p in PROFILED if "config4" not in p]
 
 
 @pytest.mark.parametrize("path", PROFILED_LINES)
@@ -91,15 +101,38 @@ def test_profiles_carry_per_region_kernel_summaries():
     assert regions == {k: v for k, v in d["launches"].items() if v}
 
 
-def test_driver_line_launch_time_matches_rocprof():
-    """The algorithmic roofline's launch time is the median HIP-event launch of the profiled
-    region (profile ABI 6); it agrees with the rocprofv3 average launch of the cited profile
-    (same command, a separate run) within 15%, which the mean it replaced did not (r03z: 262.5
-    against 191 us)."""
-    d = _line(DRIVER)
+@pytest.mark.parametrize("path", PROFILED_LINES)
+def test_algorithmic_roofline_uses_the_timed_regions_launches(path):
+    """roofline.algorithmic divides the bytes of one launch by the rocprofv3 average of the TIMED
+    region's launches from the committed profile of the same build (the profiled region's HIP
+    events bracket launches slowed by the profiling itself); the HIP-event median stays as a
+    cross-check."""
+    d = _line(path)
     a = d["roofline"]["algorithmic"]
     prof = json.load(open(os.path.join(ROOT, d["roofline"]["source"])))
-    rocprof_ms = prof["stats_avg_ns_all_launches"] / 1e6
-    assert a["launch_ms_mean"] > 0 and a["launch_ms"] > 0
-    assert abs(a["launch_ms"] - rocprof_ms) / rocprof_ms < 0.15
+    assert abs(a["launch_ms"] - prof["avg_ns_by_region"]["timed"] / 1e6) < 1e-4
+    assert "timed region" in a["kind"] and a["hip_event_median_launch_ms"] > 0
     assert abs(a["achieved"] - a["units_per_launch"] * a["bytes_per_unit"] / (a["launch_ms"] * 1e-3) / 1e9) / a["achieved"] < 2e-3
+
+
+def test_config_lines_carry_traffic_and_stream_window_counts():
+    """configs[3] with and without LDS streaming and configs[4]: each line carries its HBM traffic
+    and physical fraction from its own profile, and the stream window's hit rate is counted
+    (a -DMIRT_DIAG build, tools/stream_window.py)."""
+    t3 = _line("profiles/r06f_bench_config3.log")["roofline"]["traffic"]
+    t3ns = _line("profiles/r06f_bench_config3ns.log")["roofline"]["traffic"]
+    t4 = _line("profiles/r06f_bench_config4.log")["roofline"]["traffic"]
+    assert all(isinstance(t, int) and t > 1e8 for t in (t3, t3ns, t4))
+    sw = _line("profiles/r06f_stream_window.log")
+    assert sw["window_leaves_served_per_frame"] > sw["window_reloads_per_frame"] > 0
+    assert 0.0 < sw["window_hit_rate"] < 1.0 and sw["window_faces"] == 25
+
+
+def test_box_lines():
+    """The box drop-in's lines (bench.py --box): the contract's metric and unit, bit-exact."""
+    for path in ("profiles/r06f_bench_box1.log", "profiles/r06f_bench_box8.log"):
+        d = _line(path)
+        assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+        assert d["unit"] == "Mrays/s" and d["parity"]["bit_exact"] is True
+        assert abs(d["value"] - d["rays_per_frame"] / d["ms_per_step"] / 1e3) / d["value"] < 2e-3
+        assert d["config"]["box_entries"] in (1, 8)
