@@ -504,17 +504,19 @@ struct PhaseClock {
     }
 };
 
-// threadIdx.x made opaque to the compiler: the kernels' end (statistics, summary) recomputes its
-// byte offsets instead of keeping the start's 64-bit copy live through the whole work loop (that
-// copy was k_trace's only spilled VGPR pair)
+// threadIdx.x made opaque to the compiler (FRESH): k_trace's end (statistics, summary) recomputes
+// its byte offsets instead of keeping the start's 64-bit copy live through the whole work loop
+// (that copy was k_trace's only spilled VGPR pair; in k_shadow the same change spilled 3 more)
+template <bool FRESH>
 __device__ __forceinline__ uint32_t tid_fresh() {
     uint32_t t = threadIdx.x;
-    asm volatile("" : "+v"(t));
+    if (FRESH) asm volatile("" : "+v"(t));
     return t;
 }
+template <bool FRESH = false>
 __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], int stat_tests, int stat_nodes,
                                             int stat_leaves, int stat_hits, const WaveStats& w) {
-    const uint32_t tid = tid_fresh();
+    const uint32_t tid = tid_fresh<FRESH>();
     const uint32_t wave = tid >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[wave][0] = w.tests;
@@ -1500,8 +1502,9 @@ __device__ __forceinline__ bool launch_last(const WorkArgs& wa) {
     return last;
 }
 // The frame's statistics totals, by the launch's last workgroup.
+template <bool FRESH = false>
 __device__ __forceinline__ void frame_summary(const FrameArgs& fa, const WorkArgs& wa, bool last) {
-    const uint32_t tid = tid_fresh();
+    const uint32_t tid = tid_fresh<FRESH>();
     if (!last || tid >= kStatN) return;
     const int st = (int)tid;
     cnt_t sum = 0;
@@ -2936,9 +2939,9 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const Fu
     if (mine == 0) clock.mark_staged();
     if (spins >= kSpinLimit) wp.overflow += 1;
     __syncthreads();
-    stats_flush(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, wp);
+    stats_flush<true>(wa.counters, red, kStatPrimTests, kStatPrimNodes, kStatPrimLeaves, kStatHits, wp);
     __syncthreads();
-    stats_flush(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
+    stats_flush<true>(wa.counters, red, kStatShadowTests, kStatShadowNodes, kStatShadowLeaves, -1, wsh);
     if (wa.timeline && !MIRT_ITEM_TRACE) clock.record(wa, 0, taken);
     const bool last = launch_last(wa);
     if (last && wa.bgcnt) {
@@ -2961,7 +2964,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const Fu
                 fr.out.rgbv[fr.xf.words + 1] = fr.xf.words;
             }
         }
-    frame_summary(fa, wa, last);
+    frame_summary<true>(fa, wa, last);
 }
 
 // ---------------------------------------------------------------- reflections (configs[4])
