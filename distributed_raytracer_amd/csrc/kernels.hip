@@ -513,6 +513,10 @@ __device__ __forceinline__ uint32_t tid_fresh() {
     if (FRESH) asm volatile("" : "+v"(t));
     return t;
 }
+// The wave's index in its workgroup, said to be wave-uniform (it is): loop indices and work
+// items derived from it live in SGPRs.  Held as a VGPR, they had been spilled across the work
+// loops: k_shadow's 27 spilled VGPRs and k_bounce's 5 were these indices, shard cursors included.
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 template <bool FRESH = false>
 __device__ __forceinline__ void stats_flush(cnt_t* counters, cnt_t (*red)[4], int stat_tests, int stat_nodes,
                                             int stat_leaves, int stat_hits, const WaveStats& w) {
@@ -775,7 +779,7 @@ constexpr size_t kStreamBytes = (kWG / 64) * kStreamSlice * sizeof(double);
 __shared__ uint32_t g_stream_base[kWG / 64];
 extern __shared__ __attribute__((aligned(16))) double g_lds_mesh[];
 __device__ __forceinline__ const double* stream_leaf(cdptr tri, uint32_t ntri, uint32_t first, uint32_t cnt) {
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = wave_id();
     double* slice = g_lds_mesh + (size_t)wave * kStreamSlice;
     uint32_t base = __builtin_amdgcn_readfirstlane(g_stream_base[wave]);
     diag(23);  // leaves served through the window (MIRT_DIAG builds)
@@ -1531,7 +1535,9 @@ __device__ __forceinline__ void frame_fold(const FrameArgs& fa, const WorkArgs& 
 struct ShardCursor {
     uint32_t gw, nw;  // global wave id, waves in the grid
     __device__ __forceinline__ ShardCursor() {
-        gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        // wave-uniform, said so: every index derived from it (shard, rank, item, chunk) then
+        // lives in SGPRs instead of VGPRs held (and in k_shadow spilled) across the item loop
+        gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (kWG / 64) + (threadIdx.x >> 6));
         nw = gridDim.x * (kWG / 64);
     }
     __device__ __forceinline__ uint32_t first_shard() const { return nw >= (uint32_t)kQShards ? gw % kQShards : gw; }
@@ -1556,7 +1562,7 @@ struct WaveClock {
     __device__ __forceinline__ void mark_staged() { staged = __builtin_amdgcn_s_memrealtime(); }
     __device__ __forceinline__ void record(const WorkArgs& wa, uint32_t kernel, uint32_t items) const {
         const uint64_t real1 = __builtin_amdgcn_s_memrealtime(), clk1 = __builtin_amdgcn_s_memtime();
-        const uint32_t gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        const uint32_t gw = blockIdx.x * (kWG / 64) + wave_id();
         const uint32_t lane = threadIdx.x & 63;
         if (gw >= wa.timeline_cap || lane >= kTimelineRec) return;
         const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
@@ -1588,7 +1594,7 @@ struct ItemClock {
         if (!MIRT_ITEM_TRACE || !wa.timeline) return;
         const uint64_t real1 = __builtin_amdgcn_s_memrealtime(), clk1 = __builtin_amdgcn_s_memtime();
         const uint32_t lane = threadIdx.x & 63;
-        const uint32_t gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        const uint32_t gw = blockIdx.x * (kWG / 64) + wave_id();
         const uint32_t idx = gw * kItemRecs + k;
         ++k;
         if (k > kItemRecs || idx >= 2 * wa.timeline_cap || lane >= kTimelineRec) return;
@@ -2163,7 +2169,9 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, bool pass2,
                                             uint32_t vf = ~0u, const ViewCache* vc = nullptr, uint32_t lim = 64,
                                             uint32_t* ring = nullptr, uint32_t rpos = ~0u, uint32_t defer = ~0u) {
-    const uint32_t lane = threadIdx.x & 63;
+    // (a fresh lane index: its derived per-lane offsets are recomputed per item instead of being
+    // hoisted out of the caller's item loop and held, or spilled, across every item)
+    const uint32_t lane = tid_fresh<true>() & 63;
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
     const uint64_t* w = (const uint64_t*)&wa.hits[slot];
@@ -2229,31 +2237,40 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
     ws.leaves += vis.leaves;
     ws.overflow += vis.overflow;
     // publish this light's bit, then count the light done for the chunk; device-scope
-    // atomics are coherent across XCDs and the wait orders the two atomics
+    // atomics are coherent across XCDs and the wait orders the two atomics (the slot index is
+    // recomputed here: nothing of the item's start stays live across the traversal)
+    const size_t slot_b = chunk + (tid_fresh<true>() & 63);
     if (active && is_lit) {
         const uint32_t old =
-            __hip_atomic_fetch_or(&wa.litw[slot], 1u << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(&wa.litw[slot_b], 1u << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("" ::"v"(old));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t done = 0;
-    if (lane == 0) done = atomicAdd(&wa.blkdone[slot / 64], 1u);
+    if (lane == 0) done = atomicAdd(&wa.blkdone[chunk / 64], 1u);
     done = __builtin_amdgcn_readfirstlane(done);
     if (done != nl - 1) return false;
-    // Phong of the lane's hit (tracer.go:53-76) once its lit word is complete, and its outputs
+    // Phong of the lane's hit (tracer.go:53-76) once its lit word is complete, and its outputs.
+    // The record is read again here (hit point and obj | mat too, through a slot index the
+    // compiler cannot reuse from the item's start): none of it stays live across the traversal,
+    // which in k_shadow had spilled it to scratch.
     auto shade = [&](uint64_t& oidx) {
-        const uint32_t lit = atomicOr(&wa.litw[slot], 0u);
-        const V3 n{bitsd(ld64(w + 3)), bitsd(ld64(w + 4)), bitsd(ld64(w + 5))};
-        oidx = ld64(w + 6);
-        const uint32_t obj = (uint32_t)w7, mat = (uint32_t)(w7 >> 32);
-        return phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, hit, n, lit);
+        const size_t s2 = chunk + (tid_fresh<true>() & 63);
+        const uint64_t* w2 = (const uint64_t*)&wa.hits[s2];
+        const uint32_t lit = atomicOr(&wa.litw[s2], 0u);
+        const V3 h2{bitsd(ld64(w2)), bitsd(ld64(w2 + 1)), bitsd(ld64(w2 + 2))};
+        const V3 n{bitsd(ld64(w2 + 3)), bitsd(ld64(w2 + 4)), bitsd(ld64(w2 + 5))};
+        oidx = ld64(w2 + 6);
+        const uint64_t w7b = ld64(w2 + 7);
+        const uint32_t obj = (uint32_t)w7b, mat = (uint32_t)(w7b >> 32);
+        return phong(fa, fa.obj[obj].m.mats + (size_t)mat * 10, h2, n, lit);
     };
     auto store = [&](uint64_t oidx, const RGB& col) {
         // k_trace (ring != nullptr) of a share in its transfer form: a hit lies inside its
         // frame's hit rectangle, so this is never taken (the split kernels have no such frames)
         if (ring && oidx == kNoOut) return;
         if (wa.bounces) {  // the level's phong: the reflection fold combines the levels and writes the pixel
-            double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot) * wa.ph_stride;
+            double* e = wa.ph_out + (wa.ph_by_origin ? (size_t)oidx : slot_b) * wa.ph_stride;
             e[0] = col.r;
             e[1] = col.g;
             e[2] = col.b;
@@ -2380,7 +2397,7 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
     // LDS ticket: block costs differ by orders of magnitude (culled or not, hit or not), and
     // an LDS atomic balances them without touching the vector memory counter.
     // MIRT_OPT_STATIC_SCHEDULE: wave v of the workgroup takes entries v, v + 8, ... instead.
-    const uint32_t G = gridDim.x, wave = threadIdx.x >> 6;
+    const uint32_t G = gridDim.x, wave = wave_id();
     const uint32_t mine = wa.nblocks > blockIdx.x ? (wa.nblocks - blockIdx.x + G - 1) / G : 0u;
     const bool dyn = (wa.dynamic & kDynPrimary) != 0;
     for (uint32_t c0 = 0; c0 < mine; c0 += kBlkQ) {
@@ -2467,7 +2484,7 @@ void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
     const uint32_t nl = max(fa.n_lights, 1u);
     cnt_t* const qctr = wa.qcounters ? wa.qcounters : wa.counters;
     for (uint32_t q = sc.first_shard(); q < (uint32_t)kQShards; q += sc.shard_step()) {
-        const uint32_t nrec = *lo32(&qctr[cnt_hits(q)]), nch = (nrec + 63) / 64;
+        const uint32_t nrec = __builtin_amdgcn_readfirstlane(*lo32(&qctr[cnt_hits(q)])), nch = (nrec + 63) / 64;
         const uint32_t items = nch * nl, peers = sc.peers();
         cnt_t* qc = &qctr[cnt_queue(1, q)];
         // item rank is this wave's (static); with the queue on, items peers + ticket follow,
@@ -2478,7 +2495,7 @@ void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
             nxt = dyn ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+            if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
                                                               (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, false, ~0u,
                                                               nullptr, min(64u, nrec - c * 64)))
                 // the same item again, every candidate box-gated, at the launch's end (not counted
@@ -2490,9 +2507,9 @@ void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
 #ifndef MIRT_EXP_NO_SPLIT_REDO
     if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
         const uint32_t last = split_redo_last(wa);
-        for (uint32_t e = threadIdx.x >> 6; e < (last & 0x7fffffffu); e += kWG / 64) {
+        for (uint32_t e = wave_id(); e < (last & 0x7fffffffu); e += kWG / 64) {
             const uint32_t ch = split_redo_entry(wa, e, 0), w1 = split_redo_entry(wa, e, 1);
-            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[threadIdx.x >> 6], RESIDENT, segment,
+            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
                                                           (size_t)ch * 64, w1 & 0xffu, ws, true, ~0u, nullptr, w1 >> 8);
         }
         split_redo_reset(wa, last);
@@ -2745,14 +2762,14 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const Fu
         // the host copy of an earlier launch's frames on this stream (a column per wave; that
         // launch has ended: stream order), before this workgroup's tracing: fire and forget
         const FusedCopy* cp = at_use((const FusedCopy*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceFcOffset));
-        const uint32_t nw = gridDim.x * (kWG / 64), gw = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+        const uint32_t nw = gridDim.x * (kWG / 64), gw = blockIdx.x * (kWG / 64) + wave_id();
         for (uint32_t f = 0; f < cp->n; ++f)
             for (uint32_t x = cp->jobs.rect[f][0] + gw; x < cp->jobs.rect[f][2]; x += nw)
                 copy_column(cp->jobs, f, x, cp->H, threadIdx.x & 63);
     }
     if (RESIDENT) stage_tris<false>(lds, fa.obj[0].m.tri, 0, fa.obj[0].m.ntri, V3{0, 0, 0});
     if (HBM1 == 2 && threadIdx.x < kWG / 64) g_stream_base[threadIdx.x] = ~0u;  // no window yet (read after the batch barrier)
-    uint32_t* stk = wstk[threadIdx.x >> 6];
+    uint32_t* stk = wstk[wave_id()];
     WaveStats wp{0, 0, 0, 0, 0}, wsh{0, 0, 0, 0, 0};
     PhaseClock pc;
     const uint32_t nl = max(fa.n_lights, 1u);
@@ -2947,7 +2964,7 @@ MIRT_TRACE_KERNEL void k_trace(const FrameRecs recs, const WorkArgs wa, const Fu
     if (last && wa.bgcnt) {
         // the deferred second passes (redo_mark): every other workgroup is done
         const uint32_t n = __hip_atomic_load(&wa.bgcnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t e = threadIdx.x >> 6; e < n; e += kWG / 64)
+        for (uint32_t e = wave_id(); e < n; e += kWG / 64)
             trace_redo_entry<PREFILTER, BRUTE, RESIDENT, HBM1>(
                 frames, (const WorkArgs*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kTraceWaOffset), e);
         __syncthreads();
@@ -3240,7 +3257,7 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
     }
     if (wa.split_redo) {  // the deferred second passes, in the launch's last workgroup
         const uint32_t last = split_redo_last(wa);
-        for (uint32_t e = threadIdx.x >> 6; e < (last & 0x7fffffffu); e += kWG / 64) {
+        for (uint32_t e = wave_id(); e < (last & 0x7fffffffu); e += kWG / 64) {
             const uint32_t q = split_redo_entry(wa, e, 0), k = split_redo_entry(wa, e, 1);
             const uint32_t n = *lo32((cnt_t*)&ba.in_cnt[cnt_hits(q)]);
             bounce_chunk<PREFILTER, BRUTE, RESIDENT>(fa, wa, ba, lds, q, k, n, cp, true, ws, rays, shadow_rays);
@@ -3355,7 +3372,7 @@ hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStre
 __global__ __launch_bounds__(256) void k_refl_fold(const FrameArgs fa, const WorkArgs wa, OutPlanes out,
                                                    const uint32_t* __restrict__ chain) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    const uint32_t gw = blockIdx.x * 4 + wave_id(), nw = gridDim.x * 4;
     // one walk over every region's chunks (a loop per region left most waves idle per region)
     __shared__ uint32_t s_first[kQShards + 1];
     if (threadIdx.x == 0) {
@@ -3820,7 +3837,7 @@ hipError_t launch_unpack_rect(const TileDesc* tiles, uint32_t ntiles, uint64_t m
 __global__ __launch_bounds__(256) void k_copy_rect_host(HostCopyJobs jobs, uint32_t H) {
     const uint32_t f = blockIdx.z, lane = threadIdx.x & 63;
     const uint32_t* R = jobs.rect[f];
-    for (uint32_t x = R[0] + blockIdx.x * 4 + (threadIdx.x >> 6); x < R[2]; x += gridDim.x * 4) copy_column(jobs, f, x, H, lane);
+    for (uint32_t x = R[0] + blockIdx.x * 4 + wave_id(); x < R[2]; x += gridDim.x * 4) copy_column(jobs, f, x, H, lane);
 }
 hipError_t launch_copy_rect_host(const HostCopyJobs& jobs, uint32_t nframes, uint32_t H, uint32_t max_cols,
                                  hipStream_t s) {
