@@ -1625,6 +1625,13 @@ __device__ __forceinline__ uint32_t shard_items(uint32_t n, uint32_t q) {
 // ---------------------------------------------------------------- hit slots
 // A HitRec is eight 64-bit words: h[3], n[3], out, obj | mat << 32.
 __device__ __forceinline__ void st64(uint64_t* p, uint64_t v) { *p = v; }
+// A constant made at its store (as store_black's zero): k_primary had hoisted the miss slot's
+// kNoHit word and the -1 of the face and object planes out of its loops and spilled them.
+template <typename T>
+__device__ __forceinline__ T at_store(T v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 // A miss's fp64 colour (three zeros), its zero made at the store: a zero hoisted out of the
 // block loops would stay live across the traversal, and k_trace spilled it to scratch.
 __device__ __forceinline__ void store_black(double* p) {
@@ -1747,6 +1754,19 @@ __device__ __forceinline__ uint32_t ring_take(uint32_t* ring, uint32_t c) {
 // The output word of a block's pixel (lx, ly): its packed index bd.out + lx * th + ly, or, for
 // a share written in its transfer form (k_trace's FrameRec::xf, full-height strips: th = H),
 // the word k_pack_rect would have copied it to; kNoOut for a pixel outside the hit rectangle.
+// The primary ray's direction at pixel (i, j): tracer.go:15-22 pixelToPoint, then tracer.go:86
+// (p - Cam.Pos).Norm(), in the reference's fp64 operations.  A is FrameArgs (k_primary, k_trace)
+// or RayGen (k_pack at level 0, which makes the direction again instead of reading it): one
+// function, so both get the same bits.
+template <class A>
+__device__ __forceinline__ V3 primary_dir(const A& a, uint32_t i, uint32_t j) {
+    const V3 cam{a.cam[0], a.cam[1], a.cam[2]};
+    const double si = a.phw * ((double)(a.halfW - (int32_t)i) - 0.5) / (double)a.halfW;
+    const double sj = a.phh * ((double)(a.halfH - (int32_t)j) - 0.5) / (double)a.halfH;
+    const V3 p = add(add(add(cam, V3{a.fwd[0], a.fwd[1], a.fwd[2]}), scale(V3{a.left[0], a.left[1], a.left[2]}, si)),
+                     scale(V3{a.up[0], a.up[1], a.up[2]}, sj));
+    return norm(sub(p, cam));
+}
 __device__ __forceinline__ uint64_t out_index(const XferArgs* xf, const BlockDesc& bd, uint32_t lx, uint32_t ly,
                                               uint32_t th) {
     if (!xf || !xf->on) return (uint64_t)bd.out + (uint64_t)lx * th + ly;
@@ -1798,11 +1818,7 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
     // tracer.go:15-22 pixelToPoint with the reference's fp64 operations (computed, not
     // loaded: a vector load here would wait for the previous block's stores, which share
     // its in-order memory counter), then tracer.go:86 (p - Cam.Pos).Norm()
-    const double si = fa.phw * ((double)(fa.halfW - (int32_t)i) - 0.5) / (double)fa.halfW;
-    const double sj = fa.phh * ((double)(fa.halfH - (int32_t)j) - 0.5) / (double)fa.halfH;
-    V3 p = add(add(add(cam, V3{fa.fwd[0], fa.fwd[1], fa.fwd[2]}), scale(V3{fa.left[0], fa.left[1], fa.left[2]}, si)),
-               scale(V3{fa.up[0], fa.up[1], fa.up[2]}, sj));
-    V3 d = norm(sub(p, cam));
+    V3 d = primary_dir(fa, i, j);
 
     Visits vis{0, 0, 0, 0};
     // view table walk: the lane's direction (s_i, t_j) and the block's range (block_frustum's)
@@ -1858,6 +1874,9 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
             atomicAdd(&wa.bgcnt[blk / kPackGroup], (uint32_t)__popcll(mask));
         }
         uint64_t* w = (uint64_t*)&wa.hits[slot];
+        // the chunk's hit ballot (split kernels): its missed lanes write nothing below
+        const bool ballot = !lc && wa.hmask;
+        if (ballot && lane == 0) st64(&wa.hmask[slot / 64], mask);
         if (is_hit) {
             st64(w + 0, dbits(nh.hit.x));
             st64(w + 1, dbits(nh.hit.y));
@@ -1869,11 +1888,11 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
             st64(w + 7, (uint64_t)nh.obj | ((uint64_t)nh.mat << 32));
             // the reflect kernel's incoming D (reflection frames run the split kernels: k_trace,
             // the caller with local chunks, never sees one, launch_frames)
-            if (!lc && wa.bounces) vstore(wa.dir0 + 3 * slot, d);
-        } else {
-            st64(w + 7, (uint64_t)kNoHit);
+            if (!lc && wa.bounces && wa.dir0) vstore(wa.dir0 + 3 * slot, d);  // (chains: k_reflect reads it)
+        } else if (!ballot) {
+            st64(w + 7, at_store((uint64_t)kNoHit));
         }
-        st32(&wa.litw[slot], 0u);
+        if (is_hit || !ballot) st32(&wa.litw[slot], 0u);
         if (lane == 0) st32(&wa.blkdone[slot / 64], 0u);
         if (lc) {
             // publish to the workgroup: the chunk's stores have reached L2 (shared by every
@@ -1888,8 +1907,8 @@ __device__ __forceinline__ bool primary_block(const FrameArgs& fa, const WorkArg
     }
     if (active && oidx != kNoOut) {
         if (out.valid) out.valid[oidx] = is_hit ? 1 : 0;
-        if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : -1;
-        if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : -1;
+        if (out.face) out.face[oidx] = is_hit ? (int32_t)nh.face : at_store(-1);
+        if (out.object) out.object[oidx] = is_hit ? (int32_t)nh.obj : at_store(-1);
         if (!is_hit) {
             if (out.rgb) store_black(out.rgb + 3 * oidx);
             if (out.rgb8) {
@@ -2163,7 +2182,7 @@ __device__ __forceinline__ void redo_mark(const WorkArgs& wa, uint32_t key) {
 //   vf: the chunk's frame within the launch (its view tables, k_trace), ~0u: none.
 //   pass2 / returns: shadow_lit_single's retry.  true = the item must run again with pass2
 //   (nothing was published: no lit bit, no count, no shading); false = done.
-template <bool PREFILTER, bool BRUTE, bool LT3 = true, int HBM1 = 0>
+template <bool PREFILTER, bool BRUTE, bool LT3 = true, int HBM1 = 0, bool SPLIT = false>
 __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs& wa, const OutPlanes& out,
                                             const double* __restrict__ lds, uint32_t* __restrict__ stk, bool resident,
                                             bool segment, size_t chunk, uint32_t l, WaveStats& ws, bool pass2,
@@ -2175,9 +2194,15 @@ __device__ __forceinline__ bool shadow_item(const FrameArgs& fa, const WorkArgs&
     const uint32_t nl = max(fa.n_lights, 1u);
     const size_t slot = chunk + lane;
     const uint64_t* w = (const uint64_t*)&wa.hits[slot];
-    const uint64_t w7 = ld64(w + 7);
-    // lim: the chunk's records (a bounce level's last chunk of a region is partial)
-    const bool active = lane < lim && (uint32_t)w7 != kNoHit;
+    // lim: the chunk's records (a bounce level's last chunk of a region is partial); a chunk
+    // with a hit ballot (WorkArgs::hmask) has no record at its missed lanes
+    bool active;
+    if (SPLIT && wa.hmask) {  // (k_shadow only: k_trace's chunks carry no ballot)
+        const uint64_t hm = u64_uniform(wa.hmask[chunk / 64]);
+        active = lane < lim && ((hm >> lane) & 1u);
+    } else {
+        active = lane < lim && (uint32_t)ld64(w + 7) != kNoHit;
+    }
     V3 o{0, 0, 0}, d{1, 0, 0}, hit{0, 0, 0};
     const V3 lpos{fa.lpos[l][0], fa.lpos[l][1], fa.lpos[l][2]};
     if (active) {
@@ -2418,10 +2443,14 @@ MIRT_TRACE_KERNEL void k_primary(const FrameArgs fa, const WorkArgs wa, OutPlane
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][1]),
                                (uint32_t)__builtin_amdgcn_readfirstlane(bq[t][2]), 0u};
             const uint32_t b = blockIdx.x + (c0 + t) * G;
-            ++taken;
-            if (primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws, pc,
-                                                          false, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b))
-                split_redo_push(wa, b, 0u);  // the same block again, every candidate box-gated, at the launch's end
+            // WorkArgs::live: a block with no pixel in the frame's live rectangle is skipped
+            const uint32_t px = bd.pxy & 0xffffu, py = bd.pxy >> 16, vw = (bd.geo >> 16) & 0xffu, vh = bd.geo >> 24;
+            if (px < wa.live[2] && px + vw > wa.live[0] && py < wa.live[3] && py + vh > wa.live[1]) {
+                ++taken;
+                if (primary_block<RESIDENT, PREFILTER, BRUTE>(fa, wa, out, lds, wstk[wave], RESIDENT, bd, b % kQShards, ws,
+                                                              pc, false, use_frustum, frect, nullptr, 0, nullptr, 0, nullptr, b))
+                    split_redo_push(wa, b, 0u);  // the same block again, every candidate box-gated, at the launch's end
+            }
             pc.lap(3);
             if (dyn) {
                 uint32_t nt = 0;
@@ -2495,7 +2524,7 @@ void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
             nxt = dyn ? ticket_issue(qc) : 0;
             ++taken;
             const uint32_t l = k / nch, c = k - l * nch;
-            if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
+            if (shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3, 0, true>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
                                                               (size_t)q * wa.hit_cap + (size_t)c * 64, l, ws, false, ~0u,
                                                               nullptr, min(64u, nrec - c * 64)))
                 // the same item again, every candidate box-gated, at the launch's end (not counted
@@ -2509,7 +2538,7 @@ void k_shadow(const FrameArgs fa, const WorkArgs wa, OutPlanes out) {
         const uint32_t last = split_redo_last(wa);
         for (uint32_t e = wave_id(); e < (last & 0x7fffffffu); e += kWG / 64) {
             const uint32_t ch = split_redo_entry(wa, e, 0), w1 = split_redo_entry(wa, e, 1);
-            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
+            shadow_item<PREFILTER, BRUTE, MIRT_SHADOW_LT3, 0, true>(fa, wa, out, lds, wstk[wave_id()], RESIDENT, segment,
                                                           (size_t)ch * 64, w1 & 0xffu, ws, true, ~0u, nullptr, w1 >> 8);
         }
         split_redo_reset(wa, last);
@@ -3278,22 +3307,28 @@ MIRT_TRACE_KERNEL void k_bounce(const FrameArgs fa, const WorkArgs wa, const Bou
 constexpr int kPackWG = 256;
 static_assert(kPackGroup == 64, "k_pack: one source chunk per lane of wave 0");
 __device__ __forceinline__ void pack_chunk(const WorkArgs& wa, const PackArgs& pa, uint32_t e, uint32_t off, uint32_t per,
-                                           uint32_t lane) {
+                                           uint32_t lane, uint32_t blk) {
     if ((e & 127u) == 0) return;
     const size_t cs = (size_t)((e >> 7) - 1) * 64;
     const size_t from = cs + lane;
     const uint64_t* w = (const uint64_t*)&pa.in[from];
+    // primary chunks with a hit ballot: nothing is read at a missed lane
+    const uint64_t m = pa.in_hmask ? u64_uniform(pa.in_hmask[cs / 64]) : __ballot((uint32_t)ld64(w + 7) != kNoHit);
+    if (!((m >> lane) & 1u)) return;
     const uint64_t w7 = ld64(w + 7);
-    const bool valid = (uint32_t)w7 != kNoHit;
-    const uint64_t m = __ballot(valid);
-    if (!valid) return;
     const uint32_t p = off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     const uint32_t r = p / per, idx = p - r * per;
     const size_t dst = (size_t)r * wa.hit_cap + idx;
     uint64_t v[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) v[q] = ld64(w + q);
-    const V3 dir = vload(pa.in_dir + 3 * from);
+    V3 dir;
+    if (pa.in_dir) {
+        dir = vload(pa.in_dir + 3 * from);
+    } else {  // level 0: the primary ray again, from the block's pixel (lane = 8 lx + ly, primary_block)
+        const uint32_t pxy = ((const uint32_t*)wa.blocks)[4 * ((size_t)(blk % kQShards) * wa.per_shard + blk / kQShards) + 1];
+        dir = primary_dir(pa.rg, (pxy & 0xffffu) + (lane >> 3), (pxy >> 16) + (lane & 7));
+    }
     uint64_t* d = (uint64_t*)&pa.out[dst];
 #pragma unroll
     for (int q = 0; q < 6; ++q) st64(d + q, v[q]);
@@ -3358,7 +3393,7 @@ __global__ __launch_bounds__(kPackWG) void k_pack(const WorkArgs wa, const PackA
         const uint32_t a = tid * per;
         pa.out_cnt[cnt_hits(tid)] = (cnt_t)(tot > a ? min(per, tot - a) : 0u) | ((cnt_t)(per / 64) << 32);
     }
-    for (uint32_t t = wave; t < j1 - j0; t += kPackWG / 64) pack_chunk(wa, pa, s_src[t], pre + s_off[t], per, lane);
+    for (uint32_t t = wave; t < j1 - j0; t += kPackWG / 64) pack_chunk(wa, pa, s_src[t], pre + s_off[t], per, lane, j0 + t);
 }
 bool bounce_shades() { return MIRT_BOUNCE_SHADE != 0; }
 hipError_t launch_pack(const WorkArgs& wa, const PackArgs& pa, int grid, hipStream_t s) {
@@ -3389,8 +3424,9 @@ __global__ __launch_bounds__(256) void k_refl_fold(const FrameArgs fa, const Wor
         const uint32_t k = g - s_first[q];
         {
             const size_t slot = (size_t)q * wa.hit_cap + (size_t)k * 64 + lane;
+            if (wa.hmask && !((u64_uniform(wa.hmask[slot / 64]) >> lane) & 1u)) continue;
             const HitRec& rec = wa.hits[slot];
-            if (rec.obj == kNoHit) continue;
+            if (!wa.hmask && rec.obj == kNoHit) continue;
             const uint32_t st = chain[slot], L = (st & 0xffu) - 1;
             auto level = [&](uint32_t l, RGB& ph, RGB& ks) {
                 uint32_t obj = rec.obj, mat = rec.mat;

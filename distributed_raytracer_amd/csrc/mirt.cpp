@@ -97,6 +97,8 @@ struct Slot {
     size_t litw_cap = 0;
     uint32_t* blkdone = nullptr;
     size_t blkdone_cap = 0;
+    uint64_t* hmask = nullptr;  // split kernels: per primary hit chunk, its hit ballot (WorkArgs::hmask)
+    size_t hmask_cap = 0;
     double* dir0 = nullptr;   // configs[4] reflections: primary direction per hit slot
     size_t dir0_cap = 0;
     double* ph0 = nullptr;    // configs[4] reflections: phong of the primary hit per slot
@@ -284,7 +286,7 @@ void slot_free(Slot* s) {
                     (void*)s->llitw[1], (void*)s->lblk[0], (void*)s->lblk[1], (void*)s->lcnt, (void*)s->chain,
                     (void*)s->shits, (void*)s->sdir, (void*)s->ssrc, (void*)s->bmap, (void*)s->gcnt, (void*)s->redo, (void*)s->sredo})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
+    for (void* p : {(void*)s->hits, (void*)s->litw, (void*)s->blkdone, (void*)s->hmask, (void*)s->dir0, (void*)s->ph0, (void*)s->refl,
                     (void*)s->cost, (void*)s->counters, (void*)s->d_tiles, (void*)s->d_blocks, (void*)s->summary, s->out_buf,
                     (void*)s->views, (void*)s->view_heads})
         if (p) (void)hipFree(p);
@@ -1077,10 +1079,13 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     if ((r = dev_grow(sl->blkdone, sl->blkdone_cap, hit_slots / 64)) != MIRT_OK) return r;
     wa.bounces = bounces;
     if (wa.bounces) {
-        if ((r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
+        // the primary rays' directions: chains only (k_reflect); the bounce waves' k_pack makes
+        // them again from the pixels
+        const bool chains = (c->flags & MIRT_OPT_REFLECT_CHAINS) != 0;
+        if (chains && (r = dev_grow(sl->dir0, sl->dir0_cap, 3 * hit_slots)) != MIRT_OK) return r;
         if ((r = dev_grow(sl->ph0, sl->ph0_cap, 3 * hit_slots)) != MIRT_OK) return r;
         if ((r = dev_grow(sl->refl, sl->refl_cap, (size_t)kReflD * bounces * hit_slots)) != MIRT_OK) return r;
-        wa.dir0 = sl->dir0;
+        wa.dir0 = chains ? sl->dir0 : nullptr;
         wa.ph0 = sl->ph0;
         wa.refl = sl->refl;
         wa.refl_stride = hit_slots;
@@ -1130,6 +1135,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
     wa.counters_next = sl->counters + (size_t)(sl->parity ^ 1u) * kCntN;
     wa.summary = sl->summary;
     wa.fr = sl->h_frames[0].fr;
+    memcpy(wa.live, sl->h_frames[0].live, sizeof(wa.live));  // (k_primary: one frame per launch)
     wa.dynamic = (c->flags & MIRT_OPT_STATIC_SCHEDULE)
                      ? 0u
                      : (uint32_t)(kDynPrimary | kDynShadow | kDynReflect);
@@ -1213,6 +1219,11 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             if (sl->sredo_cap != cap0) HIP_TRY(hipMemsetAsync(sl->sredo, 0, sl->sredo_cap * sizeof(uint32_t), s));
             wa.split_redo = sl->sredo;
         }
+        // the primary chunks' hit ballots (not with chains: k_reflect reads the records' obj)
+        if (!(wa.bounces && (c->flags & MIRT_OPT_REFLECT_CHAINS)) && !getenv("MIRT_NO_HIT_BALLOT")) {
+            if ((r = dev_grow(sl->hmask, sl->hmask_cap, hit_slots / 64)) != MIRT_OK) return r;
+            wa.hmask = sl->hmask;
+        }
         if (prof) HIP_TRY(hipEventRecord(pr.ev[0], s));
         HIP_TRY(launch_primary(fa, wa, out, pgrid, c->flags, s));
         if (prof) HIP_TRY(hipEventRecord(pr.ev[1], s));
@@ -1233,7 +1244,17 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             const size_t ng = (std::max<size_t>(sl->nblocks, hit_slots / 64) + kPackGroup - 1) / kPackGroup;
             PackArgs p0{};
             p0.in = sl->hits;
-            p0.in_dir = sl->dir0;
+            p0.in_dir = nullptr;  // made from each hit's pixel (PackArgs::rg)
+            for (int k = 0; k < 3; ++k) {
+                p0.rg.cam[k] = fa.cam[k];
+                p0.rg.fwd[k] = fa.fwd[k];
+                p0.rg.left[k] = fa.left[k];
+                p0.rg.up[k] = fa.up[k];
+            }
+            p0.rg.phw = fa.phw;
+            p0.rg.phh = fa.phh;
+            p0.rg.halfW = fa.halfW;
+            p0.rg.halfH = fa.halfH;
             p0.src = sl->bmap;
             p0.gcnt = sl->gcnt;
             p0.nsrc = sl->nblocks;
@@ -1243,6 +1264,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
             p0.out_litw = sl->llitw[0];
             p0.out_blkdone = sl->lblk[0];
             p0.out_cnt = sl->lcnt;
+            p0.in_hmask = wa.hmask;
             HIP_TRY(launch_pack(wa, p0, (int)((sl->nblocks + kPackGroup - 1) / kPackGroup), s));
             for (uint32_t lv = 1; lv <= wa.bounces; ++lv) {
                 if (cancel && *cancel) return fail(MIRT_E_CANCELLED, "cancelled");
@@ -1277,6 +1299,7 @@ int launch_frames(mirt_ctx* c, Slot* sl, uint32_t nf, uint32_t W, uint32_t H, co
                 wl.litw = sl->llitw[ob];
                 wl.blkdone = sl->lblk[ob];
                 wl.qcounters = pk.out_cnt;
+                wl.hmask = nullptr;  // packed records: every one up to the region's count is a hit
                 wl.ph_out = sl->refl + (size_t)(lv - 1) * hit_slots * kReflD;
                 wl.ph_stride = kReflD;
                 wl.ph_by_origin = 1;
@@ -3192,8 +3215,7 @@ static int group_flush(mirt_group* g) {
         const uint64_t npx = (uint64_t)g->W * g->H;
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t* R = br.rect[i];
-            narrow[i] = !(R[0] == 0 && R[1] == 0 && R[2] == g->W && R[3] == g->H) && !g->bbounces &&
-                        !(c->flags & MIRT_OPT_SPLIT_KERNELS);
+            narrow[i] = !(R[0] == 0 && R[1] == 0 && R[2] == g->W && R[3] == g->H);
             const uint32_t j = g->bj[i];
             if (g->tiled) continue;
             if (!narrow[i]) {  // traced whole: every pixel is written

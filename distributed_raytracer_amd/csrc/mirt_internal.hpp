@@ -367,6 +367,14 @@ struct WorkArgs {
     // hits per group of kPackGroup blocks (k_pack's prefix sums)
     uint32_t* bmap;
     uint32_t* bgcnt;
+    // split kernels' primary hit chunks (k_primary without a ring; nullptr: none): per 64-slot
+    // chunk, the ballot of its lanes that hit.  A missed lane's record, lit word and direction
+    // are then never written (its lines stay clean): the chunk's readers (k_shadow at level 0,
+    // k_pack at level 0, k_refl_fold) take validity from the mask instead of the record's obj.
+    uint64_t* hmask;
+    // k_primary: FrameRec::live of its frame (a block with no pixel inside is not traced: the
+    // caller's planes already hold its miss values, as for k_trace)
+    uint32_t live[4];
 };
 constexpr uint32_t kPackGroup = 64;  // source chunks per k_pack workgroup (and per counted group)
 // Reflections in waves of bounces (configs[4] extension, kernels.hip k_bounce): level lv's
@@ -387,9 +395,16 @@ struct BounceArgs {
 };
 // k_pack: a bounce level's records compacted in source-chunk order (the screen's block
 // order), split evenly over the kQShards regions (region r: positions [r per, (r + 1) per)).
+// The camera's part of FrameArgs (tracer.go:15-22 pixelToPoint): k_pack at level 0 makes each
+// primary hit's ray direction again from its pixel, with k_primary's own operations.
+struct RayGen {
+    double cam[3], fwd[3], left[3], up[3];
+    double phw, phh;
+    int32_t halfW, halfH;
+};
 struct PackArgs {
     const HitRec* in;       // the source slots (level 0: the primary hit slots)
-    const double* in_dir;
+    const double* in_dir;   // the rays that reached them (level 0, nullptr: made from the pixel, rg)
     const uint32_t* src;    // source chunks in order: (slot / 64 + 1) << 7 | records (0: none)
     const uint32_t* gcnt;   // records per group of kPackGroup source chunks
     const cnt_t* in_cnt;    // level >= 1: the region counts of the chunks' level (their number); else null
@@ -400,6 +415,8 @@ struct PackArgs {
     uint32_t* out_litw;
     uint32_t* out_blkdone;
     cnt_t* out_cnt;         // region counts of the packed level (cnt_hits)
+    const uint64_t* in_hmask;  // level 0 with WorkArgs::hmask: the source chunks' hit ballots
+    RayGen rg;              // level 0 without in_dir: the frame's camera
 };
 constexpr int kTimelineRec = 8;
 constexpr int kReflD = 4;  // doubles per slot and level of WorkArgs::refl
