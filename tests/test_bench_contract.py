@@ -7,12 +7,12 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# round 6, final build (adfb06f513c82a80): every line ran after its command's profile was committed
-DRIVER = "profiles/r06f_bench_driver_1.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
-PROFILED = [DRIVER, "profiles/r06f_bench_driver_2.log", "profiles/r06f_bench_driver_3.log",
-            "profiles/r06f_bench_orbit.log", "profiles/r06f_bench_lights.log", "profiles/r06f_bench_config3.log",
-            "profiles/r06f_bench_config3ns.log", "profiles/r06f_bench_config4.log"]
-UNPROFILED = ["profiles/r06f_bench_bench500.log", "profiles/r06f_bench_orbit500.log"]  # 500 frames: no PMC of that shape
+# round 6, final build (profiles/r06h_*): every line ran after its command's profile was committed
+TAG = "r06h"
+DRIVER = f"profiles/{TAG}_bench_driver_1.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
+PROFILED = [DRIVER] + [f"profiles/{TAG}_bench_{k}.log" for k in ("driver_2", "driver_3", "orbit", "lights", "config3",
+                                                                  "config3ns", "config4")]
+UNPROFILED = [f"profiles/{TAG}_bench_{k}.log" for k in ("bench500", "orbit500")]  # 500 frames: no PMC of that shape
 LINES = PROFILED + UNPROFILED
 
 
@@ -119,18 +119,18 @@ def test_config_lines_carry_traffic_and_stream_window_counts():
     """configs[3] with and without LDS streaming and configs[4]: each line carries its HBM traffic
     and physical fraction from its own profile, and the stream window's hit rate is counted
     (a -DMIRT_DIAG build, tools/stream_window.py)."""
-    t3 = _line("profiles/r06f_bench_config3.log")["roofline"]["traffic"]
-    t3ns = _line("profiles/r06f_bench_config3ns.log")["roofline"]["traffic"]
-    t4 = _line("profiles/r06f_bench_config4.log")["roofline"]["traffic"]
+    t3 = _line(f"profiles/{TAG}_bench_config3.log")["roofline"]["traffic"]
+    t3ns = _line(f"profiles/{TAG}_bench_config3ns.log")["roofline"]["traffic"]
+    t4 = _line(f"profiles/{TAG}_bench_config4.log")["roofline"]["traffic"]
     assert all(isinstance(t, int) and t > 1e8 for t in (t3, t3ns, t4))
-    sw = _line("profiles/r06f_stream_window.log")
+    sw = _line(f"profiles/{TAG}_stream_window.log")
     assert sw["window_leaves_served_per_frame"] > sw["window_reloads_per_frame"] > 0
     assert 0.0 < sw["window_hit_rate"] < 1.0 and sw["window_faces"] == 25
 
 
 def test_box_lines():
     """The box drop-in's lines (bench.py --box): the contract's metric and unit, bit-exact."""
-    for path in ("profiles/r06f_bench_box1.log", "profiles/r06f_bench_box8.log"):
+    for path in (f"profiles/{TAG}_bench_box1.log", f"profiles/{TAG}_bench_box8.log"):
         d = _line(path)
         assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
         assert d["unit"] == "Mrays/s" and d["parity"]["bit_exact"] is True

@@ -1,5 +1,5 @@
 """LDS triangle streaming (configs[3]) window statistics per frame, from a -DMIRT_DIAG=1 build
-(MIRT_LIB): leaves served through the per-wave LDS windows and window reloads (8 KB each),
+(MIRT_LIB; built by `make -C distributed_raytracer_amd/csrc OUT=../libmirt_diag.so OBJ=obj_diag EXTRA=-DMIRT_DIAG=1`): leaves served through the per-wave LDS windows and window reloads (8 KB each),
 hence the window's hit rate.
   MIRT_LIB=distributed_raytracer_amd/libmirt_diag.so python tools/stream_window.py /tmp/sphere1m/scene.json"""
 import json
