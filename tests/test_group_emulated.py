@@ -116,6 +116,43 @@ def test_emulated_world_reflections(ctx, env, world, tile, chains):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [1, 2])
+def test_reflection_frames_narrowed_to_the_hit_rectangle(ctx, env, inflight):
+    """Reflection frames through a whole-screen frame group are narrowed to their hit rectangle
+    (k_primary skips the blocks outside FrameRec::live; the group refills the columns an earlier
+    frame of the slot hit).  Cameras whose rectangles differ — the default view, a turned-away
+    camera (empty), an edge cut, one inside the box — follow each other on the same slots: every
+    frame equals the single-call draw() of its camera (itself checked against the oracle in
+    test_config4.py) on every pixel."""
+    import dataclasses
+    import torch
+    import distributed_raytracer_amd as rt
+    from distributed_raytracer_amd.framebuffer import NativeFrameGroup
+    W2, H2 = 640, 360
+    base = env.mutable()
+    cams = _cameras(base)
+    order = ["default", "away", "edge", "inside", "default", "edge", "away", "default"]
+    refs = {}
+    for name in set(order):
+        pos, d, fov = cams[name]
+        mut = dataclasses.replace(rt.EnvMutables(base.objects, base.lights, rt.Camera.new(pos, d, fov)), max_bounces=3)
+        refs[name] = (mut, rt.draw(env, W2, H2, mut))
+    assert refs["away"][1].valid.sum() == 0 and refs["default"][1].valid.sum() > 1000
+    g = NativeFrameGroup(ctx, W2, H2, 0, 1, None, inflight=inflight)
+    try:
+        for k, name in enumerate(order):
+            g.render(refs[name][0].to_frame())
+            g.wait()
+            torch.cuda.synchronize()
+            got, ref = g.frames[k % inflight], refs[name][1]
+            assert np.array_equal(got.valid.cpu().numpy(), ref.valid), f"frame {k} ({name}): valid differs"
+            assert np.array_equal(got.rgb8.cpu().numpy(), ref.rgb8), f"frame {k} ({name}): rgb8 differs"
+    finally:
+        g.close()
+        ctx.set_grid()
+
+
+@pytest.mark.gpu
 def test_adaptive_grid_lone_and_burst_frames(ctx, views, monkeypatch):
     """MIRT_ADAPTIVE_GRID=2: a frame issued while none runs gets the whole chip's grid, a
     frame of a burst the fixed one; one slot sees both launch shapes in turn (its hit

@@ -142,9 +142,12 @@ def main():
                                                        "device_mrays_s")},
         "trace_pass_roofline": line["roofline"],
     }
-    # PMC passes: per-launch counters of every frame kernel, over the timed and profiled regions
+    # PMC passes: per-launch counters of every frame kernel over the TIMED region (the launches
+    # ms_per_step measures; the profiled region's HIP events and the lone frames of the latency
+    # region run heavier launches), plus every region's HBM bytes per launch for reference
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))  # (kernel) -> counter -> values
-    nl = {}  # kernel -> launches of the timed and profiled regions
+    nl = {}  # kernel -> launches of the timed region
+    hbm_reg = collections.defaultdict(lambda: collections.defaultdict(float))  # region -> counter -> KiB (all frame kernels)
     for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_valu", "pmc_active"):
         f = os.path.join(src, p, "run_counter_collection.csv")
         if not os.path.exists(f):
@@ -158,9 +161,12 @@ def main():
         for k, pk in per.items():
             ids = sorted(pk)
             preg = regions(ids, pl["launches"], k)
-            nl[k] = sum(pl["launches"].get(g, 0) for g in ("timed", "profiled"))
+            nl[k] = pl["launches"].get("timed", 0)
             for d in ids:
-                if preg[d] in ("timed", "profiled"):
+                for n, v in pk[d].items():
+                    if n in ("FETCH_SIZE", "WRITE_SIZE"):
+                        hbm_reg[preg[d]][n] += v / pl["launches"][preg[d]]
+                if preg[d] == "timed":
                     for n, v in pk[d].items():
                         ctr[k][n].append(v)
     mean = collections.defaultdict(float)  # summed over the frame kernels, per launch
@@ -175,6 +181,9 @@ def main():
         out["fetch_kib_per_launch"] = mean["FETCH_SIZE"]
         out["write_kib_per_launch"] = mean["WRITE_SIZE"]
         out["hbm_bytes_per_launch"] = int((2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024)
+        out["pmc_region"] = "timed"
+        out["hbm_bytes_per_launch_by_region"] = {g: int((2 * c.get("FETCH_SIZE", 0) + c.get("WRITE_SIZE", 0)) * 1024)
+                                                 for g, c in hbm_reg.items()}
     for n, key in (("SQ_INSTS_VALU", "sq_insts_valu_per_launch"), ("SQ_INSTS_SALU", "sq_insts_salu_per_launch"),
                    ("SQ_INSTS_VALU_FLOPS_FP64", "fp64_flops_per_launch"), ("SQ_INSTS_LDS", "sq_insts_lds_per_launch"),
                    ("SQ_INSTS_SMEM", "sq_insts_smem_per_launch"), ("SQ_WAVES", "sq_waves_per_launch"),
