@@ -3493,7 +3493,14 @@ int mirt_group_wait(mirt_group* g, void* stream) {
     const uint64_t used = std::min<uint64_t>(g->nb, g->HB);
     for (uint64_t b = 0; b < used; ++b) {
         if (stream) {
-            HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[b], 0));
+            // a batch already complete needs no wait on the caller's stream (each wait is a
+            // barrier packet on the stream's queue; after a host wait on every batch, as the
+            // bench's finish does, all 16 were redundant)
+            const hipError_t q = hipEventQuery(g->ev_done[b]);
+            if (q != hipSuccess) {
+                (void)hipGetLastError();  // (hipErrorNotReady is not an error here)
+                HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, g->ev_done[b], 0));
+            }
         } else {
             if ((r = group_wait_event(g, g->ev_done[b], "mirt_group_wait")) != MIRT_OK)
                 return group_timed_out(g, (uint32_t)b, r);
