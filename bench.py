@@ -579,14 +579,17 @@ def main():
 
     def finish():
         """The enqueued frames are done (gathers, unpacks and D2H included): a host wait on
-        the group's completion events first (hipEventSynchronize, or within the group's
-        deadline at N > 1), then torch's stream waits for them.  Waiting on the events
-        before torch.cuda.synchronize() keeps the runtime's blocking device-wide wait, which
-        returned ~120 us after the last kernel ended (rocprofv3 HIP trace),
-        out of the measured time; the synchronize that follows still brackets the steps."""
+        the group's completion events (hipEventSynchronize, or within the group's deadline at
+        N > 1); the torch.cuda.synchronize() that follows brackets the steps.  Waiting on the
+        events first keeps the runtime's blocking device-wide wait, which had returned ~120 us
+        after the last kernel ended (rocprofv3 HIP trace), out of the measured
+        time.  The torch.distributed sharder: torch's stream waits for its streams."""
         if isinstance(sh, NativeFrameGroup):
+            # the host wait covers every batch, gathers included: torch's stream has nothing
+            # left to wait for (a flush here only cost ~20-40 us of host time, DESIGN.md §6)
             sh.wait()
-        sh.flush()
+        else:
+            sh.flush()
 
     # launches per region (the key that partitions the rocprofv3 kernel trace of this command)
     launches = {}
