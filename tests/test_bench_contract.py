@@ -7,8 +7,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# round 6, final build (profiles/r06h_*): every line ran after its command's profile was committed
-TAG = "r06h"
+# round 6, final build (profiles/r06i_*): every line ran after its command's profile was committed
+TAG = "r06i"
 DRIVER = f"profiles/{TAG}_bench_driver_1.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
 PROFILED = [DRIVER] + [f"profiles/{TAG}_bench_{k}.log" for k in ("driver_2", "driver_3", "orbit", "lights", "config3",
                                                                   "config3ns", "config4")]
