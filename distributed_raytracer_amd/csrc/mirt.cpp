@@ -2879,7 +2879,16 @@ int mirt_group_create(mirt_ctx* c, const uint8_t* unique_id, int rank, int world
     // for the copy stream let each frame's D2H run beside the next frames' traces
     const char* dc = getenv("MIRT_D2H_CUS");
     g->d2h_cus = dc ? std::min(std::max(atoi(dc), 0), c->cus / 2) : 0;
-    for (uint32_t j = 0; j < inflight; ++j) HIP_TRY(stream_with_queue(c->cus, &g->streams[j], 0, c->cus - g->d2h_cus));
+    // the frame streams: each with a hardware queue of its own (a CU-masked stream), so frames in
+    // flight run concurrently; MIRT_PLAIN_STREAMS=1 (measurement): plain streams, which share the
+    // runtime's hardware queues
+    static const bool plain = getenv("MIRT_PLAIN_STREAMS") && atoi(getenv("MIRT_PLAIN_STREAMS"));
+    for (uint32_t j = 0; j < inflight; ++j) {
+        if (plain && !g->d2h_cus)
+            HIP_TRY(hipStreamCreateWithFlags(&g->streams[j], hipStreamNonBlocking));
+        else
+            HIP_TRY(stream_with_queue(c->cus, &g->streams[j], 0, c->cus - g->d2h_cus));
+    }
     for (uint32_t j = 0; j < ring; ++j) {
         HIP_TRY(hipEventCreateWithFlags(&g->ev_traced[j], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_gathered[j], hipEventDisableTiming));
