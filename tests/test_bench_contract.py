@@ -136,3 +136,17 @@ def test_box_lines():
         assert d["unit"] == "Mrays/s" and d["parity"]["bit_exact"] is True
         assert abs(d["value"] - d["rays_per_frame"] / d["ms_per_step"] / 1e3) / d["value"] < 2e-3
         assert d["config"]["box_entries"] in (1, 8)
+
+
+def test_in_tree_library_is_the_profiled_build():
+    """The library in the tree (built by __graft_entry__.build() from these sources) has the build
+    id of the committed profiles the driver's line cites: otherwise a round-end bench of this
+    tree could only report the algorithmic figure."""
+    import ctypes
+    so = os.path.join(ROOT, "distributed_raytracer_amd", "libmirt.so")
+    if not os.path.exists(so):
+        pytest.skip("libmirt.so not built")
+    lib = ctypes.CDLL(so)
+    lib.mirt_build_id.restype = ctypes.c_char_p
+    prof = json.load(open(os.path.join(ROOT, _line(DRIVER)["roofline"]["source"])))
+    assert lib.mirt_build_id().decode() == prof["build_id"] == _line(DRIVER)["build_id"]
