@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAG = "r06i"
 DRIVER = f"profiles/{TAG}_bench_driver_1.log"   # python3 bench.py --gpus 1 --steps 20 --warmup 5
 PROFILED = [DRIVER] + [f"profiles/{TAG}_bench_{k}.log" for k in ("driver_2", "driver_3", "orbit", "lights", "config3",
-                                                                  "config3ns", "config4")]
+                                                                  "config3ns", "config4", "brute")]
 UNPROFILED = [f"profiles/{TAG}_bench_{k}.log" for k in ("bench500", "orbit500")]  # 500 frames: no PMC of that shape
 LINES = PROFILED + UNPROFILED
 
